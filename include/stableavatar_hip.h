@@ -1,0 +1,97 @@
+/* C ABI of libstableavatar_hip.so — the MI355X (gfx950) kernels of the StableAvatar hot path
+ * (Wan-2.1 1.3B DiT denoise loop + 3-D causal VAE decode).
+ *
+ * Conventions:
+ *  - plain device pointers, element strides, sizes; no framework types cross the ABI;
+ *  - every call is asynchronous on the caller's HIP stream (`stream` = hipStream_t, may be NULL);
+ *  - the library never allocates; scratch comes from the caller;
+ *  - return 0 on success, 1 on a rejected argument, 2000 + hipError_t on a launch failure;
+ *    nothing throws across the ABI.  bf16 = IEEE bfloat16 bit pattern (uint16 storage).
+ *
+ * Each entry point names the reference interface it replaces (paths under the reference repo).
+ */
+#ifndef STABLEAVATAR_HIP_H
+#define STABLEAVATAR_HIP_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Epilogue codes for sa_gemm_bf16 */
+enum {
+  SA_EPI_BF16 = 0,          /* C(bf16) = A·W^T + bias                                    */
+  SA_EPI_GELU_TANH_BF16 = 1,/* C(bf16) = gelu_tanh(A·W^T + bias)   (nn.GELU('tanh'))       */
+  SA_EPI_F32 = 2,           /* C(f32)  = A·W^T + bias                                    */
+  SA_EPI_RES_F32 = 3,       /* C(f32)  = R + (A·W^T + bias) * gate[row / rows_per_batch] */
+  SA_EPI_GELU_ERF_BF16 = 4, /* C(bf16) = gelu_erf(A·W^T + bias)    (nn.GELU())           */
+  SA_EPI_SILU_F32 = 5       /* C(f32)  = silu(A·W^T + bias)                              */
+};
+
+/* nn.Linear on bf16 activations (every Linear of wan/models/wan_fantasy_transformer3d_1B.py
+ * :376-379,523-524,550-554,577-578,644-646,832-838,710 and
+ * wan/models/vocal_projector_fantasy_1B.py:238-241,313-316,374,393).
+ * C[b][M,N] = epi(A[b][M,K] · W[b][N,K]^T).  K % 64 == 0, lda/ldw % 8 == 0, A/W 16-B aligned. */
+int sa_gemm_bf16(const void* A, int64_t lda, int64_t strideA, const void* W, int64_t ldw, int64_t strideW,
+                 const float* bias, void* C, int64_t ldc, int64_t strideC, int M, int N, int K, int batch,
+                 int epilogue, const float* residual, int64_t ldr, int64_t strideR, const float* gate,
+                 int64_t gate_bstride, int rows_per_batch, void* stream);
+
+/* attention(q,k,v,...) of wan/models/wan_fantasy_transformer3d_1B.py:158-207 (SDPA path, no mask,
+ * q_lens/k_lens ignored) for head_dim 128.  Rows of q/k/v/o are flat [rows, stride] bf16 matrices,
+ * head h at column h*head_dim.  segs = device int32 [nseg][4] = {q_row0, q_len, kv_row0, kv_len}:
+ * every query row of a segment attends to the kv_len rows starting at kv_row0 (this expresses the
+ * batch dimension and the per-frame vocal grouping of :575-586).  accumulate != 0 adds into o. */
+int sa_attn_fwd(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg, int max_q_len,
+                int heads, int head_dim, int64_t q_stride, int64_t k_stride, int64_t v_stride, int64_t o_stride,
+                float scale, int accumulate, void* stream);
+
+/* LayerNorm (+affine) (+AdaLN modulate  y*(1+scale[b])+shift[b]) (+gated residual x + y*gate[b]):
+ * WanLayerNorm 1B:345-355 and its call sites :675,684,687,721-722; MLPProj LayerNorms :731-734;
+ * vocal_projector_fantasy_1B.py:345-347,352,354,386,398.  in/out dtype: 0 = f32, 1 = bf16. */
+int sa_layernorm_mod(const void* x, int64_t ldx, int in_dtype, void* out, int64_t ldo, int out_dtype,
+                     const float* weight, const float* bias, const float* shift, const float* scale,
+                     int64_t mod_bstride, const float* gate, int rows_per_batch, int M, int C, float eps,
+                     void* stream);
+
+/* WanRMSNorm over the full width on q (and k) + rope_apply (1B:295-342, :395-396, :403-404) in place.
+ * rope = fp32 [1024][head_dim/2][2] (cos, sin) table or NULL (no rotation); token index
+ * t = tok_offset + row % rows_per_batch; t >= F*H*W is not rotated (padding, 1B:319). */
+int sa_qk_rmsnorm_rope(void* x, int64_t ldx, int q_col, int k_col, const float* wq, const float* wk, int M, int C,
+                       int head_dim, float eps, const float* rope, int rows_per_batch, int tok_offset, int F, int H,
+                       int W, int n_frame_pairs, int n_height_pairs, void* stream);
+
+/* cat(x, y, dim=channels) -> Conv3d(k=s=(1,2,2)) im2col (1B:972-976); out = bf16 [B, Lpad, Kpad]. */
+int sa_patch_im2col(const void* x, int64_t xb, int64_t xc, int64_t xf, int xcn, const void* y, int64_t yb, int64_t yc,
+                    int64_t yf, int ycn, int B, int F, int H, int W, void* out, int Kpad, int Lpad, void* stream);
+
+/* unpatchify (1B:1161-1184): bf16 [B, Lpad, ld_in] -> [B, C, F, H, W] (out_dtype 0 f32 / 1 bf16). */
+int sa_unpatchify(const void* in, int64_t ld_in, int Lpad, int B, int C, int F, int H, int W, void* out,
+                  int out_dtype, void* stream);
+
+/* sinusoidal_embedding_1d (1B:210-220), fp64 math, fp32 out [B, dim]. */
+int sa_timestep_embed(const float* t, int B, int dim, float* out, void* stream);
+
+/* fp32 Linear for <= 8 rows (time MLPs under fp32 autocast, 1B:986-990); act: 0 none, 1 SiLU. */
+int sa_small_linear_f32(const float* in, int64_t ldi, int M, const void* W, int64_t ldw, const float* bias,
+                        float* out, int64_t ldo, int N, int K, int act_in, int act_out, void* stream);
+
+/* out[l,b,j,c] = mod[l,j,c] + e[b,j,c]   ((self.modulation + e).chunk(6), 1B:672, :721) */
+int sa_mod_add(const float* mod, const float* e, float* out, int L, int B, int J, int C, void* stream);
+
+/* CFG combine + FlowMatchEulerDiscreteScheduler.step + overlap blend + scatter of one window
+ * (wan/pipeline/wan_inference_long_pipeline.py:751-779). */
+int sa_flow_step(const void* latents_all, void* pred_all, const void* noise, int R, int C, int T, int Fw,
+                 int64_t HW, int start, float dsigma, float audio_scale, float text_scale, int overlap, int prev_end,
+                 const float* weights, int blend, void* stream);
+
+/* out[r] = idx[r] >= 0 ? in[idx[r]] : 0  (split_tensor_with_padding, vocal_projector_fantasy.py:81-131) */
+int sa_gather_rows(const void* in, int64_t in_row_bytes, const int32_t* idx, int nrows, void* out,
+                   int64_t out_row_bytes, int64_t row_bytes, void* stream);
+
+int sa_fill_f32(float* p, int64_t n, float v, void* stream);
+int sa_cast_f32_bf16(const float* in, void* out, int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

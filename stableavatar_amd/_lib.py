@@ -1,0 +1,68 @@
+"""ctypes binding of libstableavatar_hip.so (the C ABI declared in include/stableavatar_hip.h).
+
+The product path has no fallback: if the library is missing or a symbol is absent, `lib()` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("SA_LIB", PKG / "libstableavatar_hip.so"))
+HEADER = PKG.parent / "include" / "stableavatar_hip.h"
+
+# argument codes: p = pointer, i = int32, l = int64, f = float
+SIGNATURES = {
+    "sa_gemm_bf16": "pllpllpplliiiiipllplip",
+    "sa_attn_fwd": "pppppiiiillllfip",
+    "sa_layernorm_mod": "pliplipppplpiiifp",
+    "sa_qk_rmsnorm_rope": "pliippiiifpiiiiiiip",
+    "sa_patch_im2col": "plllipllliiiiipiip",
+    "sa_unpatchify": "pliiiiiipip",
+    "sa_timestep_embed": "piipp",
+    "sa_small_linear_f32": "pliplppliiiip",
+    "sa_mod_add": "pppiiiip",
+    "sa_flow_step": "pppiiiilifffiipip",
+    "sa_gather_rows": "plpipllp",
+    "sa_fill_f32": "plfp",
+    "sa_cast_f32_bf16": "pplp",
+}
+_CT = {"p": ctypes.c_void_p, "i": ctypes.c_int32, "l": ctypes.c_int64, "f": ctypes.c_float}
+
+_lib = None
+
+
+def header_symbols() -> list[str]:
+    """Function names declared in include/stableavatar_hip.h."""
+    txt = HEADER.read_text()
+    return sorted(set(re.findall(r"^\s*int\s+(sa_\w+)\s*\(", txt, flags=re.M)))
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise RuntimeError(f"libstableavatar_hip.so not built ({LIB_PATH}); run __graft_entry__.build()")
+    L = ctypes.CDLL(str(LIB_PATH))
+    for name in header_symbols():
+        fn = getattr(L, name)  # AttributeError = missing export -> loud failure
+        sig = SIGNATURES[name]
+        fn.argtypes = [_CT[c] for c in sig]
+        fn.restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+class KernelError(RuntimeError):
+    pass
+
+
+def call(name: str, *args):
+    fn = getattr(lib(), name)
+    rc = fn(*args)
+    if rc != 0:
+        kind = "bad argument" if rc == 1 else f"launch failure (hipError {rc - 2000})"
+        raise KernelError(f"{name}: {kind} (rc={rc})")

@@ -1,0 +1,206 @@
+// Flash-attention forward, bf16 in / fp32 softmax+accumulate / bf16 out, head_dim 128, no mask
+// (the reference's SDPA path: wan_fantasy_transformer3d_1B.py:158-207 with q_lens/k_lens ignored,
+// which it warns about at :190-193).  One kernel serves every attention site of the DiT:
+//   * self-attention            (1B:402-407)   segments = batch rows, Lq = Lk = seq_len
+//   * text / image cross-attn   (1B:556-570)   Lk = 512 / 257 (tail key block masked)
+//   * per-frame vocal cross-attn(1B:575-586)   segments = (batch, latent frame), Lk = 17
+// Segments come from a device table {q_row0, q_len, kv_row0, kv_len}; rows index flat
+// [rows, stride] bf16 matrices with head h at column h*128, so Q/K/V are read straight out of
+// the fused QKV GEMM output (no transposes).  ACCUMULATE adds into an existing bf16 output,
+// which is how the three cross-attention terms are summed (1B:603).
+//
+// Structure (cdna_hip_programming.md App. B "Fused attention prefill"): 8 waves x 32 query rows,
+// KV blocks of 64 keys staged by global_load_lds into a 2-deep LDS ring (XOR-swizzled 256-B rows).
+// Swapped product S^T = K·Q^T (mfma_f32_32x32x16_bf16) puts one query per lane, so the online
+// softmax is lane-local; P^T is fed back as the B operand straight from the accumulator and V^T
+// comes from ds_read_b64_tr_b16, giving O^T with the query on the lane (rescale is per lane).
+#include "common.h"
+
+namespace {
+
+struct AttnArgs {
+  const bf16* q; const bf16* k; const bf16* v; bf16* o;
+  const int* segs;
+  long qs, ks, vs, os;
+  float c;  // softmax scale * log2(e)
+  int accumulate;
+};
+
+constexpr int D = 128;
+constexpr int WAVES = 8;
+constexpr int QB = WAVES * 32;
+constexpr int KVB = 64;
+constexpr int TILE_BYTES = KVB * D * 2;      // 16 KB
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;  // K + V
+constexpr int LDS_BYTES = 2 * STAGE_BYTES;   // 64 KB
+
+// 16-byte chunk swizzle for 256-B rows: conflict-free for both row (ds_read_b128) and
+// transposed (ds_read_b64_tr_b16) reads (cdna_hip_programming.md T10 form (b))
+__device__ __forceinline__ int gsw(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+__global__ __launch_bounds__(512) void attn_fwd_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int* sg = a.segs + blockIdx.z * 4;
+  const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
+  const int qb = blockIdx.x, h = blockIdx.y;
+  if (qb * QB >= q_len || kv_len <= 0) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5;
+
+  const int qi = qb * QB + wave * 32 + (lane & 31);
+  const int qc = min(qi, q_len - 1);
+  const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * hi;
+  bf16x8 qf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
+
+  // staging: each wave moves 2 x 1-KB pieces (4 rows each) of K and of V per block
+  const bf16* kbase = a.k + h * D;
+  const bf16* vbase = a.v + h * D;
+  int srow[2], schunk[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    srow[i] = (wave * 2 + i) * 4 + (lane >> 4);
+    schunk[i] = (lane & 15) ^ gsw(srow[i]);
+  }
+  auto stage = [&](int kb, int buf) {
+    char* base = smem + buf * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long key = kv_row0 + min(kb * KVB + srow[i], kv_len - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(kbase + key * a.ks + schunk[i] * 8),
+                                       LDS_PTR(base + (wave * 2 + i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(vbase + key * a.vs + schunk[i] * 8),
+                                       LDS_PTR(base + TILE_BYTES + (wave * 2 + i) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x16 O[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) O[db][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+
+  const int nkb = (kv_len + KVB - 1) / KVB;
+  stage(0, 0);
+  for (int kb = 0; kb < nkb; ++kb) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kb + 1 < nkb) stage(kb + 1, (kb + 1) & 1);
+    const char* Ks = smem + (kb & 1) * STAGE_BYTES;
+    const char* Vs = Ks + TILE_BYTES;
+
+    // S^T[key][query] = K · Q^T
+    f32x16 S[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) S[t][r] = 0.f;
+      const int row = t * 32 + (lane & 31);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int ch = 2 * s + hi;
+        const bf16x8 kf = *(const bf16x8*)(Ks + row * 256 + ((ch ^ gsw(row)) << 4));
+        S[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], S[t], 0, 0, 0);
+      }
+    }
+    if (kb * KVB + KVB > kv_len) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kb * KVB + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+          if (key >= kv_len) S[t][r] = -INFINITY;
+        }
+    }
+    float mx = S[0][0];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[t][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx * a.c);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+    float ps = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(S[t][r], a.c, -m_new));
+        S[t][r] = p;
+        ps += p;
+      }
+    l_run = fmaf(l_run, alpha, ps);
+    m_run = m_new;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) O[db][r] *= alpha;
+
+    // O^T[d][query] += V^T · P^T
+    const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[j] = f2bf(S[t][8 * s + j]);
+        const int r0 = t * 32 + 16 * s + 4 * hi + q4;
+        const int r1 = r0 + 8;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          const int col = db * 32 + 16 * ((lane >> 4) & 1) + 4 * p4;
+          const int off0 = r0 * 256 + (((col >> 3) ^ gsw(r0)) << 4) + 8 * ((col >> 2) & 1);
+          const int off1 = r1 * 256 + (((col >> 3) ^ gsw(r1)) << 4) + 8 * ((col >> 2) & 1);
+          const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(Vs + off0));
+          const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(Vs + off1));
+          const bf16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+          O[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb, O[db], 0, 0, 0);
+        }
+      }
+  }
+
+  const float lt = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = 1.0f / lt;
+  if (qi < q_len) {
+    bf16* op = a.o + (long)(q_row0 + qi) * a.os + h * D;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const int d0 = db * 32 + 8 * r4 + 4 * hi;
+        float v0 = O[db][4 * r4 + 0] * inv, v1 = O[db][4 * r4 + 1] * inv;
+        float v2 = O[db][4 * r4 + 2] * inv, v3 = O[db][4 * r4 + 3] * inv;
+        if (a.accumulate) {
+          const bf16x4 old = *(const bf16x4*)(op + d0);
+          v0 += bf2f(old[0]); v1 += bf2f(old[1]); v2 += bf2f(old[2]); v3 += bf2f(old[3]);
+        }
+        *(bf16x4*)(op + d0) = (bf16x4){f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
+      }
+  }
+}
+
+}  // namespace
+
+extern "C" int sa_attn_fwd(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
+                           int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride,
+                           int64_t v_stride, int64_t o_stride, float scale, int accumulate, void* stream) {
+  if (!q || !k || !v || !o || !segs || nseg <= 0 || max_q_len <= 0 || heads <= 0) return SA_ERR_ARG;
+  if (head_dim != D) return SA_ERR_ARG;
+  if ((q_stride | k_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
+  if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)o)) & 15) return SA_ERR_ARG;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    attr = true;
+  }
+  AttnArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, segs,
+             q_stride, k_stride, v_stride, o_stride, scale * 1.4426950408889634f, accumulate};
+  dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
+  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+  SA_LAUNCH_CHECK();
+  return SA_OK;
+}

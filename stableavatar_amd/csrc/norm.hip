@@ -1,0 +1,206 @@
+// Row normalisations of the DiT / vocal projector, one wave per row, fp32 math:
+//  * sa_layernorm_mod: LayerNorm (biased var, eps) -> optional affine -> optional AdaLN
+//    modulate  y*(1+scale[b]) + shift[b]                      (1B:345-355,675,684,687,721-722;
+//    vocal_projector_fantasy_1B.py:345,352,354,386,398; MLPProj 1B:731-734)
+//    and an optional gated residual  out = x + y*gate[b]       (vocal_projector_fantasy_1B.py:345-347)
+//  * sa_qk_rmsnorm_rope: WanRMSNorm over the FULL model dim on q and k (1B:326-342,395-396),
+//    then the 3-D complex RoPE (1B:295-323) with fp64-derived fp32 (cos,sin) tables; tokens past
+//    f*h*w (padding) are left unrotated (1B:319).  In place on the fused QKV GEMM output.
+#include "common.h"
+
+namespace {
+
+template <typename TI>
+__device__ __forceinline__ void load8(const TI* p, float* v);
+template <>
+__device__ __forceinline__ void load8<float>(const float* p, float* v) {
+  f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+template <>
+__device__ __forceinline__ void load8<bf16>(const bf16* p, float* v) {
+  bf16x8 a = *(const bf16x8*)p;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = bf2f(a[j]);
+}
+template <typename TO>
+__device__ __forceinline__ void store8(TO* p, const float* v);
+template <>
+__device__ __forceinline__ void store8<float>(float* p, const float* v) {
+  *(f32x4*)p = (f32x4){v[0], v[1], v[2], v[3]};
+  *(f32x4*)(p + 4) = (f32x4){v[4], v[5], v[6], v[7]};
+}
+template <>
+__device__ __forceinline__ void store8<bf16>(bf16* p, const float* v) {
+  bf16x8 a;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = f2bf(v[j]);
+  *(bf16x8*)p = a;
+}
+
+struct LnArgs {
+  const void* x; long ldx;
+  void* out; long ldo;
+  const float* w; const float* b;         // affine (optional)
+  const float* shift; const float* scale; long mod_bstride;  // AdaLN (optional)
+  const float* gate;                       // gated residual (optional, f32 out only)
+  int rows_per_batch;
+  int M, C;
+  float eps;
+};
+
+constexpr int MAXV = 8;  // up to 8 chunks of 8 per lane -> C <= 4096
+
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void layernorm_mod_kernel(LnArgs a) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= a.M) return;
+  const TI* x = (const TI*)a.x + (long)row * a.ldx;
+  const int nch = (a.C + 511) / 512;
+  float v[MAXV][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i)
+    if (i < nch && i * 512 + lane * 8 < a.C) {
+      load8<TI>(x + i * 512 + lane * 8, v[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[i][j];
+    }
+  const float mean = wave_sum(s) / a.C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i)
+    if (i < nch && i * 512 + lane * 8 < a.C) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float d = v[i][j] - mean; q += d * d; }
+    }
+  const float rstd = rsqrtf(wave_sum(q) / a.C + a.eps);
+  const long bo = (long)(row / a.rows_per_batch) * a.mod_bstride;
+  TO* out = (TO*)a.out + (long)row * a.ldo;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i)
+    if (i < nch && i * 512 + lane * 8 < a.C) {
+      const int c0 = i * 512 + lane * 8;
+      float y[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float t = (v[i][j] - mean) * rstd;
+        if (a.w) t = t * a.w[c0 + j] + (a.b ? a.b[c0 + j] : 0.f);
+        if (a.scale) t = t * (1.f + a.scale[bo + c0 + j]) + a.shift[bo + c0 + j];
+        if (a.gate) t = v[i][j] + t * a.gate[bo + c0 + j];
+        y[j] = t;
+      }
+      store8<TO>(out + c0, y);
+    }
+}
+
+struct QkArgs {
+  bf16* x; long ldx;
+  int q_col, k_col;  // column offsets of q and k inside a row (k_col < 0: q only)
+  const float* wq; const float* wk;
+  int M, C, head_dim;
+  float eps;
+  const float* rope;  // [1024][head_dim/2][2] (cos, sin) or null
+  int rows_per_batch, tok_offset, F, H, W;  // token t = tok_offset + row % rows_per_batch
+  int nf, nh;         // pairs assigned to frame / height axes (rest: width)
+};
+
+__device__ __forceinline__ void rms_rope_one(bf16* p, const float* w, const QkArgs& a, int lane, int fi, int hi_,
+                                             int wi, bool rot) {
+  const int nch = (a.C + 511) / 512;
+  float v[MAXV][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i)
+    if (i < nch && i * 512 + lane * 8 < a.C) {
+      load8<bf16>(p + i * 512 + lane * 8, v[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[i][j] * v[i][j];
+    }
+  const float r = rsqrtf(wave_sum(s) / a.C + a.eps);
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i)
+    if (i < nch && i * 512 + lane * 8 < a.C) {
+      const int c0 = i * 512 + lane * 8;
+      float y[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y[j] = v[i][j] * r * w[c0 + j];
+      if (rot) {
+        const int d0 = c0 % a.head_dim;
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          const int pi = (d0 + j) >> 1;
+          const int pos = pi < a.nf ? fi : (pi < a.nf + a.nh ? hi_ : wi);
+          const float cs = a.rope[(pos * (a.head_dim / 2) + pi) * 2 + 0];
+          const float sn = a.rope[(pos * (a.head_dim / 2) + pi) * 2 + 1];
+          const float re = y[j], im = y[j + 1];
+          y[j] = re * cs - im * sn;
+          y[j + 1] = re * sn + im * cs;
+        }
+      }
+      store8<bf16>(p + c0, y);
+    }
+}
+
+__global__ __launch_bounds__(256) void qk_rmsnorm_rope_kernel(QkArgs a) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= a.M) return;
+  bool rot = false;
+  int fi = 0, hi_ = 0, wi = 0;
+  if (a.rope) {
+    const int t = a.tok_offset + row % a.rows_per_batch;
+    if (t < a.F * a.H * a.W) {
+      rot = true;
+      fi = t / (a.H * a.W);
+      hi_ = (t / a.W) % a.H;
+      wi = t % a.W;
+    }
+  }
+  bf16* base = a.x + (long)row * a.ldx;
+  rms_rope_one(base + a.q_col, a.wq, a, lane, fi, hi_, wi, rot);
+  if (a.k_col >= 0) rms_rope_one(base + a.k_col, a.wk, a, lane, fi, hi_, wi, rot);
+}
+
+template <typename TI, typename TO>
+int launch_ln(const LnArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((layernorm_mod_kernel<TI, TO>), dim3((a.M + 3) / 4), dim3(256), 0, st, a);
+  SA_LAUNCH_CHECK();
+  return SA_OK;
+}
+
+}  // namespace
+
+// in_dtype / out_dtype: 0 = fp32, 1 = bf16
+extern "C" int sa_layernorm_mod(const void* x, int64_t ldx, int in_dtype, void* out, int64_t ldo, int out_dtype,
+                                const float* weight, const float* bias, const float* shift, const float* scale,
+                                int64_t mod_bstride, const float* gate, int rows_per_batch, int M, int C, float eps,
+                                void* stream) {
+  if (!x || !out || M <= 0 || C <= 0 || C % 8 || C > 512 * MAXV || ldx % 8 || ldo % 8) return SA_ERR_ARG;
+  if ((shift == nullptr) != (scale == nullptr)) return SA_ERR_ARG;
+  if ((scale || gate) && rows_per_batch <= 0) return SA_ERR_ARG;
+  if (gate && (out_dtype != 0 || !scale)) return SA_ERR_ARG;
+  LnArgs a{x, ldx, out, ldo, weight, bias, shift, scale, mod_bstride, gate, rows_per_batch > 0 ? rows_per_batch : 1,
+           M, C, eps};
+  hipStream_t st = (hipStream_t)stream;
+  if (in_dtype == 0 && out_dtype == 1) return launch_ln<float, bf16>(a, st);
+  if (in_dtype == 0 && out_dtype == 0) return launch_ln<float, float>(a, st);
+  if (in_dtype == 1 && out_dtype == 1) return launch_ln<bf16, bf16>(a, st);
+  if (in_dtype == 1 && out_dtype == 0) return launch_ln<bf16, float>(a, st);
+  return SA_ERR_ARG;
+}
+
+extern "C" int sa_qk_rmsnorm_rope(void* x, int64_t ldx, int q_col, int k_col, const float* wq, const float* wk, int M,
+                                  int C, int head_dim, float eps, const float* rope, int rows_per_batch,
+                                  int tok_offset, int F, int H, int W, int n_frame_pairs, int n_height_pairs,
+                                  void* stream) {
+  if (!x || !wq || M <= 0 || C <= 0 || C % 8 || C > 512 * MAXV || ldx % 8) return SA_ERR_ARG;
+  if (k_col >= 0 && !wk) return SA_ERR_ARG;
+  if (rope && (rows_per_batch <= 0 || head_dim % 8 || F <= 0 || H <= 0 || W <= 0)) return SA_ERR_ARG;
+  QkArgs a{(bf16*)x, ldx, q_col, k_col, wq, wk, M, C, head_dim, eps, rope, rows_per_batch > 0 ? rows_per_batch : 1,
+           tok_offset, F, H, W, n_frame_pairs, n_height_pairs};
+  hipLaunchKernelGGL(qk_rmsnorm_rope_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
+  SA_LAUNCH_CHECK();
+  return SA_OK;
+}

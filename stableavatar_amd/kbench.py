@@ -1,0 +1,75 @@
+"""Kernel micro-benchmarks at the config-2 (512x512x81f, CFG batch 3) shapes of the DiT.
+python -m stableavatar_amd.kbench  -> one JSON line per kernel with TFLOP/s (random data)."""
+from __future__ import annotations
+
+import json
+import sys
+
+import torch
+
+from . import ops
+
+
+def _time(fn, iters=10, warmup=2):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main(which=("gemm", "attn")):
+    dev = "cuda"
+    torch.manual_seed(0)
+    M = 3 * 21504
+    res = []
+    if "gemm" in which:
+        for (N, K, epi, name) in [(4608, 1536, ops.EPI_BF16, "qkv"), (1536, 1536, ops.EPI_RES_F32, "o_proj"),
+                                  (8960, 1536, ops.EPI_GELU_TANH_BF16, "ffn_up"),
+                                  (1536, 8960, ops.EPI_RES_F32, "ffn_down")]:
+            x = torch.randn(M, K, device=dev).bfloat16()
+            w = (torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
+            b = torch.randn(N, device=dev)
+            out = torch.empty(M, N, device=dev, dtype=torch.float32 if epi == ops.EPI_RES_F32 else torch.bfloat16)
+            gate = torch.randn(3, N, device=dev)
+            if epi == ops.EPI_RES_F32:
+                fn = lambda: ops.linear(x, w, b, epi, out=out, residual=out, gate=gate, rows_per_batch=21504)
+            else:
+                fn = lambda: ops.linear(x, w, b, epi, out=out)
+            ms = _time(fn)
+            ms_ref = _time(lambda: torch.nn.functional.linear(x, w))
+            fl = 2.0 * M * N * K
+            res.append({"kernel": f"gemm_{name}", "M": M, "N": N, "K": K, "ms": round(ms, 4),
+                        "tflops": round(fl / ms / 1e9, 1), "torch_ms": round(ms_ref, 4),
+                        "torch_tflops": round(fl / ms_ref / 1e9, 1)})
+            print(json.dumps(res[-1]), flush=True)
+            del x, w, out
+    if "attn" in which:
+        L, H, D = 21504, 12, 128
+        qkv = torch.randn(3 * L, 3 * H * D, device=dev).bfloat16()
+        o = torch.empty(3 * L, H * D, device=dev, dtype=torch.bfloat16)
+        segs = torch.tensor([[b * L, L, b * L, L] for b in range(3)], dtype=torch.int32, device=dev)
+        q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+        fn = lambda: ops.attention(q, k, v, o, segs, 3, L, H)
+        ms = _time(fn, iters=5)
+        fl = 4.0 * 3 * H * L * L * D
+        qh = q.view(3, L, H, D).transpose(1, 2)
+        kh = k.view(3, L, H, D).transpose(1, 2)
+        vh = v.view(3, L, H, D).transpose(1, 2)
+        try:
+            ms_ref = _time(lambda: torch.nn.functional.scaled_dot_product_attention(qh, kh, vh), iters=3)
+        except Exception:  # noqa: BLE001
+            ms_ref = float("nan")
+        res.append({"kernel": "attn_self", "L": L, "ms": round(ms, 3), "tflops": round(fl / ms / 1e9, 1),
+                    "torch_sdpa_ms": round(ms_ref, 3), "torch_tflops": round(fl / ms_ref / 1e9, 1)})
+        print(json.dumps(res[-1]), flush=True)
+    return res
+
+
+if __name__ == "__main__":
+    main(tuple(sys.argv[1:]) or ("gemm", "attn"))

@@ -1,0 +1,177 @@
+"""Tensor-level wrappers over the C ABI.  Every function launches HIP kernels from
+libstableavatar_hip.so on the current torch stream; there is no CPU / eager fallback.
+Tensors must already live on the GPU with the dtype/layout documented per function.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._lib import call
+
+EPI_BF16, EPI_GELU_TANH_BF16, EPI_F32, EPI_RES_F32, EPI_GELU_ERF_BF16, EPI_SILU_F32 = range(6)
+F32, BF16 = 0, 1
+
+
+def _p(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dt(t):
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise TypeError(f"unsupported dtype {t.dtype}")
+
+
+def _check(t, dtype, name):
+    if not t.is_cuda:
+        raise RuntimeError(f"{name}: expected a GPU tensor")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+
+
+def linear(x, weight, bias=None, epilogue=EPI_BF16, out=None, residual=None, gate=None, rows_per_batch=0):
+    """y = epi(x @ weight^T + bias).  x: bf16 [M, K] (row stride may exceed K), weight: bf16 [N, K].
+    EPI_RES_F32: out(f32) = residual + y * gate[row // rows_per_batch] (gate f32 [B, N] view)."""
+    _check(x, torch.bfloat16, "linear.x")
+    _check(weight, torch.bfloat16, "linear.weight")
+    M, K = x.shape
+    N = weight.shape[0]
+    assert weight.shape[1] == K and x.stride(1) == 1 and weight.stride(1) == 1
+    f32_out = epilogue in (EPI_F32, EPI_RES_F32, EPI_SILU_F32)
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=torch.float32 if f32_out else torch.bfloat16)
+    assert out.dtype == (torch.float32 if f32_out else torch.bfloat16) and out.stride(1) == 1
+    if bias is not None:
+        _check(bias, torch.float32, "linear.bias")
+    ldr = 0
+    gstride = 0
+    if epilogue == EPI_RES_F32:
+        assert residual is not None and residual.dtype == torch.float32
+        ldr = residual.stride(0)
+        if gate is not None:
+            assert gate.dtype == torch.float32 and gate.stride(-1) == 1
+            gstride = gate.stride(0)
+    call("sa_gemm_bf16", x.data_ptr(), x.stride(0), 0, weight.data_ptr(), weight.stride(0), 0, _p(bias),
+         out.data_ptr(), out.stride(0), 0, M, N, K, 1, epilogue, _p(residual), ldr, 0, _p(gate), gstride,
+         rows_per_batch, _stream())
+    return out
+
+
+def bmm_nt(a, b, out, epilogue=EPI_F32):
+    """out[z] = a[z] @ b[z]^T for 3-D bf16 a [Z, M, K], b [Z, N, K]."""
+    Z, M, K = a.shape
+    N = b.shape[1]
+    call("sa_gemm_bf16", a.data_ptr(), a.stride(1), a.stride(0), b.data_ptr(), b.stride(1), b.stride(0), 0,
+         out.data_ptr(), out.stride(1), out.stride(0), M, N, K, Z, epilogue, 0, 0, 0, 0, 0, 0, _stream())
+    return out
+
+
+def attention(q, k, v, out, segs, nseg, max_q_len, heads, head_dim=128, scale=None, accumulate=False):
+    """Flash attention over row-segment table `segs` (int32 [nseg,4] on device)."""
+    for t, n in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
+        _check(t, torch.bfloat16, f"attention.{n}")
+        assert t.stride(-1) == 1
+    assert segs.dtype == torch.int32 and segs.is_cuda
+    if scale is None:
+        scale = head_dim ** -0.5
+    call("sa_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), segs.data_ptr(), nseg, max_q_len,
+         heads, head_dim, q.stride(0), k.stride(0), v.stride(0), out.stride(0), float(scale), int(accumulate),
+         _stream())
+    return out
+
+
+def layernorm_mod(x, out, eps, weight=None, bias=None, shift=None, scale=None, gate=None, rows_per_batch=0):
+    """Row LayerNorm (+affine) (+y*(1+scale[b])+shift[b]) (+x+y*gate[b]).  x/out 2-D f32|bf16."""
+    M, C = x.shape
+    mstride = 0
+    if scale is not None:
+        mstride = scale.stride(0)
+        assert shift.stride(0) == mstride
+    call("sa_layernorm_mod", x.data_ptr(), x.stride(0), _dt(x), out.data_ptr(), out.stride(0), _dt(out), _p(weight),
+         _p(bias), _p(shift), _p(scale), mstride, _p(gate), rows_per_batch, M, C, float(eps), _stream())
+    return out
+
+
+def qk_rmsnorm_rope(x, q_col, k_col, wq, wk, C, eps, rope=None, rows_per_batch=0, tok_offset=0, grid=(1, 1, 1),
+                    head_dim=128, n_frame_pairs=0, n_height_pairs=0, M=None):
+    M = x.shape[0] if M is None else M
+    F, H, W = grid
+    call("sa_qk_rmsnorm_rope", x.data_ptr(), x.stride(0), q_col, k_col, wq.data_ptr(), _p(wk), M, C, head_dim,
+         float(eps), _p(rope), rows_per_batch, tok_offset, F, H, W, n_frame_pairs, n_height_pairs, _stream())
+    return x
+
+
+def patch_im2col(x, y, B, F, H, W, out, Kpad, Lpad, x_frame_offset=0, x_batch_broadcast=False):
+    """x: [Bx, Cx, Tx, H, W] bf16 (frames x_frame_offset.. used), y: [B, Cy, >=F, H, W] bf16."""
+    xc = x.stride(1)
+    xb = 0 if x_batch_broadcast else x.stride(0)
+    xf = x.stride(2)
+    xptr = x.data_ptr() + x_frame_offset * xf * x.element_size()
+    if y is not None:
+        yb, yc, yf, ycn, yptr = y.stride(0), y.stride(1), y.stride(2), y.shape[1], y.data_ptr()
+    else:
+        yb = yc = yf = ycn = yptr = 0
+    call("sa_patch_im2col", xptr, xb, xc, xf, x.shape[1], yptr, yb, yc, yf, ycn, B, F, H, W, out.data_ptr(), Kpad,
+         Lpad, _stream())
+    return out
+
+
+def unpatchify(head_out, Lpad, B, C, F, H, W, out):
+    call("sa_unpatchify", head_out.data_ptr(), head_out.stride(0), Lpad, B, C, F, H, W, out.data_ptr(), _dt(out),
+         _stream())
+    return out
+
+
+def timestep_embed(t, dim, out):
+    call("sa_timestep_embed", t.data_ptr(), t.shape[0], dim, out.data_ptr(), _stream())
+    return out
+
+
+def small_linear_f32(x, weight, bias, out, act_in=0, act_out=0):
+    M, K = x.shape
+    N = weight.shape[0]
+    call("sa_small_linear_f32", x.data_ptr(), x.stride(0), M, weight.data_ptr(), weight.stride(0), _p(bias),
+         out.data_ptr(), out.stride(0), N, K, act_in, act_out, _stream())
+    return out
+
+
+def mod_add(mod, e, out):
+    """out[l,b,j,c] = mod[l,j,c] + e[b,j,c]."""
+    L, J, C = mod.shape
+    B = e.shape[0]
+    call("sa_mod_add", mod.data_ptr(), e.data_ptr(), out.data_ptr(), L, B, J, C, _stream())
+    return out
+
+
+def flow_step(latents_all, pred_all, noise, start, dsigma, audio_scale, text_scale, overlap, prev_end, weights,
+              blend):
+    C, T = latents_all.shape[1], latents_all.shape[2]
+    R, Fw = noise.shape[0], noise.shape[2]
+    HW = noise.shape[3] * noise.shape[4]
+    call("sa_flow_step", latents_all.data_ptr(), pred_all.data_ptr(), noise.data_ptr(), R, C, T, Fw, HW, start,
+         float(dsigma), float(audio_scale), float(text_scale), overlap, prev_end, _p(weights), int(blend), _stream())
+
+
+def gather_rows(inp, idx, out):
+    row_bytes = inp.shape[-1] * inp.element_size()
+    call("sa_gather_rows", inp.data_ptr(), inp.stride(0) * inp.element_size(), idx.data_ptr(), idx.shape[0],
+         out.data_ptr(), out.stride(0) * out.element_size(), row_bytes, _stream())
+    return out
+
+
+def fill_(t, value):
+    assert t.dtype == torch.float32 and t.is_contiguous()
+    call("sa_fill_f32", t.data_ptr(), t.numel(), float(value), _stream())
+    return t
+
+
+def cast_bf16(x, out):
+    assert x.is_contiguous() and out.is_contiguous()
+    call("sa_cast_f32_bf16", x.data_ptr(), out.data_ptr(), x.numel(), _stream())
+    return out

@@ -1,0 +1,259 @@
+"""Per-kernel numerics of libstableavatar_hip.so against plain PyTorch fp32 references of the
+same op (floating-point kernels: tolerances stated per test).  Runs on the MI355X only."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+def rel(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.fixture(autouse=True)
+def _seed():
+    torch.manual_seed(0)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 520, 192), (512, 256, 64), (64512 // 16, 1536, 1536)])
+def test_gemm_epilogues(M, N, K):
+    from stableavatar_amd import ops
+    x = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device=dev)
+    ref = x.float() @ w.float().t() + b
+    y = ops.linear(x, w, b, ops.EPI_BF16)
+    assert rel(y, ref) < 1e-2
+    y = ops.linear(x, w, b, ops.EPI_F32)
+    assert rel(y, ref) < 2e-3
+    y = ops.linear(x, w, b, ops.EPI_GELU_TANH_BF16)
+    assert rel(y, torch.nn.functional.gelu(ref, approximate="tanh")) < 1e-2
+    y = ops.linear(x, w, b, ops.EPI_GELU_ERF_BF16)
+    assert rel(y, torch.nn.functional.gelu(ref)) < 1e-2
+    y = ops.linear(x, w, b, ops.EPI_SILU_F32)
+    assert rel(y, torch.nn.functional.silu(ref)) < 2e-3
+    # gated residual, 3 "batch rows" of the CFG batch
+    B = 3
+    rpb = (M + B - 1) // B
+    res = torch.randn(M, N, device=dev)
+    gate = torch.randn(B, N, device=dev)
+    g_rows = gate[torch.arange(M, device=dev) // rpb]
+    out = res.clone()
+    ops.linear(x, w, b, ops.EPI_RES_F32, out=out, residual=out, gate=gate, rows_per_batch=rpb)
+    assert rel(out, res + ref * g_rows) < 2e-3
+
+
+def test_gemm_strided_input_and_batched():
+    from stableavatar_amd import ops
+    big = torch.randn(200, 320, device=dev).bfloat16()
+    x = big[:, 64:256]  # row stride 320, K = 192
+    w = torch.randn(130, 192, device=dev).bfloat16()
+    y = ops.linear(x, w, None, ops.EPI_F32)
+    assert rel(y, x.float() @ w.float().t()) < 2e-3
+    a = torch.randn(3, 100, 128, device=dev).bfloat16()
+    bb = torch.randn(3, 70, 128, device=dev).bfloat16()
+    out = torch.empty(3, 100, 70, device=dev)
+    ops.bmm_nt(a, bb, out)
+    assert rel(out, a.float() @ bb.float().transpose(1, 2)) < 2e-3
+
+
+def _ref_attn(q, k, v, scale):
+    s = (q.float() @ k.float().t()) * scale
+    return torch.softmax(s, -1) @ v.float()
+
+
+@pytest.mark.parametrize("Lq,Lk", [(300, 300), (512, 257), (1024, 17), (64, 512)])
+def test_attention_segments(Lq, Lk):
+    from stableavatar_amd import ops
+    B, H, D = 2, 3, 128
+    q = torch.randn(B * Lq, H * D + 64, device=dev).bfloat16()[:, :H * D]  # strided rows
+    k = torch.randn(B * Lk, H * D, device=dev).bfloat16()
+    v = torch.randn(B * Lk, H * D, device=dev).bfloat16()
+    o = torch.empty(B * Lq, H * D, device=dev, dtype=torch.bfloat16)
+    segs = torch.tensor([[b * Lq, Lq, b * Lk, Lk] for b in range(B)], dtype=torch.int32, device=dev)
+    ops.attention(q, k, v, o, segs, B, Lq, H)
+    for b in range(B):
+        for h in range(H):
+            ref = _ref_attn(q[b * Lq:(b + 1) * Lq, h * D:(h + 1) * D], k[b * Lk:(b + 1) * Lk, h * D:(h + 1) * D],
+                            v[b * Lk:(b + 1) * Lk, h * D:(h + 1) * D], D ** -0.5)
+            assert rel(o[b * Lq:(b + 1) * Lq, h * D:(h + 1) * D], ref) < 1e-2, (b, h)
+    # accumulate mode adds onto the existing output
+    o2 = o.clone()
+    ops.attention(q, k, v, o2, segs, B, Lq, H, accumulate=True)
+    assert rel(o2, 2 * o.float()) < 1e-2
+
+
+def test_attention_vocal_grouping():
+    """per-frame grouping of 1B:575-586: q rows of frame f attend to that frame's 17 keys"""
+    from stableavatar_amd import ops
+    B, F, G, Lv, H, D = 2, 3, 64, 17, 2, 128
+    q = torch.randn(B * F * G, H * D, device=dev).bfloat16()
+    k = torch.randn(B * F * Lv, H * D, device=dev).bfloat16()
+    v = torch.randn(B * F * Lv, H * D, device=dev).bfloat16()
+    o = torch.empty_like(q)
+    segs = torch.tensor([[i * G, G, i * Lv, Lv] for i in range(B * F)], dtype=torch.int32, device=dev)
+    ops.attention(q, k, v, o, segs, B * F, G, H)
+    for i in range(B * F):
+        for h in range(H):
+            sl = slice(h * D, (h + 1) * D)
+            ref = _ref_attn(q[i * G:(i + 1) * G, sl], k[i * Lv:(i + 1) * Lv, sl], v[i * Lv:(i + 1) * Lv, sl], D ** -0.5)
+            assert rel(o[i * G:(i + 1) * G, sl], ref) < 1e-2
+
+
+def test_attention_spike_rescale():
+    """force the online-softmax rescale branch: a late key with a huge score"""
+    from stableavatar_amd import ops
+    L, D = 512, 128
+    q = torch.randn(L, D, device=dev).bfloat16()
+    k = torch.randn(L, D, device=dev).bfloat16()
+    k[400] = q[5] * 4
+    v = torch.randn(L, D, device=dev).bfloat16()
+    o = torch.empty_like(q)
+    segs = torch.tensor([[0, L, 0, L]], dtype=torch.int32, device=dev)
+    ops.attention(q, k, v, o, segs, 1, L, 1)
+    assert rel(o, _ref_attn(q, k, v, D ** -0.5)) < 1e-2
+
+
+def test_layernorm_modulate():
+    from stableavatar_amd import ops
+    M, C, B = 1000, 1536, 2
+    rpb = 500
+    x = torch.randn(M, C, device=dev) * 3 + 1
+    shift = torch.randn(B, C, device=dev)
+    scale = torch.randn(B, C, device=dev)
+    out = torch.empty(M, C, device=dev, dtype=torch.bfloat16)
+    ops.layernorm_mod(x, out, 1e-6, shift=shift, scale=scale, rows_per_batch=rpb)
+    ln = torch.nn.functional.layer_norm(x, (C,), eps=1e-6)
+    bi = torch.arange(M, device=dev) // rpb
+    ref = ln * (1 + scale[bi]) + shift[bi]
+    assert rel(out, ref) < 5e-3
+    w = torch.randn(C, device=dev)
+    bb = torch.randn(C, device=dev)
+    out32 = torch.empty(M, C, device=dev)
+    ops.layernorm_mod(x, out32, 1e-5, weight=w, bias=bb)
+    assert rel(out32, torch.nn.functional.layer_norm(x, (C,), w, bb, 1e-5)) < 1e-5
+    gate = torch.randn(B, C, device=dev)
+    ops.layernorm_mod(x, out32, 1e-6, shift=shift, scale=scale, gate=gate, rows_per_batch=rpb)
+    assert rel(out32, x + ref * gate[bi]) < 1e-5
+    # width 1280 (CLIP MLPProj) exercises the partial-chunk path
+    x2 = torch.randn(100, 1280, device=dev)
+    o2 = torch.empty(100, 1280, device=dev)
+    ops.layernorm_mod(x2, o2, 1e-5, weight=w[:1280], bias=bb[:1280])
+    assert rel(o2, torch.nn.functional.layer_norm(x2, (1280,), w[:1280], bb[:1280], 1e-5)) < 1e-5
+
+
+def _rope_ref(x, F, H, W, L, d=128):
+    """restatement of 1B:223-231 + 295-323 on one batch row x [L, n, d] (fp64 freqs)"""
+    def params(dim):
+        f = torch.outer(torch.arange(1024, dtype=torch.float64),
+                        1.0 / torch.pow(10000, torch.arange(0, dim, 2, dtype=torch.float64) / dim))
+        return torch.polar(torch.ones_like(f), f)
+    freqs = torch.cat([params(d - 4 * (d // 6)), params(2 * (d // 6)), params(2 * (d // 6))], 1)
+    c = d // 2
+    fr = freqs.split([c - 2 * (c // 3), c // 3, c // 3], 1)
+    n = x.shape[1]
+    S = F * H * W
+    xi = torch.view_as_complex(x[:S].double().reshape(S, n, -1, 2))
+    fi = torch.cat([fr[0][:F].view(F, 1, 1, -1).expand(F, H, W, -1), fr[1][:H].view(1, H, 1, -1).expand(F, H, W, -1),
+                    fr[2][:W].view(1, 1, W, -1).expand(F, H, W, -1)], -1).reshape(S, 1, -1)
+    out = torch.view_as_real(xi * fi.to(xi.device)).flatten(2)
+    return torch.cat([out, x[S:].double()]).float(), freqs
+
+
+def test_qk_rmsnorm_rope():
+    from stableavatar_amd import ops
+    from stableavatar_amd.transformer import rope_table
+    F, H, W, B, C = 3, 4, 6, 2, 1536
+    L = F * H * W + 8  # padded tokens are normalised but not rotated
+    qkv = torch.randn(B * L, 3 * C, device=dev).bfloat16()
+    wq = torch.randn(C, device=dev)
+    wk = torch.randn(C, device=dev)
+    x = qkv.clone()
+    rope = rope_table(128).to(dev)
+    ops.qk_rmsnorm_rope(x, 0, C, wq, wk, C, 1e-6, rope=rope, rows_per_batch=L, grid=(F, H, W), n_frame_pairs=22,
+                        n_height_pairs=21)
+    for part, w in ((0, wq), (1, wk)):
+        src = qkv[:, part * C:(part + 1) * C].float()
+        nrm = src * torch.rsqrt(src.pow(2).mean(-1, keepdim=True) + 1e-6) * w
+        for b in range(B):
+            ref, _ = _rope_ref(nrm[b * L:(b + 1) * L].view(L, 12, 128).cpu(), F, H, W, L)
+            got = x[b * L:(b + 1) * L, part * C:(part + 1) * C].float().cpu()
+            assert rel(got, ref.reshape(L, C)) < 5e-3
+    assert torch.equal(x[:, 2 * C:], qkv[:, 2 * C:])
+
+
+def test_patchify_roundtrip():
+    from stableavatar_amd import ops
+    B, F, H, W = 3, 2, 8, 12
+    lat = torch.randn(1, 16, 5, H, W, device=dev).bfloat16()
+    y = torch.randn(B, 20, F, H, W, device=dev).bfloat16()
+    L = F * (H // 2) * (W // 2) + 5
+    Kp = 192
+    cols = torch.empty(B, L, Kp, device=dev, dtype=torch.bfloat16)
+    ops.patch_im2col(lat, y, B, F, H, W, cols, Kp, L, x_frame_offset=2, x_batch_broadcast=True)
+    xin = torch.cat([lat[:, :, 2:2 + F].expand(B, -1, -1, -1, -1), y], 1).float()  # [B,36,F,H,W]
+    wconv = torch.randn(7, 36, 1, 2, 2, device=dev)
+    ref = torch.nn.functional.conv3d(xin, wconv, stride=(1, 2, 2)).flatten(2).transpose(1, 2)
+    got = cols[:, :F * (H // 2) * (W // 2), :144].float() @ wconv.flatten(1).t()
+    assert rel(got, ref) < 1e-5
+    assert cols[:, F * (H // 2) * (W // 2):].abs().sum() == 0
+    # unpatchify of a [B, L, 64] head output
+    ho = torch.randn(B, L, 64, device=dev).bfloat16()
+    out = torch.empty(B, 16, F, H, W, device=dev)
+    ops.unpatchify(ho.view(B * L, 64), L, B, 16, F, H, W, out)
+    for b in range(B):
+        u = ho[b, :F * (H // 2) * (W // 2)].float().view(F, H // 2, W // 2, 1, 2, 2, 16)
+        u = torch.einsum("fhwpqrc->cfphqwr", u).reshape(16, F, H, W)
+        assert torch.equal(out[b], u)
+
+
+def test_small_kernels():
+    from stableavatar_amd import ops
+    t = torch.tensor([1000.0, 995.87, 24.41], device=dev)
+    e = torch.empty(3, 256, device=dev)
+    ops.timestep_embed(t, 256, e)
+    pos = t.double().cpu()
+    sinus = torch.outer(pos, torch.pow(10000, -torch.arange(128).double().div(128)))
+    ref = torch.cat([torch.cos(sinus), torch.sin(sinus)], 1).float()
+    assert (e.cpu() - ref).abs().max() < 1e-5
+    W = torch.randn(9216, 1536, device=dev).bfloat16()
+    b = torch.randn(9216, device=dev)
+    x = torch.randn(3, 1536, device=dev)
+    out = torch.empty(3, 9216, device=dev)
+    ops.small_linear_f32(x, W, b, out, act_in=1)
+    assert rel(out, torch.nn.functional.silu(x) @ W.float().t() + b) < 1e-5
+    mod = torch.randn(4, 6, 1536, device=dev)
+    e0 = torch.randn(3, 6, 1536, device=dev)
+    o = torch.empty(4, 3, 6, 1536, device=dev)
+    ops.mod_add(mod, e0, o)
+    assert torch.equal(o, mod[:, None] + e0[None])
+    src = torch.randn(10, 1536, device=dev)
+    idx = torch.tensor([3, -1, 0, 9], dtype=torch.int32, device=dev)
+    g = torch.empty(4, 1536, device=dev)
+    ops.gather_rows(src, idx, g)
+    assert torch.equal(g[0], src[3]) and g[1].abs().sum() == 0 and torch.equal(g[3], src[9])
+
+
+def test_flow_step_blend():
+    from stableavatar_amd import ops
+    C, T, Fw, H, W = 16, 30, 21, 8, 8
+    lat = torch.randn(1, C, T, H, W, device=dev).bfloat16()
+    pred = torch.randn(1, C, T, H, W, device=dev).bfloat16()
+    noise = torch.randn(3, C, Fw, H, W, device=dev).bfloat16()
+    start, ov = 6, 15
+    wts = torch.arange(ov, device=dev, dtype=torch.float32) / (ov - 1)
+    pred0 = pred.clone()
+    ops.flow_step(lat, pred, noise, start, -0.0042, 5.0, 3.0, ov, start + ov, wts, True)
+    u, d, c = noise.chunk(3)
+    v = u + 5.0 * (d - u) + 3.0 * (c - d)
+    x = lat[:, :, start:start + Fw].float() + (-0.0042) * v.float()
+    wb = wts.bfloat16().view(1, 1, ov, 1, 1).float()
+    x[:, :, :ov] = x[:, :, :ov] * wb + pred0[:, :, start:start + ov].float() * (1 - wb)
+    assert rel(pred[:, :, start:start + Fw], x) < 1e-2
+    assert torch.equal(pred[:, :, :start], pred0[:, :, :start])
