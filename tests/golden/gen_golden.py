@@ -1,0 +1,194 @@
+"""Generate golden vectors by running the REFERENCE implementation (/root/reference, imported with
+the diffusers stand-ins of _refstub.py) on CPU in fp32.  Run here only:
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+
+Inputs are regenerated from seeds (stableavatar_amd.synthetic) by the tests; the .npz files hold
+outputs (and the few pipeline-internal inputs that need the reference's VAE encoder).  Weights come
+from the name-keyed rule of stableavatar_amd.synthetic, so no weights are stored.
+"""
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+
+import _refstub  # noqa: E402
+
+_refstub.install()
+
+from stableavatar_amd import synthetic  # noqa: E402
+from golden_cases import DIT_SMALL, dit_inputs, VAE_SMALL, vae_latent, PIPE, pipe_fixed_inputs  # noqa: E402
+
+torch.set_grad_enabled(False)
+
+
+def load_synthetic(module, seed):
+    sd = module.state_dict()
+    shapes = {k: tuple(v.shape) for k, v in sd.items()}
+    vals = synthetic.fill_state_dict(shapes, seed)
+    module.load_state_dict(vals, strict=True)
+    return module
+
+
+def build_ref_dit(cfg):
+    from wan.models.wan_fantasy_transformer3d_1B import WanTransformer3DFantasyModel
+    m = WanTransformer3DFantasyModel(model_type="i2v", patch_size=(1, 2, 2), text_len=cfg["text_len"],
+                                     in_dim=cfg["in_dim"], dim=cfg["dim"], ffn_dim=cfg["ffn_dim"],
+                                     freq_dim=cfg["freq_dim"], text_dim=cfg["text_dim"], out_dim=cfg["out_dim"],
+                                     num_heads=cfg["num_heads"], num_layers=cfg["num_layers"], qk_norm=True,
+                                     cross_attn_norm=True, eps=1e-6)
+    return load_synthetic(m.eval(), cfg["seed"])
+
+
+def gen_dit():
+    m = build_ref_dit(DIT_SMALL)
+    out = {}
+    for case in ("full", "short"):
+        inp = dit_inputs(DIT_SMALL, case)
+        y = m(x=inp["x"], t=inp["t"], context=inp["context"], seq_len=inp["seq_len"], clip_fea=inp["clip_fea"],
+              y=inp["y"], vocal_embeddings=inp["vocal"], is_clip_level_modeling=False,
+              video_sample_n_frames=inp["n_frames"])
+        out[f"{case}_out"] = y.numpy()
+        print(case, tuple(y.shape), float(y.abs().mean()))
+    # sub-module pins: vocal projector output for the full case
+    inp = dit_inputs(DIT_SMALL, "full")
+    np.savez_compressed(os.path.join(HERE, "dit_small.npz"), **out)
+
+
+def build_ref_vae(cfg):
+    from wan.models.wan_vae import AutoencoderKLWan, _video_vae
+    v = AutoencoderKLWan()
+    v.model = _video_vae(z_dim=16, dim=cfg["dim"])
+    return load_synthetic(v.eval(), cfg["seed"])
+
+
+def gen_vae():
+    out = {}
+    for name, cfg in VAE_SMALL.items():
+        v = build_ref_vae(cfg)
+        z = vae_latent(cfg)
+        y = v.decode(z).sample
+        out[name] = y.numpy()
+        print("vae", name, tuple(y.shape), float(y.abs().mean()))
+    np.savez_compressed(os.path.join(HERE, "vae_small.npz"), **out)
+
+
+class _Obj(types.SimpleNamespace):
+    def __getitem__(self, i):
+        return [self.last][i]
+
+
+def gen_pipeline():
+    from PIL import Image
+    from wan.pipeline.wan_inference_long_pipeline import WanI2VTalkingInferenceLongPipeline
+    from _refstub import FlowMatchEulerDiscreteScheduler
+
+    P = PIPE
+    dit = build_ref_dit(P["dit"])
+    vae = build_ref_vae(P["vae"])
+    fx = pipe_fixed_inputs(P)
+
+    class Tok:
+        def __call__(self, prompt, padding=None, max_length=None, truncation=None, add_special_tokens=None,
+                     return_tensors=None):
+            n = max_length or 8
+            lens = [P["neg_len"] if p == "" else P["pos_len"] for p in prompt]
+            ids = torch.ones(len(prompt), n, dtype=torch.long)
+            mask = torch.zeros(len(prompt), n, dtype=torch.long)
+            for i, ln in enumerate(lens):
+                mask[i, :ln] = 1
+            return types.SimpleNamespace(input_ids=ids, attention_mask=mask)
+
+        def batch_decode(self, *a, **k):
+            return []
+
+    class T5(torch.nn.Module):
+        dtype = torch.float32
+
+        def forward(self, ids, attention_mask=None):
+            ln = int(attention_mask.sum())
+            e = fx["pos_embeds"] if ln == P["pos_len"] else fx["neg_embeds"]
+            full = torch.zeros(1, ids.shape[1], e.shape[1])
+            full[0, :ln] = e
+            return (full,)
+
+    class Clip(torch.nn.Module):
+        def forward(self, imgs):
+            return fx["clip"].clone()
+
+    class Proc:
+        def __call__(self, samples, sampling_rate=None, return_tensors=None):
+            return types.SimpleNamespace(input_values=torch.as_tensor(np.asarray(samples), dtype=torch.float32)[None])
+
+    class W2V(torch.nn.Module):
+        def forward(self, x):
+            return types.SimpleNamespace(last_hidden_state=synthetic.fake_wav2vec_features(x))
+
+    calls = []
+    orig = dit.forward
+
+    def traced(**kw):
+        calls.append({"F": kw["x"].shape[2], "t": float(kw["t"][0]), "seq_len": kw["seq_len"],
+                      "n_audio": kw["vocal_embeddings"].shape[1]})
+        if len(calls) == 1:
+            calls[0]["y"] = kw["y"].clone()
+        return orig(**kw)
+
+    dit.forward = traced
+    decoded = {}
+    vdec = vae.decode
+
+    def tdec(z, return_dict=True):
+        decoded["latents"] = z.clone()
+        return vdec(z, return_dict)
+
+    vae.decode = tdec
+    img = Image.fromarray((np.random.default_rng(1).random((48, 40, 3)) * 255).astype(np.uint8))
+    path = "/tmp/_sa_golden_ref.png"
+    img.save(path)
+    pipe = WanI2VTalkingInferenceLongPipeline(tokenizer=Tok(), text_encoder=T5(), vae=vae, transformer=dit,
+                                              clip_image_encoder=Clip(),
+                                              scheduler=FlowMatchEulerDiscreteScheduler(1000, shift=5.0),
+                                              wav2vec_processor=Proc(), wav2vec=W2V())
+    video = pipe("pos prompt", negative_prompt="", num_frames=P["clip_length"], height=P["height"],
+                 width=P["width"], guidance_scale=6.0, num_inference_steps=P["steps"], latents=fx["latents"],
+                 text_guide_scale=P["text_guide"], audio_guide_scale=P["audio_guide"],
+                 vocal_input_values=fx["audio"].numpy(), fps=25, sr=16000, cond_file_path=path,
+                 overlap_window_length=P["overlap"], clip_length=P["clip_length"]).videos
+    out = {"video": video.numpy(), "latents": decoded["latents"].numpy(), "y": calls[0]["y"].numpy(),
+           "win_F": np.array([c["F"] for c in calls]), "win_t": np.array([c["t"] for c in calls]),
+           "win_seq_len": np.array([c["seq_len"] for c in calls]),
+           "win_n_audio": np.array([c["n_audio"] for c in calls])}
+    print("pipeline windows", [(c["F"], round(c["t"], 2), c["n_audio"]) for c in calls], tuple(video.shape))
+    np.savez_compressed(os.path.join(HERE, "pipeline_small.npz"), **out)
+
+
+def gen_tables():
+    from wan.models.vocal_projector_fantasy import split_audio_sequence, split_tensor_with_padding
+    from _refstub import FlowMatchEulerDiscreteScheduler
+    out = {}
+    for L, nf in ((167, 81), (161, 81), (39, 17), (23, 17), (100, 33), (400, 81)):
+        r = split_audio_sequence(L, num_frames=nf)
+        x = torch.arange(L, dtype=torch.float32).view(1, L, 1) + 1.0
+        sub, lens = split_tensor_with_padding(x, r, expand_length=4)
+        out[f"split_{L}_{nf}_ranges"] = np.array(r)
+        out[f"split_{L}_{nf}_rows"] = (sub[0, :, :, 0].numpy() - 1.0).astype(np.int64)  # -1 marks zero rows
+        out[f"split_{L}_{nf}_lens"] = lens.numpy()
+    s = FlowMatchEulerDiscreteScheduler(1000, shift=5.0)
+    s.set_timesteps(50)
+    out["sched50_timesteps"] = s.timesteps.numpy()
+    out["sched50_sigmas"] = s.sigmas.numpy()
+    np.savez_compressed(os.path.join(HERE, "tables.npz"), **out)
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["tables", "dit", "vae", "pipeline"]
+    for w in which:
+        globals()["gen_" + w]()

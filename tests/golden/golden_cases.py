@@ -1,0 +1,56 @@
+"""Shared definitions of the golden cases: configs + seeded input builders.  Used by
+gen_golden.py (with the reference, here only) and by the tests (oracle / HIP path)."""
+import math
+
+import torch
+
+from stableavatar_amd import synthetic
+
+# dim must be 1536: the vocal projector hard-codes audio_proj_dim=1536 (1B:872)
+DIT_SMALL = dict(model_type="i2v", dim=1536, ffn_dim=256, freq_dim=256, text_dim=64, in_dim=36, out_dim=16,
+                 num_heads=12, num_layers=2, text_len=32, eps=1e-6, seed=11)
+
+
+def dit_inputs(cfg, case="full"):
+    """CFG batch of 3 at 64x64 video -> 8x8 latent, clip 17 (5 latent frames, seq_len 80).
+    'short' is the last-window case: 3 latent frames padded to the 5-frame seq_len."""
+    B, H, W = 3, 8, 8
+    Fw = 5 if case == "full" else 3
+    n_frames = 17
+    seq_len = ((n_frames - 1) // 4 + 1) * (H // 2) * (W // 2)
+    lat = synthetic.seeded_normal((1, 16, Fw, H, W), 101)
+    x = torch.cat([lat] * 3)
+    y = synthetic.seeded_normal((B, 20, 5, H, W), 102)[:, :, :Fw].contiguous()
+    neg = synthetic.seeded_normal((20, cfg["text_dim"]), 103)
+    pos = synthetic.seeded_normal((25, cfg["text_dim"]), 104)
+    clip = synthetic.seeded_normal((1, 257, 1280), 105).expand(3, -1, -1).contiguous()
+    a = synthetic.seeded_normal((1, 39, 768), 106)
+    vocal = torch.cat([torch.zeros_like(a), a, a])
+    t = torch.full((3,), 937.5)
+    return dict(x=x, y=y, context=[neg, neg, pos], clip_fea=clip, vocal=vocal, t=t, seq_len=seq_len,
+                n_frames=n_frames)
+
+
+VAE_SMALL = {"dim16_T3_8x8": dict(dim=16, seed=21, T=3, h=8, w=8),
+             "dim96_T2_4x4": dict(dim=96, seed=22, T=2, h=4, w=4)}
+
+
+def vae_latent(cfg):
+    return synthetic.seeded_normal((1, 16, cfg["T"], cfg["h"], cfg["w"]), 200 + cfg["seed"])
+
+
+PIPE = dict(dit=dict(DIT_SMALL, num_layers=1, seed=31), vae=dict(dim=16, seed=32), height=64, width=64,
+            clip_length=17, steps=3, overlap=2, text_guide=3.0, audio_guide=5.0, neg_len=12, pos_len=9,
+            audio_frames=24)
+
+
+def pipe_fixed_inputs(P):
+    """Seeded inputs of the pipeline golden: 24 video frames of audio @16 kHz -> T_lat 6 -> two
+    windows (0,5),(3,6) per step (avoids the reference's single-window hang, App. A.1)."""
+    n = P["audio_frames"] * 640
+    T = (P["audio_frames"] - 1) // 4 + 1
+    return dict(audio=synthetic.seeded_normal((n,), 300, 0.1),
+                latents=synthetic.seeded_normal((1, 16, T, P["height"] // 8, P["width"] // 8), 301),
+                neg_embeds=synthetic.seeded_normal((P["neg_len"], P["dit"]["text_dim"]), 302),
+                pos_embeds=synthetic.seeded_normal((P["pos_len"], P["dit"]["text_dim"]), 303),
+                clip=synthetic.seeded_normal((1, 257, 1280), 304))

@@ -1,0 +1,108 @@
+"""Pin the CPU oracle (oracle/) against golden vectors produced by the reference implementation
+itself (tests/golden/gen_golden.py).  CPU only."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+
+from golden_cases import DIT_SMALL, PIPE, VAE_SMALL, dit_inputs, pipe_fixed_inputs, vae_latent  # noqa: E402
+
+from oracle import dit as odit  # noqa: E402
+from oracle import pipeline as opipe  # noqa: E402
+from oracle import vae as ovae  # noqa: E402
+from stableavatar_amd import synthetic  # noqa: E402
+
+G = lambda n: np.load(os.path.join(HERE, "golden", n))  # noqa: E731
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).double()
+    b = torch.as_tensor(b).double()
+    return ((a - b).norm() / b.norm()).item()
+
+
+def test_split_tables_bit_exact():
+    g = G("tables.npz")
+    for L, nf in ((167, 81), (161, 81), (39, 17), (23, 17), (100, 33), (400, 81)):
+        r = odit.split_audio_sequence(L, nf)
+        assert np.array_equal(np.array(r), g[f"split_{L}_{nf}_ranges"])
+        rows, lens = odit.split_index_table(L, nf)
+        assert np.array_equal(np.array(rows), g[f"split_{L}_{nf}_rows"])
+        assert np.array_equal(np.array(lens), g[f"split_{L}_{nf}_lens"])
+
+
+def test_sigma_table():
+    g = G("tables.npz")
+    t, s = opipe.flow_sigmas(50, 5.0)
+    assert np.array_equal(t.numpy(), g["sched50_timesteps"])
+    assert np.array_equal(s.numpy(), g["sched50_sigmas"])
+    assert abs(t[0].item() - 1000.0) < 1e-3 and abs(t[-1].item() - 24.41) < 1e-2
+
+
+def test_window_schedule():
+    # case-1 shape (T_lat 42), overlap 15 -> 5 windows; overlap 10 -> 3 windows
+    assert [w[:2] for w in opipe.window_schedule(42, 21, 15)] == [(0, 21), (6, 27), (12, 33), (18, 39), (24, 42)]
+    assert len(opipe.window_schedule(42, 21, 10)) == 3
+    assert len(opipe.window_schedule(251, 21, 10)) == 22
+    assert opipe.window_schedule(21, 21, 15) == [(0, 21, 21)]  # the reference hangs here (App. A.1)
+    with pytest.raises(ValueError):
+        opipe.window_schedule(20, 21, 15)
+
+
+@pytest.fixture(scope="module")
+def dit_params():
+    return synthetic.fill_state_dict(odit.param_shapes(DIT_SMALL), DIT_SMALL["seed"])
+
+
+@pytest.mark.parametrize("case", ["full", "short"])
+def test_dit_forward_vs_reference(dit_params, case):
+    inp = dit_inputs(DIT_SMALL, case)
+    with torch.no_grad():
+        y = odit.forward(dit_params, DIT_SMALL, inp["x"], inp["t"], inp["context"], inp["seq_len"], inp["clip_fea"],
+                         inp["y"], inp["vocal"], inp["n_frames"])
+    assert rel(y, G("dit_small.npz")[f"{case}_out"]) < 1e-5
+
+
+@pytest.mark.parametrize("name", list(VAE_SMALL))
+def test_vae_decode_vs_reference(name):
+    cfg = VAE_SMALL[name]
+    P = synthetic.fill_state_dict(ovae.param_shapes(dim=cfg["dim"]), cfg["seed"])
+    with torch.no_grad():
+        y = ovae.decode(P, vae_latent(cfg), dim=cfg["dim"])
+    g = G("vae_small.npz")[name]
+    assert y.shape == g.shape
+    assert rel(y, g) < 1e-5
+
+
+def test_pipeline_vs_reference():
+    g = G("pipeline_small.npz")
+    Pd = synthetic.fill_state_dict(odit.param_shapes(PIPE["dit"]), PIPE["dit"]["seed"])
+    Pv = synthetic.fill_state_dict(ovae.param_shapes(dim=PIPE["vae"]["dim"]), PIPE["vae"]["seed"])
+    fx = pipe_fixed_inputs(PIPE)
+    ctx = [fx["neg_embeds"], fx["neg_embeds"], fx["pos_embeds"]]
+    clip = torch.cat([fx["clip"]] * 3)
+    y = torch.from_numpy(g["y"])
+    calls = []
+
+    def dit(x, t, context, seq_len, yy, clip_fea, vocal, n):
+        calls.append((x.shape[2], round(float(t[0]), 2), vocal.shape[1], seq_len))
+        return odit.forward(Pd, PIPE["dit"], x, t, context, seq_len, clip_fea, yy, vocal, n)
+
+    enc = lambda s: synthetic.fake_wav2vec_features(torch.as_tensor(s)[None])  # noqa: E731
+    with torch.no_grad():
+        lat = opipe.denoise(dit, fx["latents"], y, ctx, clip, fx["audio"], enc, num_inference_steps=PIPE["steps"],
+                            clip_length=PIPE["clip_length"], num_frames=PIPE["clip_length"], height=PIPE["height"],
+                            width=PIPE["width"], overlap=PIPE["overlap"], text_guide_scale=PIPE["text_guide"],
+                            audio_guide_scale=PIPE["audio_guide"])
+        video = ovae.decode(Pv, lat, dim=PIPE["vae"]["dim"])
+        video = (video / 2 + 0.5).clamp(0, 1)
+    assert [c[0] for c in calls] == list(g["win_F"])
+    assert [c[2] for c in calls] == list(g["win_n_audio"])
+    assert np.allclose([c[1] for c in calls], g["win_t"], atol=1e-2)
+    assert rel(lat, g["latents"]) < 1e-3
+    assert rel(video, g["video"]) < 1e-3
