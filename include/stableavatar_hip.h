@@ -45,6 +45,12 @@ int sa_attn_fwd(const void* q, const void* k, const void* v, void* o, const int3
                 int heads, int head_dim, int64_t q_stride, int64_t k_stride, int64_t v_stride, int64_t o_stride,
                 float scale, int accumulate, void* stream);
 
+/* attention for head dims other than 128 and few queries per segment (vocal projector D=192,
+ * vocal_projector_fantasy_1B.py:259-270): exact softmax, fp32 math, kv_len <= 4096, head_dim <= 256. */
+int sa_attn_small(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg, int max_q_len,
+                  int max_kv_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride, int64_t v_stride,
+                  int64_t o_stride, float scale, void* stream);
+
 /* LayerNorm (+affine) (+AdaLN modulate  y*(1+scale[b])+shift[b]) (+gated residual x + y*gate[b]):
  * WanLayerNorm 1B:345-355 and its call sites :675,684,687,721-722; MLPProj LayerNorms :731-734;
  * vocal_projector_fantasy_1B.py:345-347,352,354,386,398.  in/out dtype: 0 = f32, 1 = bf16. */
@@ -75,8 +81,10 @@ int sa_timestep_embed(const float* t, int B, int dim, float* out, void* stream);
 int sa_small_linear_f32(const float* in, int64_t ldi, int M, const void* W, int64_t ldw, const float* bias,
                         float* out, int64_t ldo, int N, int K, int act_in, int act_out, void* stream);
 
-/* out[l,b,j,c] = mod[l,j,c] + e[b,j,c]   ((self.modulation + e).chunk(6), 1B:672, :721) */
-int sa_mod_add(const float* mod, const float* e, float* out, int L, int B, int J, int C, void* stream);
+/* out[l,b,j,c] = mod[l,j,c] + e[b*e_bstride + j*e_jstride + c]   ((self.modulation + e).chunk(6), 1B:672,
+ * :721; e_jstride = 0 broadcasts the time embedding over the chunks as Head.forward does) */
+int sa_mod_add(const float* mod, const float* e, int64_t e_bstride, int64_t e_jstride, float* out, int L, int B, int J,
+               int C, void* stream);
 
 /* CFG combine + FlowMatchEulerDiscreteScheduler.step + overlap blend + scatter of one window
  * (wan/pipeline/wan_inference_long_pipeline.py:751-779). */
@@ -90,6 +98,37 @@ int sa_gather_rows(const void* in, int64_t in_row_bytes, const int32_t* idx, int
 
 int sa_fill_f32(float* p, int64_t n, float v, void* stream);
 int sa_cast_f32_bf16(const float* in, void* out, int64_t n, void* stream);
+
+/* ---- 3-D causal VAE decoder (wan/models/wan_vae.py), channels-last bf16 activations ---- */
+
+/* CausalConv3d (wan_vae.py:20-39) / Conv2d 3x3 (:80-86) / 1x1 convs over a whole clip as an implicit
+ * GEMM: x [T, H/(1+upsample), W/(1+upsample), Cin] -> y [T, H, W, Cout] (+bias) (+residual [T,H,W,Cout]).
+ * kt in {1,3} (causal: kt-1 zero frames in front), kh = kw in {1,3} (zero pad (k-1)/2).
+ * upsample != 0 reads the input through nearest-exact 2x upsampling (Upsample, :60-66).
+ * interleave_half = C > 0 writes time_conv output channel block j of frame t to frame 2t+j
+ * (Resample 'upsample3d', :137-140).  w = bf16 [Cout_pad][kt][kh][kw][Cin], Cin % 32 == 0. */
+int sa_conv3d_cl(const void* x, int T, int H, int W, int Cin, int upsample, const void* w, const float* bias, int Cout,
+                 int Cout_pad, int kt, int kh, int kw, const void* residual, void* y, int out_f32,
+                 int interleave_half, void* stream);
+
+/* RMS_norm (wan_vae.py:42-57): x / max(||x||_2, 1e-12) * sqrt(C) * gamma over channels (+SiLU :198-200). */
+int sa_vae_rmsnorm_silu(const void* x, void* y, const float* gamma, int64_t rows, int C, int do_silu, void* stream);
+
+/* z [Cz][T*h*w] fp32 -> channels-last bf16 [T*h*w][Cp] of z*std + mean (= z / scale[1] + scale[0], :553-557). */
+int sa_vae_input(const float* z, int Cz, int64_t THW, const float* mean, const float* stdv, void* out, int Cp,
+                 void* stream);
+
+/* channels-last fp32 [THW][C_stride] -> [C][THW] clamped to [-1,1] (:668); post != 0 also applies
+ * decode_latents' /2 + 0.5 and clamp(0,1) (wan_inference_long_pipeline.py:427). */
+int sa_vae_output(const float* in, int C_stride, int C, int64_t THW, float* out, int post, void* stream);
+
+/* row softmax of fp32 scores (scaled) -> bf16 probabilities (AttentionBlock SDPA, wan_vae.py:255-259). */
+int sa_softmax_rows(const float* s, int64_t ld_s, void* p, int64_t ld_p, int64_t rows, int n, float scale,
+                    void* stream);
+
+/* batched bf16 transpose: out[z][c][r] = in[z][r][c]. */
+int sa_transpose_bf16(const void* in, int64_t ld_in, int64_t stride_in, void* out, int64_t ld_out,
+                      int64_t stride_out, int rows, int cols, int batch, void* stream);
 
 #ifdef __cplusplus
 }

@@ -23,11 +23,18 @@ SIGNATURES = {
     "sa_unpatchify": "pliiiiiipip",
     "sa_timestep_embed": "piipp",
     "sa_small_linear_f32": "pliplppliiiip",
-    "sa_mod_add": "pppiiiip",
+    "sa_mod_add": "ppllpiiiip",
+    "sa_attn_small": "pppppiiiiillllfp",
     "sa_flow_step": "pppiiiilifffiipip",
     "sa_gather_rows": "plpipllp",
     "sa_fill_f32": "plfp",
     "sa_cast_f32_bf16": "pplp",
+    "sa_conv3d_cl": "piiiiippiiiiippiip",
+    "sa_vae_rmsnorm_silu": "pppliip",
+    "sa_vae_input": "pilpppip",
+    "sa_vae_output": "piilpip",
+    "sa_softmax_rows": "plpllifp",
+    "sa_transpose_bf16": "pllplliiip",
 }
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int32, "l": ctypes.c_int64, "f": ctypes.c_float}
 

@@ -183,7 +183,70 @@ __global__ __launch_bounds__(512) void attn_fwd_kernel(AttnArgs a) {
   }
 }
 
+// ---- small-query attention for head dims the MFMA kernel does not take (vocal projector, D=192,
+// 17 queries per frame vs 1024 latent tokens: vocal_projector_fantasy_1B.py:259-270).  One wave
+// per (segment, head, query): scores for all keys in LDS, exact softmax, lane-parallel P·V.
+constexpr int SMALL_MAXK = 4096;
+constexpr int SMALL_MAXD = 256;
+
+__global__ __launch_bounds__(256) void attn_small_kernel(const bf16* q, const bf16* k, const bf16* v, bf16* o,
+                                                         const int* segs, int heads, int D, long qs, long ks, long vs,
+                                                         long os, float scale) {
+  __shared__ float p[4][SMALL_MAXK];
+  __shared__ float qv[4][SMALL_MAXD];
+  const int* sg = segs + blockIdx.z * 4;
+  const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int qi = blockIdx.x * 4 + w;
+  const int h = blockIdx.y;
+  if (qi >= q_len) return;
+  const bf16* qp = q + (long)(q_row0 + qi) * qs + h * D;
+  for (int d = lane; d < D; d += 64) qv[w][d] = bf2f(qp[d]) * scale;
+  __builtin_amdgcn_wave_barrier();
+  float mx = -INFINITY;
+  for (int j = lane; j < kv_len; j += 64) {
+    const bf16* kp = k + (long)(kv_row0 + j) * ks + h * D;
+    float s = 0.f;
+    for (int d = 0; d < D; d += 8) {
+      const bf16x8 kk = *(const bf16x8*)(kp + d);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) s = fmaf(qv[w][d + t], bf2f(kk[t]), s);
+    }
+    p[w][j] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int j = lane; j < kv_len; j += 64) {
+    const float e = __expf(p[w][j] - mx);
+    p[w][j] = e;
+    sum += e;
+  }
+  sum = wave_sum(sum);
+  __builtin_amdgcn_wave_barrier();
+  const float inv = 1.f / sum;
+  bf16* op = o + (long)(q_row0 + qi) * os + h * D;
+  for (int d = lane; d < D; d += 64) {
+    float acc = 0.f;
+    for (int j = 0; j < kv_len; ++j) acc = fmaf(p[w][j], bf2f(v[(long)(kv_row0 + j) * vs + h * D + d]), acc);
+    op[d] = f2bf(acc * inv);
+  }
+}
+
 }  // namespace
+
+extern "C" int sa_attn_small(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
+                             int max_q_len, int max_kv_len, int heads, int head_dim, int64_t q_stride,
+                             int64_t k_stride, int64_t v_stride, int64_t o_stride, float scale, void* stream) {
+  if (!q || !k || !v || !o || !segs || nseg <= 0 || max_q_len <= 0 || heads <= 0) return SA_ERR_ARG;
+  if (head_dim <= 0 || head_dim > SMALL_MAXD || head_dim % 8 || max_kv_len > SMALL_MAXK) return SA_ERR_ARG;
+  if ((k_stride % 8) || (((uintptr_t)k) & 15)) return SA_ERR_ARG;
+  dim3 grid((max_q_len + 3) / 4, heads, nseg);
+  hipLaunchKernelGGL(attn_small_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const bf16*)q, (const bf16*)k,
+                     (const bf16*)v, (bf16*)o, segs, heads, head_dim, q_stride, k_stride, v_stride, o_stride, scale);
+  SA_LAUNCH_CHECK();
+  return SA_OK;
+}
 
 extern "C" int sa_attn_fwd(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
                            int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride,

@@ -100,12 +100,13 @@ __global__ __launch_bounds__(256) void small_linear_kernel(const float* in, long
 }
 
 // out[l, b, j, c] = mod[l, j, c] + e[b, j, c]      (e broadcast over layers, mod over batch)
-__global__ void mod_add_kernel(const float* mod, const float* e, float* out, int L, int B, int J, int C) {
+__global__ void mod_add_kernel(const float* mod, const float* e, long eb, long ej, float* out, int L, int B, int J,
+                               int C) {
   const long n = (long)L * B * J * C;
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= n) return;
   const int c = idx % C, j = (idx / C) % J, b = (idx / ((long)C * J)) % B, l = idx / ((long)C * J * B);
-  out[idx] = mod[((long)l * J + j) * C + c] + e[((long)b * J + j) * C + c];
+  out[idx] = mod[((long)l * J + j) * C + c] + e[b * eb + j * ej + c];
 }
 
 // One sampler step for one window (pipeline:751-779):
@@ -217,10 +218,12 @@ extern "C" int sa_small_linear_f32(const float* in, int64_t ldi, int M, const vo
   return SA_OK;
 }
 
-extern "C" int sa_mod_add(const float* mod, const float* e, float* out, int L, int B, int J, int C, void* stream) {
+extern "C" int sa_mod_add(const float* mod, const float* e, int64_t e_bstride, int64_t e_jstride, float* out, int L,
+                          int B, int J, int C, void* stream) {
   if (!mod || !e || !out) return SA_ERR_ARG;
   const long n = (long)L * B * J * C;
-  hipLaunchKernelGGL(mod_add_kernel, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, mod, e, out, L, B, J, C);
+  hipLaunchKernelGGL(mod_add_kernel, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, mod, e, e_bstride, e_jstride,
+                     out, L, B, J, C);
   SA_LAUNCH_CHECK();
   return SA_OK;
 }

@@ -1,0 +1,364 @@
+// 3-D causal VAE decoder kernels (reference: wan/models/wan_vae.py), whole-clip formulation
+// (see oracle/vae.py for why the frame-by-frame causal cache equals whole-clip causal padding).
+// Activations are channels-last bf16 [T, H, W, C] so every conv is an implicit GEMM whose
+// A-operand rows are contiguous channel vectors.
+//  sa_conv3d_cl        : CausalConv3d (wan_vae.py:20-39) / Conv2d 3x3 / 1x1 as implicit GEMM on MFMA
+//                        (16x16x32 bf16), fused: nearest-exact 2x upsample of the input (Upsample
+//                        :60-66), bias, residual add (ResidualBlock :223 / AttentionBlock :265) and the
+//                        time_conv frame interleave of Resample 'upsample3d' (:137-140)
+//  sa_vae_rmsnorm_silu : RMS_norm (:42-57) (+SiLU) over channels
+//  sa_vae_input        : z / (1/std) + mean  (:553-557) -> channels-last bf16 (channel-padded)
+//  sa_vae_output       : channels-last fp32 -> [3, T, H, W] with clamp(-1,1) (:668) (+/2+0.5 clamp(0,1)
+//                        of decode_latents, pipeline:427)
+//  sa_softmax_rows     : softmax of fp32 score rows -> bf16 P (AttentionBlock SDPA :255-259)
+//  sa_transpose_bf16   : batched 2-D transpose (V -> V^T for the P·V GEMM)
+#include "common.h"
+
+namespace {
+
+struct ConvArgs {
+  const bf16* x;
+  int T, H, W, Cin;  // logical input (== output spatial dims)
+  int Hin, Win;      // physical input dims (H/2, W/2 when upsampling)
+  int upsample;
+  const bf16* w;     // [Coutp][kt][kh][kw][Cin]
+  const float* bias;
+  int Cout, kt, kh, kw;
+  const bf16* res;   // [T, H, W, Cout] or null
+  void* y;
+  int out_f32;
+  int ichalf;        // >0: time_conv interleave, out[2t + n/ichalf][h][w][n%ichalf]
+  long M;
+};
+
+constexpr int BM = 128, BK = 32;
+
+__device__ __forceinline__ int swz64(int r, int c) { return r * 64 + ((c ^ ((r >> 1) & 3)) << 4); }
+
+template <int NT>
+__global__ __launch_bounds__(256) void conv3d_cl_kernel(ConvArgs a) {
+  constexpr int BN = NT * 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int SBYTES = BM * 64 + BN * 64;  // one stage: A tile then B tile
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const long m0 = (long)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const long HW = (long)a.H * a.W;
+  const int K = a.kt * a.kh * a.kw * a.Cin;
+  const int nk = K / BK;
+
+  // this thread's two A staging chunks: rows r = idx>>2, chunk c = idx&3
+  int ar[2], ac[2], at[2], ah[2], aw[2];
+  bool arow_ok[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int idx = tid + j * 256;
+    ar[j] = idx >> 2;
+    ac[j] = idx & 3;
+    const long m = m0 + ar[j];
+    arow_ok[j] = m < a.M;
+    const long mm = arow_ok[j] ? m : 0;
+    at[j] = mm / HW;
+    const int p = mm % HW;
+    ah[j] = p / a.W;
+    aw[j] = p % a.W;
+  }
+  constexpr int BCH = BN * 4;  // 16-B chunks of the B tile
+  constexpr int BPT = (BCH + 255) / 256;
+
+  u32x4 ra[2], rb[BPT];
+  auto load = [&](int ks) {
+    const int k0 = ks * BK;
+    const int tap = k0 / a.Cin, ci0 = k0 % a.Cin;
+    const int dt = tap / (a.kh * a.kw), dh = (tap / a.kw) % a.kh, dw = tap % a.kw;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ti = at[j] + dt - (a.kt - 1);
+      const int hi = ah[j] + dh - (a.kh - 1) / 2;
+      const int wi = aw[j] + dw - (a.kw - 1) / 2;
+      const bool ok = arow_ok[j] && ti >= 0 && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
+      if (ok) {
+        const int hp = a.upsample ? (hi >> 1) : hi, wp = a.upsample ? (wi >> 1) : wi;
+        const bf16* src = a.x + (((long)ti * a.Hin + hp) * a.Win + wp) * a.Cin + ci0 + ac[j] * 8;
+        ra[j] = *(const u32x4*)src;
+      } else {
+        ra[j] = (u32x4){0u, 0u, 0u, 0u};
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      const int idx = tid + j * 256;
+      if (idx < BCH) {
+        const int r = idx >> 2, c = idx & 3;
+        rb[j] = *(const u32x4*)(a.w + (long)(n0 + r) * K + k0 + c * 8);
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) *(u32x4*)(smem + buf * SBYTES + swz64(ar[j], ac[j])) = ra[j];
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      const int idx = tid + j * 256;
+      if (idx < BCH) *(u32x4*)(smem + buf * SBYTES + BM * 64 + swz64(idx >> 2, idx & 3)) = rb[j];
+    }
+  };
+
+  f32x4 acc[2][NT];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[i][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  load(0);
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    store(buf);
+    __syncthreads();
+    if (ks + 1 < nk) load(ks + 1);
+    const int c = lane >> 4;
+    bf16x8 af[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(smem + buf * SBYTES + swz64(wave * 32 + i * 16 + (lane & 15), c));
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const bf16x8 bfr = *(const bf16x8*)(smem + buf * SBYTES + BM * 64 + swz64(n * 16 + (lane & 15), c));
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][n], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+
+  // epilogue through a per-wave 16 x BN fp32 strip
+  constexpr int LD = BN + 4;
+  float* strip = (float*)(smem + wave * 16 * LD * 4);
+  const int er = lane >> 2, q = lane & 3;
+  constexpr int CPL = BN / 4;  // columns per lane
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) strip[((lane >> 4) * 4 + r) * LD + n * 16 + (lane & 15)] = acc[i][n][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const long m = m0 + wave * 32 + i * 16 + er;
+    if (m < a.M) {
+      const long t = m / HW, p = m % HW;
+#pragma unroll
+      for (int g = 0; g < CPL; g += 4) {
+        const int n = n0 + q * CPL + g;
+        if (n < a.Cout) {
+          float v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = strip[er * LD + q * CPL + g + u] + a.bias[n + u];
+          long off;
+          if (a.ichalf > 0) {
+            const int half = n / a.ichalf, nc = n % a.ichalf;
+            off = ((2 * t + half) * HW + p) * a.ichalf + nc;
+          } else {
+            off = m * a.Cout + n;
+          }
+          if (a.res) {
+            const bf16x4 rr = *(const bf16x4*)(a.res + off);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] += bf2f(rr[u]);
+          }
+          if (a.out_f32) {
+            *(f32x4*)((float*)a.y + off) = (f32x4){v[0], v[1], v[2], v[3]};
+          } else {
+            *(bf16x4*)((bf16*)a.y + off) = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+          }
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+template <int NT>
+int launch_conv(const ConvArgs& a, hipStream_t st) {
+  constexpr int BN = NT * 16;
+  const int lds_main = 2 * (BM * 64 + BN * 64);
+  const int lds_epi = 4 * 16 * (BN + 4) * 4;
+  const int lds = lds_main > lds_epi ? lds_main : lds_epi;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv3d_cl_kernel<NT>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  dim3 grid((unsigned)((a.M + BM - 1) / BM), (a.Cout + BN - 1) / BN);
+  hipLaunchKernelGGL(conv3d_cl_kernel<NT>, grid, dim3(256), lds, st, a);
+  SA_LAUNCH_CHECK();
+  return SA_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+
+// rows of C channels; G lanes per row (power of two >= C/8), 64/G rows per wave
+template <int G>
+__global__ __launch_bounds__(256) void rmsnorm_silu_kernel(const bf16* x, bf16* y, const float* gamma, long rows,
+                                                           int C, int do_silu) {
+  const int lane = threadIdx.x & 63;
+  const long row = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 / G) + lane / G;
+  const int g = lane % G;
+  const bool ok = row < rows && g * 8 < C;
+  float v[8];
+  float s = 0.f;
+  if (ok) {
+    const bf16x8 a = *(const bf16x8*)(x + row * C + g * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { v[j] = bf2f(a[j]); s += v[j] * v[j]; }
+  }
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  // F.normalize: x / max(||x||, 1e-12), then * sqrt(C) * gamma
+  const float inv = sqrtf((float)C) / fmaxf(sqrtf(s), 1e-12f);
+  if (ok) {
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = v[j] * inv * gamma[g * 8 + j];
+      if (do_silu) t = silu(t);
+      o[j] = f2bf(t);
+    }
+    *(bf16x8*)(y + row * C + g * 8) = o;
+  }
+}
+
+__global__ void vae_input_kernel(const float* z, int Cz, long THW, const float* mean, const float* stdv, bf16* out,
+                                 int Cp) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= THW * Cp) return;
+  const int c = idx % Cp;
+  const long p = idx / Cp;
+  float v = 0.f;
+  if (c < Cz) v = z[c * THW + p] * stdv[c] + mean[c];
+  out[idx] = f2bf(v);
+}
+
+__global__ void vae_output_kernel(const float* in, int Cs, int C, long THW, float* out, int post) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= THW * C) return;
+  const int c = idx / THW;
+  const long p = idx % THW;
+  float v = fminf(fmaxf(in[p * Cs + c], -1.f), 1.f);
+  if (post) v = fminf(fmaxf(v / 2.f + 0.5f, 0.f), 1.f);
+  out[idx] = v;
+}
+
+__global__ __launch_bounds__(256) void softmax_rows_kernel(const float* s, long lds_, bf16* p, long ldp, int n,
+                                                           float scale) {
+  const long row = blockIdx.x;
+  const float* sr = s + row * lds_;
+  __shared__ float red[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  float mx = -INFINITY;
+  for (int i = tid; i < n; i += 256) mx = fmaxf(mx, sr[i]);
+  mx = wave_max(mx);
+  if (lane == 0) red[w] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float sum = 0.f;
+  for (int i = tid; i < n; i += 256) sum += __expf((sr[i] - mx) * scale);
+  sum = wave_sum(sum);
+  if (lane == 0) red[w] = sum;
+  __syncthreads();
+  const float inv = 1.f / (red[0] + red[1] + red[2] + red[3]);
+  for (int i = tid; i < n; i += 256) p[row * ldp + i] = f2bf(__expf((sr[i] - mx) * scale) * inv);
+}
+
+__global__ void transpose_kernel(const bf16* in, long ldi, long si, bf16* out, long ldo, long so, int R, int Cc) {
+  __shared__ bf16 tile[32][33];
+  const long z = blockIdx.z;
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 8 rows per pass
+  for (int i = ty; i < 32; i += 8) {
+    const int r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < R && c < Cc) ? in[z * si + (long)r * ldi + c] : f2bf(0.f);
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < Cc && r < R) out[z * so + (long)c * ldo + r] = tile[tx][i];
+  }
+}
+
+inline unsigned nblk(long n, int t) { return (unsigned)((n + t - 1) / t); }
+
+}  // namespace
+
+extern "C" int sa_conv3d_cl(const void* x, int T, int H, int W, int Cin, int upsample, const void* w,
+                            const float* bias, int Cout, int Cout_pad, int kt, int kh, int kw, const void* residual,
+                            void* y, int out_f32, int interleave_half, void* stream) {
+  if (!x || !w || !bias || !y || T <= 0 || H <= 0 || W <= 0) return SA_ERR_ARG;
+  if (Cin % BK || Cout % 4 || (kt != 1 && kt != 3) || (kh != 1 && kh != 3) || (kw != 1 && kw != 3)) return SA_ERR_ARG;
+  if (upsample && (H % 2 || W % 2)) return SA_ERR_ARG;
+  if (interleave_half > 0 && (Cout != 2 * interleave_half || residual)) return SA_ERR_ARG;
+  ConvArgs a{(const bf16*)x, T, H, W, Cin, upsample ? H / 2 : H, upsample ? W / 2 : W, upsample, (const bf16*)w,
+             bias, Cout, kt, kh, kw, (const bf16*)residual, y, out_f32, interleave_half, (long)T * H * W};
+  hipStream_t st = (hipStream_t)stream;
+  // N tile chosen so the packed weight rows (Cout_pad) cover whole tiles
+  if (Cout_pad % 192 == 0 && Cout > 96) return launch_conv<12>(a, st);
+  if (Cout_pad % 96 == 0 && Cout > 16) return launch_conv<6>(a, st);
+  if (Cout_pad % 16 == 0 && Cout <= 16) return launch_conv<1>(a, st);
+  return SA_ERR_ARG;
+}
+
+extern "C" int sa_vae_rmsnorm_silu(const void* x, void* y, const float* gamma, int64_t rows, int C, int do_silu,
+                                   void* stream) {
+  if (!x || !y || !gamma || C % 8 || C > 512) return SA_ERR_ARG;
+  const int g8 = C / 8;
+  hipStream_t st = (hipStream_t)stream;
+  if (g8 <= 16) {
+    hipLaunchKernelGGL(rmsnorm_silu_kernel<16>, dim3(nblk(rows, 16)), dim3(256), 0, st, (const bf16*)x, (bf16*)y,
+                       gamma, (long)rows, C, do_silu);
+  } else if (g8 <= 32) {
+    hipLaunchKernelGGL(rmsnorm_silu_kernel<32>, dim3(nblk(rows, 8)), dim3(256), 0, st, (const bf16*)x, (bf16*)y,
+                       gamma, (long)rows, C, do_silu);
+  } else {
+    hipLaunchKernelGGL(rmsnorm_silu_kernel<64>, dim3(nblk(rows, 4)), dim3(256), 0, st, (const bf16*)x, (bf16*)y,
+                       gamma, (long)rows, C, do_silu);
+  }
+  SA_LAUNCH_CHECK();
+  return SA_OK;
+}
+
+extern "C" int sa_vae_input(const float* z, int Cz, int64_t THW, const float* mean, const float* stdv, void* out,
+                            int Cp, void* stream) {
+  if (!z || !out || Cp < Cz) return SA_ERR_ARG;
+  hipLaunchKernelGGL(vae_input_kernel, dim3(nblk(THW * Cp, 256)), dim3(256), 0, (hipStream_t)stream, z, Cz, THW,
+                     mean, stdv, (bf16*)out, Cp);
+  SA_LAUNCH_CHECK();
+  return SA_OK;
+}
+
+extern "C" int sa_vae_output(const float* in, int C_stride, int C, int64_t THW, float* out, int post, void* stream) {
+  if (!in || !out || C > C_stride) return SA_ERR_ARG;
+  hipLaunchKernelGGL(vae_output_kernel, dim3(nblk(THW * C, 256)), dim3(256), 0, (hipStream_t)stream, in, C_stride, C,
+                     THW, out, post);
+  SA_LAUNCH_CHECK();
+  return SA_OK;
+}
+
+extern "C" int sa_softmax_rows(const float* s, int64_t ld_s, void* p, int64_t ld_p, int64_t rows, int n, float scale,
+                               void* stream) {
+  if (!s || !p || rows <= 0 || n <= 0) return SA_ERR_ARG;
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, s, ld_s, (bf16*)p,
+                     ld_p, n, scale);
+  SA_LAUNCH_CHECK();
+  return SA_OK;
+}
+
+extern "C" int sa_transpose_bf16(const void* in, int64_t ld_in, int64_t stride_in, void* out, int64_t ld_out,
+                                 int64_t stride_out, int rows, int cols, int batch, void* stream) {
+  if (!in || !out) return SA_ERR_ARG;
+  dim3 grid(nblk(cols, 32), nblk(rows, 32), batch);
+  hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const bf16*)in, ld_in, stride_in,
+                     (bf16*)out, ld_out, stride_out, rows, cols);
+  SA_LAUNCH_CHECK();
+  return SA_OK;
+}

@@ -68,7 +68,39 @@ def main(which=("gemm", "attn")):
         res.append({"kernel": "attn_self", "L": L, "ms": round(ms, 3), "tflops": round(fl / ms / 1e9, 1),
                     "torch_sdpa_ms": round(ms_ref, 3), "torch_tflops": round(fl / ms_ref / 1e9, 1)})
         print(json.dumps(res[-1]), flush=True)
+    if "dit" in which:
+        res.append(bench_dit())
+        print(json.dumps(res[-1]), flush=True)
     return res
+
+
+def bench_dit(iters=3):
+    """One full 30-layer DiT forward at config 2 (B=3 CFG, 21 latent frames at 64x64, L=21504)."""
+    from . import synthetic
+    from .transformer import WanTransformer3DFantasyModel, param_shapes
+    cfg = dict(model_type="i2v", dim=1536, ffn_dim=8960, freq_dim=256, text_dim=4096, in_dim=36, out_dim=16,
+               num_heads=12, num_layers=30, text_len=512)
+    dev = "cuda"
+    m = WanTransformer3DFantasyModel(**cfg)
+    m.load_state_dict(synthetic.fill_state_dict(param_shapes(cfg), 0, backend="torch", device=dev))
+    m = m.to(dev)
+    g = torch.Generator(device=dev).manual_seed(0)
+    lat = torch.randn(1, 16, 21, 64, 64, device=dev, generator=g).bfloat16()
+    y = torch.randn(3, 20, 21, 64, 64, device=dev, generator=g).bfloat16()
+    ctx = [torch.randn(n, 4096, device=dev, generator=g) for n in (120, 120, 60)]
+    clip = torch.randn(3, 257, 1280, device=dev, generator=g)
+    voc = torch.randn(3, 167, 768, device=dev, generator=g)
+    t = torch.tensor([990.0], device=dev)
+
+    def fwd():
+        return m.forward_window(lat, 0, True, 3, t, ctx, 21504, clip, y, voc, 81)
+
+    with torch.no_grad():
+        ms = _time(fwd, iters=iters, warmup=1)
+    from .flops import dit_forward_flops
+    fl = dit_forward_flops()
+    return {"kernel": "dit_forward", "ms": round(ms, 2), "tflop": round(fl / 1e12, 1),
+            "tflops": round(fl / ms / 1e9, 1)}
 
 
 if __name__ == "__main__":

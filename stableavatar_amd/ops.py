@@ -141,11 +141,20 @@ def small_linear_f32(x, weight, bias, out, act_in=0, act_out=0):
     return out
 
 
-def mod_add(mod, e, out):
-    """out[l,b,j,c] = mod[l,j,c] + e[b,j,c]."""
+def mod_add(mod, e, out, e_jstride=None):
+    """out[l,b,j,c] = mod[l,j,c] + e[b,j,c]  (e 2-D [B, C] with e_jstride=0 broadcasts over j)."""
     L, J, C = mod.shape
     B = e.shape[0]
-    call("sa_mod_add", mod.data_ptr(), e.data_ptr(), out.data_ptr(), L, B, J, C, _stream())
+    ej = e.stride(1) if e_jstride is None else e_jstride
+    call("sa_mod_add", mod.data_ptr(), e.data_ptr(), e.stride(0), ej, out.data_ptr(), L, B, J, C, _stream())
+    return out
+
+
+def attention_small(q, k, v, out, segs, nseg, max_q_len, max_kv_len, heads, head_dim, scale=None):
+    if scale is None:
+        scale = head_dim ** -0.5
+    call("sa_attn_small", q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), segs.data_ptr(), nseg, max_q_len,
+         max_kv_len, heads, head_dim, q.stride(0), k.stride(0), v.stride(0), out.stride(0), float(scale), _stream())
     return out
 
 

@@ -1,7 +1,29 @@
-"""Drop-in WanTransformer3DFantasyModel (reference: wan/models/wan_fantasy_transformer3d_1B.py)."""
+"""Drop-in WanTransformer3DFantasyModel for MI355X (reference:
+wan/models/wan_fantasy_transformer3d_1B.py + wan/models/vocal_projector_fantasy_1B.py).
+
+Same constructor arguments, state_dict keys, `from_pretrained(...)` and
+`forward(x, t, context, seq_len, clip_fea, y, cond_flag, vocal_embeddings, is_clip_level_modeling,
+video_sample_n_frames)` as the reference; every op of the forward runs as a HIP kernel from
+libstableavatar_hip.so (there is no eager/CPU fallback).
+
+Residual stream is kept in fp32 ([B*L, dim], rows = batch-major tokens), GEMM operands in bf16,
+norms/softmax/RoPE in fp32.  Weights are re-packed once per load into fused layouts:
+self-attn QKV [3*dim, dim]; cross-attn text/img/vocal K|V [2*dim, dim]; patch embedding as a
+[dim, 192] GEMM (K padded from 144).  Step-invariant cross-attention K/V of the text and image
+context are cached across forwards (they depend only on the prompt and reference image).
+"""
 from __future__ import annotations
 
+import glob
+import json
+import math
+import os
+from types import SimpleNamespace
+
 import torch
+import torch.nn as nn
+
+from . import ops
 
 
 def rope_params(max_seq_len: int, dim: int, theta: float = 10000.0) -> torch.Tensor:
@@ -17,3 +39,564 @@ def rope_table(head_dim: int = 128, max_seq_len: int = 1024) -> torch.Tensor:
     ang = torch.cat([rope_params(max_seq_len, d - 4 * (d // 6)), rope_params(max_seq_len, 2 * (d // 6)),
                      rope_params(max_seq_len, 2 * (d // 6))], dim=1)
     return torch.stack([torch.cos(ang), torch.sin(ang)], -1).float().contiguous()
+
+
+def split_audio_sequence(audio_proj_length, num_frames=81):
+    """vocal_projector_fantasy.py:39-78 (same integer arithmetic)."""
+    tokens_per_frame = audio_proj_length / num_frames
+    half = int(tokens_per_frame * 4 / 2)
+    pos = []
+    for i in range(int((num_frames - 1) / 4) + 1):
+        if i == 0:
+            pos.append(0)
+        else:
+            st = tokens_per_frame * ((i - 1) * 4 + 1)
+            en = tokens_per_frame * (i * 4 + 1)
+            pos.append(int((st + en) / 2) - 1)
+    ranges = [[p - half, p + half] for p in pos]
+    ranges[0] = [-(half * 2 - ranges[1][0]), ranges[1][0]]
+    return ranges
+
+
+def split_rows(audio_len, num_frames, expand_length=4):
+    """Gather table of split_tensor_with_padding (vocal_projector_fantasy.py:81-131): per latent
+    frame the source token rows, then -1 (zero rows) for front AND back padding, both appended."""
+    rows = []
+    for s, e in split_audio_sequence(audio_len, num_frames):
+        s, e = s - expand_length, e + expand_length
+        mx = audio_len - 1
+        pad = max(-s, 0) + max(e - mx, 0)
+        vs, ve = max(s, 0), min(e, mx)
+        rows.append((list(range(vs, ve + 1)) if vs <= ve else []) + [-1] * pad)
+    return rows
+
+
+def param_shapes(cfg: dict) -> dict:
+    """{state_dict key: shape} of the reference WanTransformer3DFantasyModel (1B:829-872)."""
+    dim, ffn, L = cfg["dim"], cfg["ffn_dim"], cfg["num_layers"]
+    S = {"patch_embedding.weight": (dim, cfg["in_dim"], 1, 2, 2), "patch_embedding.bias": (dim,),
+         "text_embedding.0.weight": (dim, cfg["text_dim"]), "text_embedding.0.bias": (dim,),
+         "text_embedding.2.weight": (dim, dim), "text_embedding.2.bias": (dim,),
+         "time_embedding.0.weight": (dim, cfg["freq_dim"]), "time_embedding.0.bias": (dim,),
+         "time_embedding.2.weight": (dim, dim), "time_embedding.2.bias": (dim,),
+         "time_projection.1.weight": (6 * dim, dim), "time_projection.1.bias": (6 * dim,)}
+    for i in range(L):
+        p = f"blocks.{i}"
+        S[p + ".modulation"] = (1, 6, dim)
+        for n in ("q", "k", "v", "o"):
+            S[f"{p}.self_attn.{n}.weight"] = (dim, dim)
+            S[f"{p}.self_attn.{n}.bias"] = (dim,)
+        S[p + ".self_attn.norm_q.weight"] = (dim,)
+        S[p + ".self_attn.norm_k.weight"] = (dim,)
+        S[p + ".norm3.weight"] = (dim,)
+        S[p + ".norm3.bias"] = (dim,)
+        for n in ("q", "k", "v", "o", "k_img", "v_img", "k_vocal", "v_vocal"):
+            S[f"{p}.cross_attn.{n}.weight"] = (dim, dim)
+            S[f"{p}.cross_attn.{n}.bias"] = (dim,)
+        for n in ("norm_q", "norm_k", "norm_k_img"):
+            S[f"{p}.cross_attn.{n}.weight"] = (dim,)
+        S[p + ".ffn.0.weight"] = (ffn, dim)
+        S[p + ".ffn.0.bias"] = (ffn,)
+        S[p + ".ffn.2.weight"] = (dim, ffn)
+        S[p + ".ffn.2.bias"] = (dim,)
+    S["head.modulation"] = (1, 2, dim)
+    S["head.head.weight"] = (cfg["out_dim"] * 4, dim)
+    S["head.head.bias"] = (cfg["out_dim"] * 4,)
+    if cfg.get("model_type", "i2v") == "i2v":
+        S.update({"img_emb.proj.0.weight": (1280,), "img_emb.proj.0.bias": (1280,),
+                  "img_emb.proj.1.weight": (1280, 1280), "img_emb.proj.1.bias": (1280,),
+                  "img_emb.proj.3.weight": (dim, 1280), "img_emb.proj.3.bias": (dim,),
+                  "img_emb.proj.4.weight": (dim,), "img_emb.proj.4.bias": (dim,)})
+    vp = "vocal_projector"
+    S[vp + ".proj_model.proj.weight"] = (1536, 768)
+    S[vp + ".proj_model.norm.weight"] = (1536,)
+    S[vp + ".proj_model.norm.bias"] = (1536,)
+    for i in range(2):
+        bp = f"{vp}.blocks.{i}"
+        S[bp + ".modulation"] = (1, 6, 1536)
+        S[bp + ".norm3.weight"] = (1536,)
+        S[bp + ".norm3.bias"] = (1536,)
+        for n in ("q", "o"):
+            S[f"{bp}.cross_attn.{n}.weight"] = (1536, 1536)
+            S[f"{bp}.cross_attn.{n}.bias"] = (1536,)
+        for n in ("k", "v"):
+            S[f"{bp}.cross_attn.{n}.weight"] = (1536, dim)
+            S[f"{bp}.cross_attn.{n}.bias"] = (1536,)
+        S[bp + ".cross_attn.norm_q.weight"] = (1536,)
+        S[bp + ".cross_attn.norm_k.weight"] = (1536,)
+        S[bp + ".ffn.0.weight"] = (3072, 1536)
+        S[bp + ".ffn.0.bias"] = (3072,)
+        S[bp + ".ffn.2.weight"] = (1536, 3072)
+        S[bp + ".ffn.2.bias"] = (1536,)
+    S[vp + ".final_head.modulation"] = (1, 2, 1536)
+    S[vp + ".final_head.final_proj.weight"] = (1536, 1536)
+    S[vp + ".final_head.final_proj.bias"] = (1536,)
+    return S
+
+
+def _register_tree(root: nn.Module, shapes: dict, dtype):
+    for name, shp in shapes.items():
+        *path, leaf = name.split(".")
+        mod = root
+        for p in path:
+            if not hasattr(mod, p) or not isinstance(getattr(mod, p), nn.Module):
+                mod.add_module(p, nn.Module())
+            mod = getattr(mod, p)
+        mod.register_parameter(leaf, nn.Parameter(torch.empty(shp, dtype=dtype), requires_grad=False))
+
+
+class _Seg:
+    """Cache of device segment tables {q_row0, q_len, kv_row0, kv_len} for sa_attn_fwd."""
+
+    def __init__(self):
+        self._c = {}
+
+    def get(self, key, rows, device):
+        t = self._c.get(key)
+        if t is None or t.device != device:
+            t = torch.tensor(rows, dtype=torch.int32).reshape(-1, 4).to(device)
+            self._c[key] = t
+        return t
+
+
+class WanTransformer3DFantasyModel(nn.Module):
+    """Audio-driven Wan-2.1 DiT (1B:741-1184) on HIP kernels."""
+
+    def __init__(self, model_type="i2v", patch_size=(1, 2, 2), text_len=512, in_dim=16, dim=2048, ffn_dim=8192,
+                 freq_dim=256, text_dim=4096, out_dim=16, num_heads=16, num_layers=32, window_size=(-1, -1),
+                 qk_norm=True, cross_attn_norm=True, eps=1e-6, in_channels=16, hidden_size=2048, **_):
+        super().__init__()
+        assert model_type in ("t2v", "i2v")
+        if tuple(patch_size) != (1, 2, 2) or not qk_norm or not cross_attn_norm:
+            raise ValueError("the StableAvatar path uses patch (1,2,2), qk_norm and cross_attn_norm (1B:1234-1237)")
+        if tuple(window_size) != (-1, -1):
+            raise ValueError("windowed attention is not part of the inference path")
+        assert dim % num_heads == 0 and dim // num_heads == 128, "HIP attention kernel is built for head_dim 128"
+        self.model_type = model_type
+        self.patch_size = tuple(patch_size)
+        self.text_len, self.in_dim, self.dim, self.ffn_dim = text_len, in_dim, dim, ffn_dim
+        self.freq_dim, self.text_dim, self.out_dim = freq_dim, text_dim, out_dim
+        self.num_heads, self.num_layers, self.eps = num_heads, num_layers, eps
+        self.d = dim // num_heads
+        self.config = SimpleNamespace(model_type=model_type, patch_size=self.patch_size, text_len=text_len,
+                                      in_dim=in_dim, dim=dim, ffn_dim=ffn_dim, freq_dim=freq_dim, text_dim=text_dim,
+                                      out_dim=out_dim, num_heads=num_heads, num_layers=num_layers,
+                                      window_size=window_size, qk_norm=qk_norm, cross_attn_norm=cross_attn_norm,
+                                      eps=eps, in_channels=in_channels, hidden_size=hidden_size)
+        self._cfg = dict(model_type=model_type, dim=dim, ffn_dim=ffn_dim, freq_dim=freq_dim, text_dim=text_dim,
+                         in_dim=in_dim, out_dim=out_dim, num_heads=num_heads, num_layers=num_layers,
+                         text_len=text_len)
+        _register_tree(self, param_shapes(self._cfg), torch.float32)
+        self.sp_world_size, self.sp_world_rank, self.sp_group = 1, 0, None
+        self.teacache = None
+        self._packed = None
+        self._ws = {}
+        self._ctx_cache = None
+        self._segs = _Seg()
+        self._split_cache = {}
+        self._events = None  # optional list to record (start, end) events around self-attention
+
+    # ------------------------------------------------------------------ loading
+
+    @classmethod
+    def from_config(cls, config, **kw):
+        import inspect
+        p = set(inspect.signature(cls.__init__).parameters) - {"self"}
+        return cls(**{k: v for k, v in {**config, **kw}.items() if k in p})
+
+    @classmethod
+    def from_pretrained(cls, pretrained_model_path, subfolder=None, transformer_additional_kwargs={},
+                        low_cpu_mem_usage=False, torch_dtype=torch.bfloat16):
+        """Same directory contract as 1B:1210-1339: config.json + diffusion_pytorch_model
+        .bin/.safetensors or sharded *.safetensors; dict_mapping; forced patch/qk/cross norms;
+        size-mismatched keys skipped; patch_embedding in_dim widening zero-filled."""
+        if subfolder is not None:
+            pretrained_model_path = os.path.join(pretrained_model_path, subfolder)
+        cfg_file = os.path.join(pretrained_model_path, "config.json")
+        if not os.path.isfile(cfg_file):
+            raise RuntimeError(f"{cfg_file} does not exist")
+        with open(cfg_file) as f:
+            config = json.load(f)
+        kw = dict(transformer_additional_kwargs)
+        for key, target in kw.pop("dict_mapping", {}).items():
+            kw[target] = config[key]
+        kw.update(patch_size=(1, 2, 2), qk_norm=True, window_size=(-1, -1), cross_attn_norm=True)
+        model = cls.from_config(config, **kw)
+        bin_file = os.path.join(pretrained_model_path, "diffusion_pytorch_model.bin")
+        st_file = bin_file.replace(".bin", ".safetensors")
+        if os.path.exists(bin_file):
+            sd = torch.load(bin_file, map_location="cpu", weights_only=True)
+        else:
+            from safetensors.torch import load_file
+            files = [st_file] if os.path.exists(st_file) else sorted(
+                glob.glob(os.path.join(pretrained_model_path, "*.safetensors")))
+            sd = {}
+            for fn in files:
+                sd.update(load_file(fn))
+        own = model.state_dict()
+        pe = "patch_embedding.weight"
+        if pe in sd and sd[pe].shape != own[pe].shape and sd[pe].shape[1] < own[pe].shape[1]:
+            w = torch.zeros(own[pe].shape, dtype=sd[pe].dtype)
+            w[:, :sd[pe].shape[1]] = sd[pe]
+            sd[pe] = w
+        sd = {k: v for k, v in sd.items() if k in own and own[k].shape == v.shape}
+        model.load_state_dict(sd, strict=False)
+        return model.to(torch_dtype)
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        self._packed = None
+        self._ctx_cache = None
+        return super().load_state_dict(state_dict, strict=strict, assign=assign)
+
+    def _apply(self, fn, recurse=True):
+        self._packed = None
+        self._ctx_cache = None
+        self._ws = {}
+        return super()._apply(fn, recurse)
+
+    def enable_teacache(self, *a, **k):
+        raise NotImplementedError("TeaCache changes the numerics and is out of scope (SURVEY.md §2 #11)")
+
+    def disable_teacache(self):
+        self.teacache = None
+
+    def enable_multi_gpus_inference(self, group=None):
+        """Ulysses sequence parallelism over torch.distributed (RCCL); replaces the xfuser path
+        installed at 1B:918-923 with single-GPU semantics."""
+        import torch.distributed as dist
+        self.sp_group = group
+        self.sp_world_size = dist.get_world_size(group)
+        self.sp_world_rank = dist.get_rank(group)
+
+    # ------------------------------------------------------------------ packing
+
+    def _pack(self):
+        if self._packed is not None:
+            return self._packed
+        dev = self.patch_embedding.weight.device
+        if dev.type != "cuda":
+            raise RuntimeError("WanTransformer3DFantasyModel runs on the MI355X HIP kernels: move it to 'cuda'")
+        P = dict(self.named_parameters())
+        bf = lambda n: P[n].detach().to(torch.bfloat16).contiguous()  # noqa: E731
+        f32 = lambda n: P[n].detach().float().contiguous()  # noqa: E731
+        cat_bf = lambda *ns: torch.cat([P[n].detach() for n in ns], 0).to(torch.bfloat16).contiguous()  # noqa: E731
+        cat_f = lambda *ns: torch.cat([P[n].detach() for n in ns], 0).float().contiguous()  # noqa: E731
+        dim = self.dim
+        pk = SimpleNamespace()
+        kin = self.in_dim * 4
+        pk.kpad = ((kin + 63) // 64) * 64
+        wpe = torch.zeros(dim, pk.kpad, device=dev, dtype=torch.bfloat16)
+        wpe[:, :kin] = P["patch_embedding.weight"].detach().reshape(dim, kin).to(torch.bfloat16)
+        pk.w_pe, pk.b_pe = wpe, f32("patch_embedding.bias")
+        tkpad = ((self.text_dim + 63) // 64) * 64
+        pk.text_kpad = tkpad
+        w0 = torch.zeros(dim, tkpad, device=dev, dtype=torch.bfloat16)
+        w0[:, :self.text_dim] = P["text_embedding.0.weight"].detach().to(torch.bfloat16)
+        pk.w_t0, pk.b_t0 = w0, f32("text_embedding.0.bias")
+        pk.w_t2, pk.b_t2 = bf("text_embedding.2.weight"), f32("text_embedding.2.bias")
+        pk.w_te0, pk.b_te0 = bf("time_embedding.0.weight"), f32("time_embedding.0.bias")
+        pk.w_te2, pk.b_te2 = bf("time_embedding.2.weight"), f32("time_embedding.2.bias")
+        pk.w_tp, pk.b_tp = bf("time_projection.1.weight"), f32("time_projection.1.bias")
+        pk.mod = torch.cat([P[f"blocks.{i}.modulation"].detach() for i in range(self.num_layers)], 0).float().contiguous()
+        pk.layers = []
+        for i in range(self.num_layers):
+            p = f"blocks.{i}."
+            L = SimpleNamespace()
+            L.w_qkv = cat_bf(p + "self_attn.q.weight", p + "self_attn.k.weight", p + "self_attn.v.weight")
+            L.b_qkv = cat_f(p + "self_attn.q.bias", p + "self_attn.k.bias", p + "self_attn.v.bias")
+            L.nq, L.nk = f32(p + "self_attn.norm_q.weight"), f32(p + "self_attn.norm_k.weight")
+            L.w_o, L.b_o = bf(p + "self_attn.o.weight"), f32(p + "self_attn.o.bias")
+            L.n3w, L.n3b = f32(p + "norm3.weight"), f32(p + "norm3.bias")
+            c = p + "cross_attn."
+            L.w_cq, L.b_cq = bf(c + "q.weight"), f32(c + "q.bias")
+            L.cnq, L.cnk, L.cnki = f32(c + "norm_q.weight"), f32(c + "norm_k.weight"), f32(c + "norm_k_img.weight")
+            L.w_kv_t, L.b_kv_t = cat_bf(c + "k.weight", c + "v.weight"), cat_f(c + "k.bias", c + "v.bias")
+            L.w_kv_i, L.b_kv_i = cat_bf(c + "k_img.weight", c + "v_img.weight"), cat_f(c + "k_img.bias", c + "v_img.bias")
+            L.w_kv_v, L.b_kv_v = (cat_bf(c + "k_vocal.weight", c + "v_vocal.weight"),
+                                  cat_f(c + "k_vocal.bias", c + "v_vocal.bias"))
+            L.w_co, L.b_co = bf(c + "o.weight"), f32(c + "o.bias")
+            L.w_f0, L.b_f0 = bf(p + "ffn.0.weight"), f32(p + "ffn.0.bias")
+            L.w_f2, L.b_f2 = bf(p + "ffn.2.weight"), f32(p + "ffn.2.bias")
+            pk.layers.append(L)
+        pk.head_mod = f32("head.modulation").reshape(1, 2, dim)
+        pk.w_head, pk.b_head = bf("head.head.weight"), f32("head.head.bias")
+        if self.model_type == "i2v":
+            pk.ie0w, pk.ie0b = f32("img_emb.proj.0.weight"), f32("img_emb.proj.0.bias")
+            pk.w_ie1, pk.b_ie1 = bf("img_emb.proj.1.weight"), f32("img_emb.proj.1.bias")
+            pk.w_ie3, pk.b_ie3 = bf("img_emb.proj.3.weight"), f32("img_emb.proj.3.bias")
+            pk.ie4w, pk.ie4b = f32("img_emb.proj.4.weight"), f32("img_emb.proj.4.bias")
+        vp = "vocal_projector."
+        V = SimpleNamespace()
+        V.w_proj = bf(vp + "proj_model.proj.weight")
+        V.nw, V.nb = f32(vp + "proj_model.norm.weight"), f32(vp + "proj_model.norm.bias")
+        V.mod = torch.cat([P[f"{vp}blocks.{i}.modulation"].detach() for i in range(2)], 0).float().contiguous()
+        V.blocks = []
+        for i in range(2):
+            b = f"{vp}blocks.{i}."
+            B_ = SimpleNamespace()
+            B_.n3w, B_.n3b = f32(b + "norm3.weight"), f32(b + "norm3.bias")
+            B_.w_q, B_.b_q = bf(b + "cross_attn.q.weight"), f32(b + "cross_attn.q.bias")
+            B_.w_kv = cat_bf(b + "cross_attn.k.weight", b + "cross_attn.v.weight")
+            B_.b_kv = cat_f(b + "cross_attn.k.bias", b + "cross_attn.v.bias")
+            B_.nq, B_.nk = f32(b + "cross_attn.norm_q.weight"), f32(b + "cross_attn.norm_k.weight")
+            B_.w_o, B_.b_o = bf(b + "cross_attn.o.weight"), f32(b + "cross_attn.o.bias")
+            B_.w_f0, B_.b_f0 = bf(b + "ffn.0.weight"), f32(b + "ffn.0.bias")
+            B_.w_f2, B_.b_f2 = bf(b + "ffn.2.weight"), f32(b + "ffn.2.bias")
+            V.blocks.append(B_)
+        V.fmod = f32(vp + "final_head.modulation").reshape(1, 2, 1536)
+        V.w_fp, V.b_fp = bf(vp + "final_head.final_proj.weight"), f32(vp + "final_head.final_proj.bias")
+        pk.vocal = V
+        pk.rope = rope_table(self.d).to(dev)
+        self._packed = pk
+        return pk
+
+    # ------------------------------------------------------------------ workspace
+
+    def _workspace(self, M, dev):
+        key = (M, dev)
+        ws = self._ws.get(key)
+        if ws is None:
+            dim = self.dim
+            ws = SimpleNamespace(
+                x=torch.empty(M, dim, device=dev, dtype=torch.float32),
+                mod=torch.empty(M, dim, device=dev, dtype=torch.bfloat16),
+                qkv=torch.empty(M, 3 * dim, device=dev, dtype=torch.bfloat16),
+                att=torch.empty(M, dim, device=dev, dtype=torch.bfloat16),
+                ffn=torch.empty(M, self.ffn_dim, device=dev, dtype=torch.bfloat16),
+            )
+            self._ws = {key: ws}  # keep one shape at a time
+        return ws
+
+    # ------------------------------------------------------------------ context (step-invariant)
+
+    def _context(self, pk, context, clip_fea, B, dev):
+        key = tuple((c.data_ptr(), c._version, tuple(c.shape)) for c in context)
+        key += ((clip_fea.data_ptr(), clip_fea._version, tuple(clip_fea.shape)) if clip_fea is not None else (),)
+        if self._ctx_cache is not None and self._ctx_cache[0] == key:
+            return self._ctx_cache[1]
+        dim, tl = self.dim, self.text_len
+        # text: pad each prompt to text_len with zeros (the pads are attended, 1B:993-999)
+        tin = torch.zeros(B, tl, pk.text_kpad, device=dev, dtype=torch.bfloat16)
+        for b, c in enumerate(context):
+            tin[b, :c.shape[0], :c.shape[1]] = c.to(device=dev, dtype=torch.bfloat16)
+        h = ops.linear(tin.view(B * tl, pk.text_kpad), pk.w_t0, pk.b_t0, ops.EPI_GELU_TANH_BF16)
+        ctx_t = ops.linear(h, pk.w_t2, pk.b_t2, ops.EPI_BF16)
+        # image: MLPProj (1B:726-738): LN(1280) -> Linear -> GELU(erf) -> Linear -> LN(dim)
+        ni = 0
+        if self.model_type == "i2v":
+            ni = clip_fea.shape[1]
+            cf = clip_fea.to(device=dev, dtype=torch.float32).reshape(B * ni, -1).contiguous()
+            cn = torch.empty(B * ni, cf.shape[1], device=dev, dtype=torch.bfloat16)
+            ops.layernorm_mod(cf, cn, 1e-5, weight=pk.ie0w, bias=pk.ie0b)
+            h1 = ops.linear(cn, pk.w_ie1, pk.b_ie1, ops.EPI_GELU_ERF_BF16)
+            h3 = ops.linear(h1, pk.w_ie3, pk.b_ie3, ops.EPI_F32)
+            ctx_i = torch.empty(B * ni, dim, device=dev, dtype=torch.bfloat16)
+            ops.layernorm_mod(h3, ctx_i, 1e-5, weight=pk.ie4w, bias=pk.ie4b)
+        kv = []
+        for L in pk.layers:
+            kvt = ops.linear(ctx_t, L.w_kv_t, L.b_kv_t, ops.EPI_BF16)      # [B*tl, 2dim] = k | v
+            ops.qk_rmsnorm_rope(kvt, 0, -1, L.cnk, None, dim, self.eps)
+            kvi = None
+            if ni:
+                kvi = ops.linear(ctx_i, L.w_kv_i, L.b_kv_i, ops.EPI_BF16)
+                ops.qk_rmsnorm_rope(kvi, 0, -1, L.cnki, None, dim, self.eps)
+            kv.append((kvt, kvi))
+        out = SimpleNamespace(kv=kv, text_len=tl, img_len=ni)
+        self._ctx_cache = (key, out)
+        return out
+
+    # ------------------------------------------------------------------ vocal projector
+
+    def _vocal(self, pk, vocal_embeddings, n_frames, lat_bf16, Lq, e0_row, e_row, dev):
+        """FantasyTalkingVocalCondition1BModel.forward (vocal_projector_fantasy_1B.py:433-450) for one
+        audio row; lat_bf16 = patch-embedded tokens of that row [Lq, dim]. Returns [F*n, 1536] bf16."""
+        V = pk.vocal
+        va = vocal_embeddings.to(device=dev, dtype=torch.bfloat16).contiguous()
+        Na = va.shape[0]
+        feat = ops.linear(va, V.w_proj, None, ops.EPI_F32)
+        ops.layernorm_mod(feat, feat, 1e-5, weight=V.nw, bias=V.nb)
+        key = (Na, n_frames)
+        rows = self._split_cache.get(key)
+        if rows is None:
+            r = split_rows(Na, n_frames)
+            rows = (torch.tensor([i for row in r for i in row], dtype=torch.int32, device=dev), len(r), len(r[0]))
+            self._split_cache[key] = rows
+        idx, Fn, nper = rows
+        x = torch.empty(Fn * nper, 1536, device=dev, dtype=torch.float32)
+        ops.gather_rows(feat, idx, x)
+        em = torch.empty(2, 1, 6, 1536, device=dev, dtype=torch.float32)
+        ops.mod_add(V.mod, e0_row, em)
+        Mv = Fn * nper
+        hb = torch.empty(Mv, 1536, device=dev, dtype=torch.bfloat16)
+        G = Lq // Fn
+        segs = self._segs.get(("vp", Fn, nper, G), [[f * nper, nper, f * G, G] for f in range(Fn)], dev)
+        for i, B_ in enumerate(V.blocks):
+            e = em[i, 0]
+            # "self-attention" branch is x + modulate(LN(x))*e2 (vocal_projector_fantasy_1B.py:345-347)
+            ops.layernorm_mod(x, x, 1e-6, shift=e[0:1], scale=e[1:2], gate=e[2:3], rows_per_batch=Mv)
+            ops.layernorm_mod(x, hb, 1e-6, weight=B_.n3w, bias=B_.n3b)
+            q = ops.linear(hb, B_.w_q, B_.b_q, ops.EPI_BF16)
+            ops.qk_rmsnorm_rope(q, 0, -1, B_.nq, None, 1536, 1e-6)
+            kv = ops.linear(lat_bf16, B_.w_kv, B_.b_kv, ops.EPI_BF16)
+            ops.qk_rmsnorm_rope(kv, 0, -1, B_.nk, None, 1536, 1e-6)
+            o = torch.empty(Mv, 1536, device=dev, dtype=torch.bfloat16)
+            ops.attention_small(q, kv[:, :1536], kv[:, 1536:], o, segs, Fn, nper, G, 8, 192)
+            ops.linear(o, B_.w_o, B_.b_o, ops.EPI_RES_F32, out=x, residual=x)
+            ops.layernorm_mod(x, hb, 1e-6, shift=e[3:4], scale=e[4:5], rows_per_batch=Mv)
+            h = ops.linear(hb, B_.w_f0, B_.b_f0, ops.EPI_GELU_TANH_BF16)
+            ops.linear(h, B_.w_f2, B_.b_f2, ops.EPI_RES_F32, out=x, residual=x, gate=e[5:6], rows_per_batch=Mv)
+        ef = torch.empty(1, 1, 2, 1536, device=dev, dtype=torch.float32)
+        ops.mod_add(V.fmod, e_row, ef, e_jstride=0)
+        ops.layernorm_mod(x, hb, 1e-6, shift=ef[0, 0, 0:1], scale=ef[0, 0, 1:2], rows_per_batch=Mv)
+        return ops.linear(hb, V.w_fp, V.b_fp, ops.EPI_BF16), Fn, nper
+
+    # ------------------------------------------------------------------ forward
+
+    def forward(self, x, t, context, seq_len, clip_fea=None, y=None, cond_flag=True, vocal_embeddings=None,
+                is_clip_level_modeling=False, video_sample_n_frames=81):
+        """1B:928-1159.  x, y: [B, C, F, H, W] tensors (or lists of [C, F, H, W]); context: list of
+        [L_i, text_dim]; t: [B]; vocal_embeddings: [B, N_audio, 768].  Returns [B, out_dim, F, H, W]
+        (bf16)."""
+        if isinstance(x, (list, tuple)):
+            x = torch.stack(list(x))
+        if isinstance(y, (list, tuple)):
+            y = torch.stack(list(y))
+        return self.forward_window(x, 0, False, x.shape[0], t, context, seq_len, clip_fea, y, vocal_embeddings,
+                                   video_sample_n_frames, is_clip_level_modeling)
+
+    def forward_window(self, lat, frame_offset, broadcast, B, t, context, seq_len, clip_fea, y, vocal_embeddings,
+                       video_sample_n_frames=81, is_clip_level_modeling=False, out=None):
+        """Forward on frames [frame_offset, frame_offset + Fw) of `lat` ([B|1, C, T, H, W]); with
+        broadcast=True one latent row feeds all B CFG rows (the pipeline's torch.cat([latents]*3))."""
+        if is_clip_level_modeling:
+            raise NotImplementedError("clip-level audio modeling is a training mode (1B:1011-1015)")
+        if self.model_type == "i2v":
+            assert clip_fea is not None and y is not None
+        pk = self._pack()
+        dev = pk.w_pe.device
+        dim, H_ = self.dim, self.num_heads
+        Fw = y.shape[2] if y is not None else lat.shape[2] - frame_offset
+        Hh, Ww = lat.shape[3], lat.shape[4]
+        hp, wp = Hh // 2, Ww // 2
+        real = Fw * hp * wp
+        Lp = int(seq_len)
+        if self.sp_world_size > 1:
+            Lp = int(math.ceil(Lp / self.sp_world_size)) * self.sp_world_size
+        assert real <= Lp, "seq_len smaller than the token count"
+        M = B * Lp
+        ws = self._workspace(M, dev)
+
+        # patch embedding (1B:972-983): im2col + GEMM, padding rows zero
+        cols = torch.empty(B, Lp, pk.kpad, device=dev, dtype=torch.bfloat16)
+        ops.patch_im2col(lat, y, B, Fw, Hh, Ww, cols, pk.kpad, Lp, x_frame_offset=frame_offset,
+                         x_batch_broadcast=broadcast)
+        call_gemm_batched(cols, pk.w_pe, pk.b_pe, ws.x, B, real, Lp, dim, pk.kpad)
+        if real < Lp:
+            for b in range(B):
+                ops.fill_(ws.x[b * Lp + real:(b + 1) * Lp], 0.0)
+
+        # time embedding (fp32, 1B:986-990)
+        tt = t.to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
+        if tt.numel() == 1:
+            tt = tt.expand(B).contiguous()
+        sin = torch.empty(B, self.freq_dim, device=dev, dtype=torch.float32)
+        ops.timestep_embed(tt, self.freq_dim, sin)
+        h1 = torch.empty(B, dim, device=dev, dtype=torch.float32)
+        ops.small_linear_f32(sin, pk.w_te0, pk.b_te0, h1, act_out=1)
+        e = torch.empty(B, dim, device=dev, dtype=torch.float32)
+        ops.small_linear_f32(h1, pk.w_te2, pk.b_te2, e)
+        e0 = torch.empty(B, 6 * dim, device=dev, dtype=torch.float32)
+        ops.small_linear_f32(e, pk.w_tp, pk.b_tp, e0, act_in=1)
+        e0 = e0.view(B, 6, dim)
+        emod = torch.empty(self.num_layers, B, 6, dim, device=dev, dtype=torch.float32)
+        ops.mod_add(pk.mod, e0, emod)
+        hmod = torch.empty(1, B, 2, dim, device=dev, dtype=torch.float32)
+        ops.mod_add(pk.head_mod, e, hmod, e_jstride=0)
+
+        ctx = self._context(pk, context, clip_fea, B, dev)
+
+        # vocal context (1B:1004-1009): projector on the last (full-condition) row only
+        n_fr = (video_sample_n_frames - 1) // 4 + 1
+        if Lp % n_fr:
+            raise ValueError("seq_len must split evenly into latent frames for the per-frame audio attention")
+        lat_row = torch.empty(Lp, dim, device=dev, dtype=torch.bfloat16)
+        if vocal_embeddings.shape[0] == 1 and B != 1:
+            raise ValueError("a single audio row drives a batch of 1 (1B:1008-1009); CFG batches pass 3 rows")
+        rows_v = 1 if vocal_embeddings.shape[0] > 1 else B
+        voc_rows = []
+        for r in range(rows_v):
+            src = B - 1 if rows_v == 1 else r
+            ops.cast_bf16(ws.x[src * Lp:(src + 1) * Lp], lat_row)
+            vv, Fn, nper = self._vocal(pk, vocal_embeddings[src], video_sample_n_frames, lat_row, Lp,
+                                       e0[src:src + 1], e[src:src + 1], dev)
+            voc_rows.append(vv)
+        assert Fn == n_fr
+        if rows_v == 1:
+            vctx = torch.zeros(B, Fn * nper, dim, device=dev, dtype=torch.bfloat16)
+            for b in range(1, B):
+                vctx[b].copy_(voc_rows[0])
+        else:
+            vctx = torch.stack(voc_rows)
+        vctx = vctx.view(B * Fn * nper, dim)
+
+        G = Lp // n_fr
+        segs_self = self._segs.get(("self", B, Lp), [[b * Lp, Lp, b * Lp, Lp] for b in range(B)], dev)
+        segs_txt = self._segs.get(("txt", B, Lp, ctx.text_len),
+                                  [[b * Lp, Lp, b * ctx.text_len, ctx.text_len] for b in range(B)], dev)
+        segs_img = self._segs.get(("img", B, Lp, ctx.img_len),
+                                  [[b * Lp, Lp, b * ctx.img_len, ctx.img_len] for b in range(B)], dev)
+        segs_voc = self._segs.get(("voc", B, Lp, n_fr, nper),
+                                  [[b * Lp + f * G, G, (b * n_fr + f) * nper, nper]
+                                   for b in range(B) for f in range(n_fr)], dev)
+        x = ws.x
+        grid = (Fw, hp, wp)
+        for li, L in enumerate(pk.layers):
+            em = emod[li]  # [B, 6, dim]
+            # self-attention (1B:675-679)
+            ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 0], scale=em[:, 1], rows_per_batch=Lp)
+            ops.linear(ws.mod, L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv)
+            ops.qk_rmsnorm_rope(ws.qkv, 0, dim, L.nq, L.nk, dim, self.eps, rope=pk.rope, rows_per_batch=Lp,
+                                grid=grid, head_dim=self.d, n_frame_pairs=self.d // 2 - 2 * (self.d // 6),
+                                n_height_pairs=self.d // 6)
+            if self._events is not None:
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev0.record()
+            ops.attention(ws.qkv[:, :dim], ws.qkv[:, dim:2 * dim], ws.qkv[:, 2 * dim:], ws.att, segs_self, B, Lp, H_)
+            if self._events is not None:
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev1.record()
+                self._events.append((ev0, ev1))
+            ops.linear(ws.att, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2], rows_per_batch=Lp)
+            # cross-attention: text + image + per-frame vocal (1B:534-605, 684)
+            ops.layernorm_mod(x, ws.mod, self.eps, weight=L.n3w, bias=L.n3b)
+            qc = ws.qkv[:, :dim]
+            ops.linear(ws.mod, L.w_cq, L.b_cq, ops.EPI_BF16, out=qc)
+            ops.qk_rmsnorm_rope(qc, 0, -1, L.cnq, None, dim, self.eps)
+            kvt, kvi = ctx.kv[li]
+            ops.attention(qc, kvt[:, :dim], kvt[:, dim:], ws.att, segs_txt, B, Lp, H_)
+            if kvi is not None:
+                ops.attention(qc, kvi[:, :dim], kvi[:, dim:], ws.att, segs_img, B, Lp, H_, accumulate=True)
+            kvv = ws.qkv[:B * n_fr * nper, dim:3 * dim]
+            ops.linear(vctx, L.w_kv_v, L.b_kv_v, ops.EPI_BF16, out=kvv)
+            ops.attention(qc, kvv[:, :dim], kvv[:, dim:], ws.att, segs_voc, B * n_fr, G, H_, accumulate=True)
+            ops.linear(ws.att, L.w_co, L.b_co, ops.EPI_RES_F32, out=x, residual=x)
+            # FFN (1B:687-691)
+            ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 3], scale=em[:, 4], rows_per_batch=Lp)
+            ops.linear(ws.mod, L.w_f0, L.b_f0, ops.EPI_GELU_TANH_BF16, out=ws.ffn)
+            ops.linear(ws.ffn, L.w_f2, L.b_f2, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 5], rows_per_batch=Lp)
+
+        # head (1B:715-723) + unpatchify (1B:1161-1184)
+        hm = hmod[0]
+        ops.layernorm_mod(x, ws.mod, self.eps, shift=hm[:, 0], scale=hm[:, 1], rows_per_batch=Lp)
+        ho = ops.linear(ws.mod, pk.w_head, pk.b_head, ops.EPI_BF16)
+        if out is None:
+            out = torch.empty(B, self.out_dim, Fw, Hh, Ww, device=dev, dtype=torch.bfloat16)
+        ops.unpatchify(ho, Lp, B, self.out_dim, Fw, Hh, Ww, out)
+        return out
+
+
+def call_gemm_batched(cols, w, bias, xout, B, real, Lp, dim, kpad):
+    """patch-embedding GEMM per batch row over its real tokens only (pads stay zero, 1B:983)."""
+    from ._lib import call
+    call("sa_gemm_bf16", cols.data_ptr(), kpad, Lp * kpad, w.data_ptr(), kpad, 0, bias.data_ptr(), xout.data_ptr(),
+         dim, Lp * dim, real, dim, kpad, B, ops.EPI_F32, 0, 0, 0, 0, 0, 0, ops._stream())

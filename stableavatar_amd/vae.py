@@ -1,0 +1,298 @@
+"""Drop-in AutoencoderKLWan decode for MI355X (reference: wan/models/wan_vae.py).
+
+Same state_dict keys ('model.conv2.*', 'model.decoder.*'), `from_pretrained(path, additional_kwargs)`
+and `decode(z, return_dict=True) -> DecoderOutput(sample=...)` as the reference.  The decoder runs
+over the whole clip at once (equivalent to the reference's frame-by-frame causal cache, see
+oracle/vae.py) with channels-last bf16 activations and every conv as an MFMA implicit GEMM.
+Encoding (reference-frame conditioning, once per call) is SURVEY.md §8(f) "next" and not part of
+this hot path.
+"""
+from __future__ import annotations
+
+from types import SimpleNamespace
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from ._lib import call
+
+MEAN = [-0.7571, -0.7089, -0.9113, 0.1075, -0.1745, 0.9653, -0.1517, 1.5508,
+        0.4134, -0.0715, 0.5517, -0.3632, -0.1922, -0.9497, 0.2503, -0.2921]
+STD = [2.8184, 1.4541, 2.3275, 2.6558, 1.2196, 1.7708, 2.6052, 2.0743,
+       3.2687, 2.1526, 2.8652, 1.5579, 1.6382, 1.1253, 2.8251, 1.9160]
+
+
+def decoder_layout(dim=96, z_dim=16, dim_mult=(1, 2, 4, 4), num_res_blocks=2, temperal_upsample=(True, True, False)):
+    """Module list of Decoder3d (wan_vae.py:372-424): (kind, name, in, out)."""
+    dims = [dim * u for u in [dim_mult[-1]] + list(dim_mult[::-1])]
+    L = [("conv", "conv1", z_dim, dims[0]),
+         ("res", "middle.0", dims[0], dims[0]), ("attn", "middle.1", dims[0], dims[0]),
+         ("res", "middle.2", dims[0], dims[0])]
+    k = 0
+    for i, (din, dout) in enumerate(zip(dims[:-1], dims[1:])):
+        if i in (1, 2, 3):
+            din = din // 2
+        for _ in range(num_res_blocks + 1):
+            L.append(("res", f"upsamples.{k}", din, dout))
+            k += 1
+            din = dout
+        if i != len(dim_mult) - 1:
+            L.append(("up3d" if temperal_upsample[i] else "up2d", f"upsamples.{k}", dout, dout // 2))
+            k += 1
+    L.append(("head", "head", dims[-1], 3))
+    return L
+
+
+def param_shapes(dim=96, z_dim=16):
+    """{key: shape} of the decode half of AutoencoderKLWan ('model.' prefix, wan_vae.py:683-704)."""
+    S = {"model.conv2.weight": (z_dim, z_dim, 1, 1, 1), "model.conv2.bias": (z_dim,)}
+    p = "model.decoder."
+    for kind, name, cin, cout in decoder_layout(dim, z_dim):
+        q = p + name
+        if kind == "conv":
+            S[q + ".weight"] = (cout, cin, 3, 3, 3)
+            S[q + ".bias"] = (cout,)
+        elif kind == "res":
+            S[q + ".residual.0.gamma"] = (cin, 1, 1, 1)
+            S[q + ".residual.2.weight"] = (cout, cin, 3, 3, 3)
+            S[q + ".residual.2.bias"] = (cout,)
+            S[q + ".residual.3.gamma"] = (cout, 1, 1, 1)
+            S[q + ".residual.6.weight"] = (cout, cout, 3, 3, 3)
+            S[q + ".residual.6.bias"] = (cout,)
+            if cin != cout:
+                S[q + ".shortcut.weight"] = (cout, cin, 1, 1, 1)
+                S[q + ".shortcut.bias"] = (cout,)
+        elif kind == "attn":
+            S[q + ".norm.gamma"] = (cin, 1, 1)
+            S[q + ".to_qkv.weight"] = (cin * 3, cin, 1, 1)
+            S[q + ".to_qkv.bias"] = (cin * 3,)
+            S[q + ".proj.weight"] = (cin, cin, 1, 1)
+            S[q + ".proj.bias"] = (cin,)
+        elif kind in ("up3d", "up2d"):
+            S[q + ".resample.1.weight"] = (cout, cin, 3, 3)
+            S[q + ".resample.1.bias"] = (cout,)
+            if kind == "up3d":
+                S[q + ".time_conv.weight"] = (cin * 2, cin, 3, 1, 1)
+                S[q + ".time_conv.bias"] = (cin * 2,)
+        elif kind == "head":
+            S[q + ".0.gamma"] = (cin, 1, 1, 1)
+            S[q + ".2.weight"] = (cout, cin, 3, 3, 3)
+            S[q + ".2.bias"] = (cout,)
+    return S
+
+
+def _cout_pad(cout):
+    if cout > 96:
+        return ((cout + 191) // 192) * 192
+    if cout > 16:
+        return ((cout + 95) // 96) * 96
+    return 16
+
+
+def _pack_conv(w, b, cin_pad=None, cout_store=None):
+    """torch conv weight [Cout, Cin, (kt,) kh, kw] -> bf16 [Cout_pad][kt][kh][kw][Cin_pad] + fp32 bias."""
+    w = w.detach().float()
+    if w.dim() == 4:
+        w = w.unsqueeze(2)
+    cout, cin, kt, kh, kw = w.shape
+    cin_p = cin_pad or cin
+    cout_s = cout_store or cout
+    cp = _cout_pad(cout_s)
+    out = torch.zeros(cp, kt, kh, kw, cin_p, device=w.device, dtype=torch.float32)
+    out[:cout, :, :, :, :cin] = w.permute(0, 2, 3, 4, 1)
+    bias = torch.zeros(cp, device=w.device, dtype=torch.float32)
+    bias[:cout] = b.detach().float()
+    return SimpleNamespace(w=out.to(torch.bfloat16).contiguous(), b=bias, cin=cin_p, cout=cout_s, cout_pad=cp,
+                           kt=kt, kh=kh, kw=kw)
+
+
+class DecoderOutput:
+    def __init__(self, sample):
+        self.sample = sample
+
+
+class AutoencoderKLWan(nn.Module):
+    """wan_vae.py:619-704, decode path on HIP kernels."""
+
+    def __init__(self, latent_channels=16, temporal_compression_ratio=4, spacial_compression_ratio=8, dim=96):
+        super().__init__()
+        self.config = SimpleNamespace(latent_channels=latent_channels,
+                                      temporal_compression_ratio=temporal_compression_ratio,
+                                      spacial_compression_ratio=spacial_compression_ratio)
+        self.z_dim, self.dim = latent_channels, dim
+        self.mean = torch.tensor(MEAN, dtype=torch.float32)
+        self.std = torch.tensor(STD, dtype=torch.float32)
+        for name, shp in param_shapes(dim, latent_channels).items():
+            *path, leaf = name.split(".")
+            mod = self
+            for p in path:
+                if not hasattr(mod, p) or not isinstance(getattr(mod, p), nn.Module):
+                    mod.add_module(p, nn.Module())
+                mod = getattr(mod, p)
+            mod.register_parameter(leaf, nn.Parameter(torch.empty(shp), requires_grad=False))
+        self._packed = None
+
+    @property
+    def dtype(self):
+        return torch.float32
+
+    @classmethod
+    def from_pretrained(cls, pretrained_model_path, additional_kwargs={}):
+        import inspect
+        sig = set(inspect.signature(cls.__init__).parameters) - {"self"}
+        model = cls(**{k: v for k, v in additional_kwargs.items() if k in sig})
+        if pretrained_model_path.endswith(".safetensors"):
+            from safetensors.torch import load_file
+            sd = load_file(pretrained_model_path)
+        else:
+            sd = torch.load(pretrained_model_path, map_location="cpu", weights_only=True)
+        sd = {"model." + k: v for k, v in sd.items()}
+        model.load_state_dict(sd, strict=False)
+        return model
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        self._packed = None
+        return super().load_state_dict(state_dict, strict=strict, assign=assign)
+
+    def _apply(self, fn, recurse=True):
+        self._packed = None
+        return super()._apply(fn, recurse)
+
+    def encode(self, x, return_dict=True):
+        raise NotImplementedError("VAE encode (reference-frame conditioning, once per call) is SURVEY.md §8(f) "
+                                  "'next'; pass the conditioning latents `y` directly")
+
+    # ------------------------------------------------------------------ packing
+
+    def _pack(self):
+        if self._packed is not None:
+            return self._packed
+        dev = self.model.conv2.weight.device
+        if dev.type != "cuda":
+            raise RuntimeError("AutoencoderKLWan.decode runs on the MI355X HIP kernels: move it to 'cuda'")
+        P = dict(self.named_parameters())
+        zp = ((self.z_dim + 31) // 32) * 32
+        pk = SimpleNamespace(zp=zp, layers=[])
+        pk.conv2 = _pack_conv(P["model.conv2.weight"], P["model.conv2.bias"], cin_pad=zp, cout_store=zp)
+        pk.mean, pk.std = self.mean.to(dev), self.std.to(dev)
+        g = lambda n: P[n].detach().float().reshape(-1).contiguous()  # noqa: E731
+        for kind, name, cin, cout in decoder_layout(self.dim, self.z_dim):
+            q = "model.decoder." + name
+            e = SimpleNamespace(kind=kind, cin=cin, cout=cout)
+            if kind == "conv":
+                e.conv = _pack_conv(P[q + ".weight"], P[q + ".bias"], cin_pad=zp)
+            elif kind == "res":
+                e.g0, e.g3 = g(q + ".residual.0.gamma"), g(q + ".residual.3.gamma")
+                e.c1 = _pack_conv(P[q + ".residual.2.weight"], P[q + ".residual.2.bias"])
+                e.c2 = _pack_conv(P[q + ".residual.6.weight"], P[q + ".residual.6.bias"])
+                e.sc = (_pack_conv(P[q + ".shortcut.weight"], P[q + ".shortcut.bias"])
+                        if q + ".shortcut.weight" in P else None)
+            elif kind == "attn":
+                e.g = g(q + ".norm.gamma")
+                e.qkv = _pack_conv(P[q + ".to_qkv.weight"], P[q + ".to_qkv.bias"])
+                e.proj = _pack_conv(P[q + ".proj.weight"], P[q + ".proj.bias"])
+            elif kind in ("up3d", "up2d"):
+                e.rs = _pack_conv(P[q + ".resample.1.weight"], P[q + ".resample.1.bias"])
+                if kind == "up3d":
+                    e.tc = _pack_conv(P[q + ".time_conv.weight"], P[q + ".time_conv.bias"])
+            elif kind == "head":
+                e.g = g(q + ".0.gamma")
+                e.conv = _pack_conv(P[q + ".2.weight"], P[q + ".2.bias"], cout_store=4)
+            pk.layers.append(e)
+        self._packed = pk
+        return pk
+
+    # ------------------------------------------------------------------ kernels
+
+    @staticmethod
+    def _conv(x, T, H, W, c, residual=None, upsample=False, out=None, out_f32=False, interleave=0):
+        if out is None:
+            if interleave:
+                out = torch.empty(2 * T, H, W, interleave, device=x.device, dtype=torch.bfloat16)
+            else:
+                out = torch.empty(T, H, W, c.cout, device=x.device,
+                                  dtype=torch.float32 if out_f32 else torch.bfloat16)
+        call("sa_conv3d_cl", x.data_ptr(), T, H, W, c.cin, int(upsample), c.w.data_ptr(), c.b.data_ptr(), c.cout,
+             c.cout_pad, c.kt, c.kh, c.kw, 0 if residual is None else residual.data_ptr(), out.data_ptr(),
+             int(out_f32), interleave, ops._stream())
+        return out
+
+    @staticmethod
+    def _rms(x, gamma, silu):
+        y = torch.empty_like(x)
+        C = x.shape[-1]
+        call("sa_vae_rmsnorm_silu", x.data_ptr(), y.data_ptr(), gamma.data_ptr(), x.numel() // C, C, int(silu),
+             ops._stream())
+        return y
+
+    def _res(self, e, x, T, H, W):
+        h = self._conv(x, T, H, W, e.sc) if e.sc is not None else x
+        y = self._rms(x, e.g0, True)
+        y = self._conv(y, T, H, W, e.c1)
+        y = self._rms(y, e.g3, True)
+        return self._conv(y, T, H, W, e.c2, residual=h)
+
+    def _attn(self, e, x, T, H, W):
+        """AttentionBlock (wan_vae.py:243-265): per-frame single-head attention over H*W tokens."""
+        C = x.shape[-1]
+        HW = H * W
+        y = self._rms(x, e.g, False)
+        qkv = self._conv(y, T, H, W, e.qkv).view(T, HW, 3 * C)
+        q, k, v = qkv[:, :, :C], qkv[:, :, C:2 * C], qkv[:, :, 2 * C:]
+        o = torch.empty(T, HW, C, device=x.device, dtype=torch.bfloat16)
+        vt = torch.empty(T, C, HW, device=x.device, dtype=torch.bfloat16)
+        call("sa_transpose_bf16", v.data_ptr(), v.stride(1), v.stride(0), vt.data_ptr(), HW, C * HW, HW, C, T,
+             ops._stream())
+        chunk = max(1, min(T, (1 << 30) // (HW * HW * 6)))  # bound the fp32 score buffer
+        s = torch.empty(chunk, HW, HW, device=x.device, dtype=torch.float32)
+        p = torch.empty(chunk, HW, HW, device=x.device, dtype=torch.bfloat16)
+        for t0 in range(0, T, chunk):
+            n = min(chunk, T - t0)
+            ops.bmm_nt(q[t0:t0 + n], k[t0:t0 + n], s[:n])
+            call("sa_softmax_rows", s.data_ptr(), HW, p.data_ptr(), HW, n * HW, HW, float(C) ** -0.5, ops._stream())
+            ops.bmm_nt(p[:n], vt[t0:t0 + n], o[t0:t0 + n], epilogue=ops.EPI_BF16)
+        return self._conv(o.view(T, H, W, C), T, H, W, e.proj, residual=x)
+
+    def _up(self, e, x, T, H, W):
+        C = x.shape[-1]
+        if e.kind == "up3d" and T > 1:
+            u = torch.empty(1 + 2 * (T - 1), H, W, C, device=x.device, dtype=torch.bfloat16)
+            u[0].copy_(x[0])
+            self._conv(x[1:], T - 1, H, W, e.tc, out=u[1:], interleave=C)
+            x, T = u, 1 + 2 * (T - 1)
+        return self._conv(x, T, 2 * H, 2 * W, e.rs, upsample=True), T, 2 * H, 2 * W
+
+    def decode_clip(self, z, post=False):
+        """z [16, T, h, w] fp32 (one batch item) -> [3, 1+4(T-1), 8h, 8w] fp32 in [-1,1]
+        (post=True: decode_latents' [0,1] mapping, pipeline:425-430)."""
+        pk = self._pack()
+        dev = pk.mean.device
+        Cz, T, H, W = z.shape
+        zc = z.to(device=dev, dtype=torch.float32).contiguous()
+        x = torch.empty(T, H, W, pk.zp, device=dev, dtype=torch.bfloat16)
+        call("sa_vae_input", zc.data_ptr(), Cz, T * H * W, pk.mean.data_ptr(), pk.std.data_ptr(), x.data_ptr(),
+             pk.zp, ops._stream())
+        x = self._conv(x, T, H, W, pk.conv2)
+        for e in pk.layers:
+            if e.kind == "conv":
+                x = self._conv(x, T, H, W, e.conv)
+            elif e.kind == "res":
+                x = self._res(e, x, T, H, W)
+            elif e.kind == "attn":
+                x = self._attn(e, x, T, H, W)
+            elif e.kind in ("up3d", "up2d"):
+                x, T, H, W = self._up(e, x, T, H, W)
+            elif e.kind == "head":
+                y = self._rms(x, e.g, True)
+                x = self._conv(y, T, H, W, e.conv, out_f32=True)
+        out = torch.empty(3, T, H, W, device=dev, dtype=torch.float32)
+        call("sa_vae_output", x.data_ptr(), 4, 3, T * H * W, out.data_ptr(), int(post), ops._stream())
+        return out
+
+    def decode(self, z, return_dict=True):
+        """wan_vae.py:666-681: [B, 16, T, h, w] -> DecoderOutput(sample=[B, 3, 1+4(T-1), 8h, 8w])."""
+        dec = torch.stack([self.decode_clip(u) for u in z])
+        if not return_dict:
+            return (dec,)
+        return DecoderOutput(sample=dec)

@@ -1,0 +1,63 @@
+"""C-ABI checks that need no GPU: the library builds/loads, exports every symbol declared in
+include/stableavatar_hip.h, and the ctypes signatures match the header's parameter lists."""
+import ctypes
+import re
+import subprocess
+
+import pytest
+
+from stableavatar_amd import _lib
+
+
+def _header_decls():
+    txt = _lib.HEADER.read_text()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    out = {}
+    for m in re.finditer(r"\bint\s+(sa_\w+)\s*\(([^)]*)\)\s*;", txt, flags=re.S):
+        params = [p.strip() for p in m.group(2).replace("\n", " ").split(",") if p.strip()]
+        codes = ""
+        for p in params:
+            if "*" in p:
+                codes += "p"
+            elif p.startswith("int64_t"):
+                codes += "l"
+            elif p.startswith("float"):
+                codes += "f"
+            elif p.startswith("int"):
+                codes += "i"
+            else:
+                raise AssertionError(f"unknown param type: {p}")
+        out[m.group(1)] = codes
+    return out
+
+
+def test_signatures_match_header():
+    decls = _header_decls()
+    assert decls, "no declarations parsed"
+    assert set(decls) == set(_lib.header_symbols())
+    for name, codes in decls.items():
+        assert _lib.SIGNATURES.get(name) == codes, (name, codes, _lib.SIGNATURES.get(name))
+
+
+def test_library_exports_every_symbol():
+    if not _lib.LIB_PATH.exists():
+        pytest.skip("library not built (run __graft_entry__.build())")
+    nm = subprocess.run(["nm", "-D", "--defined-only", str(_lib.LIB_PATH)], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (sa_\w+)", nm))
+    missing = set(_lib.header_symbols()) - exported
+    assert not missing, missing
+    L = ctypes.CDLL(str(_lib.LIB_PATH))
+    for name in _lib.header_symbols():
+        assert getattr(L, name) is not None
+
+
+def test_bad_arguments_are_rejected_without_gpu_work():
+    """argument validation happens before any HIP call: NULL pointers return rc=1"""
+    if not _lib.LIB_PATH.exists():
+        pytest.skip("library not built")
+    L = _lib.lib()
+    assert L.sa_gemm_bf16(None, 64, 0, None, 64, 0, None, None, 64, 0, 1, 1, 64, 1, 0, None, 0, 0, None, 0, 0,
+                          None) == 1
+    assert L.sa_attn_fwd(None, None, None, None, None, 1, 1, 1, 128, 128, 128, 128, 128, 1.0, 0, None) == 1
+    with pytest.raises(_lib.KernelError):
+        _lib.call("sa_fill_f32", None, 10, 0.0, None)
