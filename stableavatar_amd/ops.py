@@ -47,6 +47,8 @@ def linear(x, weight, bias=None, epilogue=EPI_BF16, out=None, residual=None, gat
     if out is None:
         out = torch.empty(M, N, device=x.device, dtype=torch.float32 if f32_out else torch.bfloat16)
     assert out.dtype == (torch.float32 if f32_out else torch.bfloat16) and out.stride(1) == 1
+    if tuple(out.shape) != (M, N):
+        raise ValueError(f"linear: out shape {tuple(out.shape)} != {(M, N)}")
     if bias is not None:
         _check(bias, torch.float32, "linear.bias")
     ldr = 0

@@ -549,6 +549,7 @@ class WanTransformer3DFantasyModel(nn.Module):
                                   [[b * Lp + f * G, G, (b * n_fr + f) * nper, nper]
                                    for b in range(B) for f in range(n_fr)], dev)
         x = ws.x
+        kvv = torch.empty(B * n_fr * nper, 2 * dim, device=dev, dtype=torch.bfloat16)  # per-frame vocal K|V
         grid = (Fw, hp, wp)
         for li, L in enumerate(pk.layers):
             em = emod[li]  # [B, 6, dim]
@@ -576,7 +577,6 @@ class WanTransformer3DFantasyModel(nn.Module):
             ops.attention(qc, kvt[:, :dim], kvt[:, dim:], ws.att, segs_txt, B, Lp, H_)
             if kvi is not None:
                 ops.attention(qc, kvi[:, :dim], kvi[:, dim:], ws.att, segs_img, B, Lp, H_, accumulate=True)
-            kvv = ws.qkv[:B * n_fr * nper, dim:3 * dim]
             ops.linear(vctx, L.w_kv_v, L.b_kv_v, ops.EPI_BF16, out=kvv)
             ops.attention(qc, kvv[:, :dim], kvv[:, dim:], ws.att, segs_voc, B * n_fr, G, H_, accumulate=True)
             ops.linear(ws.att, L.w_co, L.b_co, ops.EPI_RES_F32, out=x, residual=x)

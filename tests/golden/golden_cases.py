@@ -31,7 +31,7 @@ def dit_inputs(cfg, case="full"):
                 n_frames=n_frames)
 
 
-VAE_SMALL = {"dim16_T3_8x8": dict(dim=16, seed=21, T=3, h=8, w=8),
+VAE_SMALL = {"dim32_T3_8x8": dict(dim=32, seed=21, T=3, h=8, w=8),
              "dim96_T2_4x4": dict(dim=96, seed=22, T=2, h=4, w=4)}
 
 
@@ -39,7 +39,7 @@ def vae_latent(cfg):
     return synthetic.seeded_normal((1, 16, cfg["T"], cfg["h"], cfg["w"]), 200 + cfg["seed"])
 
 
-PIPE = dict(dit=dict(DIT_SMALL, num_layers=1, seed=31), vae=dict(dim=16, seed=32), height=64, width=64,
+PIPE = dict(dit=dict(DIT_SMALL, num_layers=1, seed=31), vae=dict(dim=32, seed=32), height=64, width=64,
             clip_length=17, steps=3, overlap=2, text_guide=3.0, audio_guide=5.0, neg_len=12, pos_len=9,
             audio_frames=24)
 
