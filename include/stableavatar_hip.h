@@ -36,6 +36,12 @@ int sa_gemm_bf16(const void* A, int64_t lda, int64_t strideA, const void* W, int
                  int epilogue, const float* residual, int64_t ldr, int64_t strideR, const float* gate,
                  int64_t gate_bstride, int rows_per_batch, void* stream);
 
+/* Kernel-variant selection for A/B benchmarking in one process (also env SA_GEMM_VARIANT /
+ * SA_ATTN_VARIANT).  gemm: 0 = 2-phase 8-wave, 1 = 4-phase 8-wave, 2 = 4-wave AGPR (default);
+ * attention: 0 = 2-deep ring (default), 1 = 3-deep ring with pipelined QK^T. */
+int sa_gemm_set_variant(int variant);
+int sa_attn_set_variant(int variant);
+
 /* attention(q,k,v,...) of wan/models/wan_fantasy_transformer3d_1B.py:158-207 (SDPA path, no mask,
  * q_lens/k_lens ignored) for head_dim 128.  Rows of q/k/v/o are flat [rows, stride] bf16 matrices,
  * head h at column h*head_dim.  segs = device int32 [nseg][4] = {q_row0, q_len, kv_row0, kv_len}:

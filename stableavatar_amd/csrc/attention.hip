@@ -14,6 +14,8 @@
 // Swapped product S^T = K·Q^T (mfma_f32_32x32x16_bf16) puts one query per lane, so the online
 // softmax is lane-local; P^T is fed back as the B operand straight from the accumulator and V^T
 // comes from ds_read_b64_tr_b16, giving O^T with the query on the lane (rescale is per lane).
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -183,6 +185,189 @@ __global__ __launch_bounds__(512) void attn_fwd_kernel(AttnArgs a) {
   }
 }
 
+// ---- v2: 3-deep K/V ring, software-pipelined QK^T of block j+1 beside the softmax of block j
+// (T15), deferred rescale with threshold (T13), permlane32 half-wave reductions (T12).
+constexpr float RESCALE_THR = 8.0f;  // log2 units: P <= 2^8 between rescales
+constexpr int LDS_BYTES_V2 = 3 * STAGE_BYTES;  // 96 KB
+
+__device__ __forceinline__ float fmax_nc(float a, float b) { return a > b ? a : b; }
+__device__ __forceinline__ float half_swap_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmax_nc(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+__global__ __launch_bounds__(512) void attn_fwd_v2_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int* sg = a.segs + blockIdx.z * 4;
+  const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
+  const int qb = blockIdx.x, h = blockIdx.y;
+  if (qb * QB >= q_len || kv_len <= 0) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5;
+
+  const int qi = qb * QB + wave * 32 + (lane & 31);
+  const int qc = min(qi, q_len - 1);
+  const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * hi;
+  bf16x8 qf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
+
+  const bf16* kbase = a.k + h * D;
+  const bf16* vbase = a.v + h * D;
+  int srow[2], schunk[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    srow[i] = (wave * 2 + i) * 4 + (lane >> 4);
+    schunk[i] = (lane & 15) ^ gsw(srow[i]);
+  }
+  auto stage = [&](int kb) {
+    char* base = smem + (kb % 3) * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long key = kv_row0 + min(kb * KVB + srow[i], kv_len - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(kbase + key * a.ks + schunk[i] * 8),
+                                       LDS_PTR(base + (wave * 2 + i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(vbase + key * a.vs + schunk[i] * 8),
+                                       LDS_PTR(base + TILE_BYTES + (wave * 2 + i) * 1024), 16, 0, 0);
+    }
+  };
+  auto qk = [&](int kb, f32x16* S) {
+    const char* Ks = smem + (kb % 3) * STAGE_BYTES;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) S[t][r] = 0.f;
+      const int row = t * 32 + (lane & 31);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int ch = 2 * s + hi;
+        const bf16x8 kf = *(const bf16x8*)(Ks + row * 256 + ((ch ^ gsw(row)) << 4));
+        S[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], S[t], 0, 0, 0);
+      }
+    }
+  };
+
+  f32x16 O[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) O[db][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+  const int nkb = (kv_len + KVB - 1) / KVB;
+  // transposed V reads: with r0 = 32t + 16s + 4hi + q4 the swizzle term gsw(r0) = (q4<<2)|hi does not
+  // depend on (t, s), so each lane needs 8 base addresses and (t, s) become immediate offsets
+  int vaddr[4][2];
+  {
+    const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+    const int g0 = (q4 << 2) | hi, g1 = (q4 << 2) | ((hi + 2) & 3);
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const int ch = db * 4 + 2 * ((lane >> 4) & 1) + (p4 >> 1);
+      vaddr[db][0] = (4 * hi + q4) * 256 + ((ch ^ g0) << 4) + 8 * (p4 & 1);
+      vaddr[db][1] = (4 * hi + q4 + 8) * 256 + ((ch ^ g1) << 4) + 8 * (p4 & 1);
+    }
+  }
+
+  stage(0);
+  if (nkb > 1) stage(1);
+  if (nkb > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  auto body = [&](int kb, f32x16 (&Sc)[2], f32x16 (&Sn)[2]) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K/V(kb+1) landed (issued one iteration ago)
+    __builtin_amdgcn_s_barrier();                     // ... for every wave; and PV(kb-1) done everywhere
+    asm volatile("" ::: "memory");
+    if (kb + 2 < nkb) stage(kb + 2);  // into the slot PV(kb-1) just released
+    if (kb + 1 < nkb) qk(kb + 1, Sn);  // MFMA work independent of the softmax below
+
+    // ---- softmax of block kb (lane = query; 32 scores here, 32 on the partner half)
+    if (kb * KVB + KVB > kv_len) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kb * KVB + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+          if (key >= kv_len) Sc[t][r] = -INFINITY;
+        }
+    }
+    float mx = Sc[0][0];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmax_nc(mx, Sc[t][r]);
+    mx = half_swap_max(mx) * a.c;
+    if (!__all(mx <= m_run + RESCALE_THR)) {  // wave-uniform: rescale O, l to a new running max
+      const float m_new = fmax_nc(m_run, mx);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+      l_run *= alpha;
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) O[db][r] *= alpha;
+      m_run = m_new;
+    }
+    float ps = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(Sc[t][r], a.c, -m_run));
+        Sc[t][r] = p;
+        ps += p;
+      }
+    l_run += ps;
+
+    // ---- O^T += V^T · P^T for block kb
+    const char* Vs = smem + (kb % 3) * STAGE_BYTES + TILE_BYTES;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[j] = f2bf(Sc[t][8 * s + j]);
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          const char* vb = Vs + (t * 32 + 16 * s) * 256;
+          const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (__attribute__((address_space(3))) bf16x4*)(vb + vaddr[db][0]));
+          const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (__attribute__((address_space(3))) bf16x4*)(vb + vaddr[db][1]));
+          const bf16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+          O[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb, O[db], 0, 0, 0);
+        }
+      }
+  };
+  f32x16 SA[2], SB[2];
+  qk(0, SA);
+  for (int kb = 0; kb < nkb; kb += 2) {
+    body(kb, SA, SB);
+    if (kb + 1 < nkb) body(kb + 1, SB, SA);
+  }
+
+  const float lt = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = 1.0f / lt;
+  if (qi < q_len) {
+    bf16* op = a.o + (long)(q_row0 + qi) * a.os + h * D;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const int d0 = db * 32 + 8 * r4 + 4 * hi;
+        float v0 = O[db][4 * r4 + 0] * inv, v1 = O[db][4 * r4 + 1] * inv;
+        float v2 = O[db][4 * r4 + 2] * inv, v3 = O[db][4 * r4 + 3] * inv;
+        if (a.accumulate) {
+          const bf16x4 old = *(const bf16x4*)(op + d0);
+          v0 += bf2f(old[0]); v1 += bf2f(old[1]); v2 += bf2f(old[2]); v3 += bf2f(old[3]);
+        }
+        *(bf16x4*)(op + d0) = (bf16x4){f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
+      }
+  }
+}
+
 // ---- small-query attention for head dims the MFMA kernel does not take (vocal projector, D=192,
 // 17 queries per frame vs 1024 latent tokens: vocal_projector_fantasy_1B.py:259-270).  One wave
 // per (segment, head, query): scores for all keys in LDS, exact softmax, lane-parallel P·V.
@@ -248,6 +433,14 @@ extern "C" int sa_attn_small(const void* q, const void* k, const void* v, void* 
   return SA_OK;
 }
 
+int g_attn_variant = -1;  // 0 = v1 (2-deep ring), 1 = v2 (3-deep ring, pipelined QK^T, deferred rescale)
+
+extern "C" int sa_attn_set_variant(int variant) {
+  if (variant < 0 || variant > 1) return SA_ERR_ARG;
+  g_attn_variant = variant;
+  return SA_OK;
+}
+
 extern "C" int sa_attn_fwd(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
                            int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride,
                            int64_t v_stride, int64_t o_stride, float scale, int accumulate, void* stream) {
@@ -256,14 +449,24 @@ extern "C" int sa_attn_fwd(const void* q, const void* k, const void* v, void* o,
   if ((q_stride | k_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
   if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)o)) & 15) return SA_ERR_ARG;
   static bool attr = false;
+  if (g_attn_variant < 0) {
+    const char* e = getenv("SA_ATTN_VARIANT");
+    g_attn_variant = e ? atoi(e) : 0;
+  }
+  const bool v1 = g_attn_variant == 0;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_v2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES_V2);
     attr = true;
   }
   AttnArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, segs,
              q_stride, k_stride, v_stride, o_stride, scale * 1.4426950408889634f, accumulate};
   dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+  if (v1)
+    hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(attn_fwd_v2_kernel, grid, dim3(512), LDS_BYTES_V2, (hipStream_t)stream, a);
   SA_LAUNCH_CHECK();
   return SA_OK;
 }

@@ -82,14 +82,25 @@ __global__ __launch_bounds__(256) void layernorm_mod_kernel(LnArgs a) {
   for (int i = 0; i < MAXV; ++i)
     if (i < nch && i * 512 + lane * 8 < a.C) {
       const int c0 = i * 512 + lane * 8;
-      float y[8];
+      float y[8], w8[8], b8[8], sc8[8], sh8[8], g8[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float t = (v[i][j] - mean) * rstd;
-        if (a.w) t = t * a.w[c0 + j] + (a.b ? a.b[c0 + j] : 0.f);
-        if (a.scale) t = t * (1.f + a.scale[bo + c0 + j]) + a.shift[bo + c0 + j];
-        if (a.gate) t = v[i][j] + t * a.gate[bo + c0 + j];
-        y[j] = t;
+      for (int j = 0; j < 8; ++j) y[j] = (v[i][j] - mean) * rstd;
+      if (a.w) {
+        load8<float>(a.w + c0, w8);
+        if (a.b) load8<float>(a.b + c0, b8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = y[j] * w8[j] + (a.b ? b8[j] : 0.f);
+      }
+      if (a.scale) {
+        load8<float>(a.scale + bo + c0, sc8);
+        load8<float>(a.shift + bo + c0, sh8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = y[j] * (1.f + sc8[j]) + sh8[j];
+      }
+      if (a.gate) {
+        load8<float>(a.gate + bo + c0, g8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = v[i][j] + y[j] * g8[j];
       }
       store8<TO>(out + c0, y);
     }
@@ -125,15 +136,21 @@ __device__ __forceinline__ void rms_rope_one(bf16* p, const float* w, const QkAr
       const int c0 = i * 512 + lane * 8;
       float y[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) y[j] = v[i][j] * r * w[c0 + j];
+      for (int j = 0; j < 8; ++j) y[j] = v[i][j] * r;
+      {
+        float w8[8];
+        load8<float>(w + c0, w8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] *= w8[j];
+      }
       if (rot) {
         const int d0 = c0 % a.head_dim;
 #pragma unroll
         for (int j = 0; j < 8; j += 2) {
           const int pi = (d0 + j) >> 1;
           const int pos = pi < a.nf ? fi : (pi < a.nf + a.nh ? hi_ : wi);
-          const float cs = a.rope[(pos * (a.head_dim / 2) + pi) * 2 + 0];
-          const float sn = a.rope[(pos * (a.head_dim / 2) + pi) * 2 + 1];
+          const float2 csn = *(const float2*)(a.rope + (pos * (a.head_dim / 2) + pi) * 2);
+          const float cs = csn.x, sn = csn.y;
           const float re = y[j], im = y[j + 1];
           y[j] = re * cs - im * sn;
           y[j + 1] = re * sn + im * cs;

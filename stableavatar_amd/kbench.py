@@ -24,10 +24,70 @@ def _time(fn, iters=10, warmup=2):
 
 
 def main(which=("gemm", "attn")):
+    from ._lib import call
     dev = "cuda"
     torch.manual_seed(0)
     M = 3 * 21504
     res = []
+    if "gemmvar" in which:  # A/B of the GEMM variants in one process (rule: interleaved rounds)
+        for (N, K, epi, name) in [(4608, 1536, ops.EPI_BF16, "qkv"), (1536, 1536, ops.EPI_RES_F32, "o_proj"),
+                                  (8960, 1536, ops.EPI_GELU_TANH_BF16, "ffn_up"),
+                                  (1536, 8960, ops.EPI_RES_F32, "ffn_down")]:
+            x = torch.randn(M, K, device=dev).bfloat16()
+            w = (torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
+            b = torch.randn(N, device=dev)
+            out = torch.empty(M, N, device=dev, dtype=torch.float32 if epi == ops.EPI_RES_F32 else torch.bfloat16)
+            gate = torch.randn(3, N, device=dev)
+            ref = None
+            times = {0: [], 1: [], 2: []}
+            for rnd in range(3):
+                for v in (0, 1, 2):
+                    call("sa_gemm_set_variant", v)
+                    if epi == ops.EPI_RES_F32:
+                        out.zero_()
+                        fn = lambda: ops.linear(x, w, b, epi, out=out, residual=out, gate=gate, rows_per_batch=21504)
+                    else:
+                        fn = lambda: ops.linear(x, w, b, epi, out=out)
+                    times[v].append(_time(fn, iters=5, warmup=1))
+                    if epi != ops.EPI_RES_F32:
+                        o = out.float()
+                        if ref is None:
+                            ref = o.clone()
+                        err = ((o - ref).norm() / ref.norm()).item()
+                        assert err < 1e-2, (name, v, err)
+            fl = 2.0 * M * N * K
+            r = {"kernel": f"gemm_{name}", "M": M, "N": N, "K": K}
+            for v in (0, 1, 2):
+                ms = sorted(times[v])[1]
+                r[f"v{v}_ms"] = round(ms, 4)
+                r[f"v{v}_tflops"] = round(fl / ms / 1e9, 1)
+            res.append(r)
+            print(json.dumps(r), flush=True)
+            del x, w, out
+        call("sa_gemm_set_variant", 2)
+    if "attnvar" in which:
+        L, H, D = 21504, 12, 128
+        qkv = torch.randn(3 * L, 3 * H * D, device=dev).bfloat16()
+        segs = torch.tensor([[b * L, L, b * L, L] for b in range(3)], dtype=torch.int32, device=dev)
+        q, k, v_ = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+        outs = {}
+        times = {0: [], 1: []}
+        for rnd in range(3):
+            for v in (0, 1):
+                call("sa_attn_set_variant", v)
+                o = torch.empty(3 * L, H * D, device=dev, dtype=torch.bfloat16)
+                times[v].append(_time(lambda: ops.attention(q, k, v_, o, segs, 3, L, H), iters=3, warmup=1))
+                outs[v] = o.float()
+        err = ((outs[1] - outs[0]).norm() / outs[0].norm()).item()
+        fl = 4.0 * 3 * H * L * L * D
+        r = {"kernel": "attn_self", "err_v1_v0": err}
+        for v in (0, 1):
+            ms = sorted(times[v])[1]
+            r[f"v{v}_ms"] = round(ms, 3)
+            r[f"v{v}_tflops"] = round(fl / ms / 1e9, 1)
+        res.append(r)
+        print(json.dumps(r), flush=True)
+        call("sa_attn_set_variant", 0)
     if "gemm" in which:
         for (N, K, epi, name) in [(4608, 1536, ops.EPI_BF16, "qkv"), (1536, 1536, ops.EPI_RES_F32, "o_proj"),
                                   (8960, 1536, ops.EPI_GELU_TANH_BF16, "ffn_up"),

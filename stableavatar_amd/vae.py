@@ -241,16 +241,18 @@ class AutoencoderKLWan(nn.Module):
         qkv = self._conv(y, T, H, W, e.qkv).view(T, HW, 3 * C)
         q, k, v = qkv[:, :, :C], qkv[:, :, C:2 * C], qkv[:, :, 2 * C:]
         o = torch.empty(T, HW, C, device=x.device, dtype=torch.bfloat16)
-        vt = torch.empty(T, C, HW, device=x.device, dtype=torch.bfloat16)
-        call("sa_transpose_bf16", v.data_ptr(), v.stride(1), v.stride(0), vt.data_ptr(), HW, C * HW, HW, C, T,
+        HWp = ((HW + 63) // 64) * 64  # the P·V GEMM contracts over keys: pad them to the 64-deep K tile
+        alloc = torch.empty if HWp == HW else torch.zeros
+        vt = alloc(T, C, HWp, device=x.device, dtype=torch.bfloat16)
+        call("sa_transpose_bf16", v.data_ptr(), v.stride(1), v.stride(0), vt.data_ptr(), HWp, C * HWp, HW, C, T,
              ops._stream())
         chunk = max(1, min(T, (1 << 30) // (HW * HW * 6)))  # bound the fp32 score buffer
         s = torch.empty(chunk, HW, HW, device=x.device, dtype=torch.float32)
-        p = torch.empty(chunk, HW, HW, device=x.device, dtype=torch.bfloat16)
+        p = alloc(chunk, HW, HWp, device=x.device, dtype=torch.bfloat16)
         for t0 in range(0, T, chunk):
             n = min(chunk, T - t0)
             ops.bmm_nt(q[t0:t0 + n], k[t0:t0 + n], s[:n])
-            call("sa_softmax_rows", s.data_ptr(), HW, p.data_ptr(), HW, n * HW, HW, float(C) ** -0.5, ops._stream())
+            call("sa_softmax_rows", s.data_ptr(), HW, p.data_ptr(), HWp, n * HW, HW, float(C) ** -0.5, ops._stream())
             ops.bmm_nt(p[:n], vt[t0:t0 + n], o[t0:t0 + n], epilogue=ops.EPI_BF16)
         return self._conv(o.view(T, H, W, C), T, H, W, e.proj, residual=x)
 
