@@ -40,6 +40,18 @@ constexpr int LDS_BYTES = 2 * STAGE_BYTES;   // 64 KB
 // transposed (ds_read_b64_tr_b16) reads (cdna_hip_programming.md T10 form (b))
 __device__ __forceinline__ int gsw(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 
+constexpr float RESCALE_THR = 8.0f;  // log2 units: P <= 2^8 between rescales
+
+__device__ __forceinline__ float fmax_nc(float a, float b) { return a > b ? a : b; }
+__device__ __forceinline__ float half_swap_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmax_nc(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+// OPT adds (cdna_hip_programming.md §5.5): static priority for the younger half (T5 static form),
+// non-canonicalising max chain + permlane32 half-swap (T12), and the deferred rescale (T13): O and l
+// are rescaled only when some query's running max grows by more than RESCALE_THR (log2 units).
+template <bool OPT>
 __global__ __launch_bounds__(512) void attn_fwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int* sg = a.segs + blockIdx.z * 4;
@@ -87,6 +99,8 @@ __global__ __launch_bounds__(512) void attn_fwd_kernel(AttnArgs a) {
 
   const int nkb = (kv_len + KVB - 1) / KVB;
   stage(0, 0);
+  if constexpr (OPT)
+    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
   for (int kb = 0; kb < nkb; ++kb) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -117,29 +131,58 @@ __global__ __launch_bounds__(512) void attn_fwd_kernel(AttnArgs a) {
           if (key >= kv_len) S[t][r] = -INFINITY;
         }
     }
-    float mx = S[0][0];
+    if constexpr (OPT) {
+      float mx = S[0][0];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[t][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx * a.c);
-    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-    float ps = 0.f;
+        for (int r = 0; r < 16; ++r) mx = fmax_nc(mx, S[t][r]);
+      mx = half_swap_max(mx) * a.c;
+      if (!__all(mx <= m_run + RESCALE_THR)) {  // wave-uniform decision, before this block's P exists
+        const float m_new = fmax_nc(m_run, mx);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        l_run *= alpha;
+        m_run = m_new;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+        for (int db = 0; db < 4; ++db)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(S[t][r], a.c, -m_new));
-        S[t][r] = p;
-        ps += p;
+          for (int r = 0; r < 16; ++r) O[db][r] *= alpha;
       }
-    l_run = fmaf(l_run, alpha, ps);
-    m_run = m_new;
+      float ps = 0.f;
 #pragma unroll
-    for (int db = 0; db < 4; ++db)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) O[db][r] *= alpha;
+        for (int r = 0; r < 16; ++r) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(S[t][r], a.c, -m_run));
+          S[t][r] = p;
+          ps += p;
+        }
+      l_run += ps;
+    } else {
+      float mx = S[0][0];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[t][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run, mx * a.c);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+      float ps = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(S[t][r], a.c, -m_new));
+          S[t][r] = p;
+          ps += p;
+        }
+      l_run = fmaf(l_run, alpha, ps);
+      m_run = m_new;
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) O[db][r] *= alpha;
+    }
 
     // O^T[d][query] += V^T · P^T
     const int q4 = (lane & 15) >> 2, p4 = lane & 3;
@@ -187,14 +230,7 @@ __global__ __launch_bounds__(512) void attn_fwd_kernel(AttnArgs a) {
 
 // ---- v2: 3-deep K/V ring, software-pipelined QK^T of block j+1 beside the softmax of block j
 // (T15), deferred rescale with threshold (T13), permlane32 half-wave reductions (T12).
-constexpr float RESCALE_THR = 8.0f;  // log2 units: P <= 2^8 between rescales
 constexpr int LDS_BYTES_V2 = 3 * STAGE_BYTES;  // 96 KB
-
-__device__ __forceinline__ float fmax_nc(float a, float b) { return a > b ? a : b; }
-__device__ __forceinline__ float half_swap_max(float v) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmax_nc(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
 
 __global__ __launch_bounds__(512) void attn_fwd_v2_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -368,6 +404,507 @@ __global__ __launch_bounds__(512) void attn_fwd_v2_kernel(AttnArgs a) {
   }
 }
 
+// ---- v3: v1's structure with every LDS read issued from inline asm at base+immediate addresses
+// and retired by counted lgkmcnt waits (cdna_hip_programming.md §5.7 item 1 form (ii)).  hipcc
+// cannot see these reads, so it neither serialises each K fragment behind its own wait nor drains
+// the next block's LDS-DMA (vmcnt(0)) before the V^T reads, which is what the compiler-scheduled v1
+// does.  K fragments come in groups of 4 (16 VGPR) two groups ahead of their MFMAs; V^T fragments
+// in groups of 8 (one per (t, s) P slice), the first two issued before the softmax.  Deferred
+// rescale as in OPT.
+template <int OFF>
+__device__ __forceinline__ void ds_b128(u32x4& d, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF));
+}
+template <int OFF>
+__device__ __forceinline__ void ds_tr64(u32x2& d, uint32_t addr) {
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF));
+}
+template <int N>
+__device__ __forceinline__ void wait_k(u32x4* f) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]) : "i"(N));
+}
+template <int N>
+__device__ __forceinline__ void wait_v(u32x2* f) {
+  asm volatile("s_waitcnt lgkmcnt(%8)"
+               : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7])
+               : "i"(N));
+}
+__device__ __forceinline__ bf16x8 as_bf8(u32x4 x) { return __builtin_bit_cast(bf16x8, x); }
+__device__ __forceinline__ bf16x8 as_bf8(u32x2 lo, u32x2 hi) {
+  const u32x4 x = {lo[0], lo[1], hi[0], hi[1]};
+  return __builtin_bit_cast(bf16x8, x);
+}
+
+// K fragments for (t, s0..s0+3) of stage BUF
+template <int BUF, int T, int S0>
+__device__ __forceinline__ void read_k4(u32x4* f, const uint32_t* ka) {
+  constexpr int base = BUF * STAGE_BYTES + T * 8192;
+  ds_b128<base>(f[0], ka[S0 + 0]);
+  ds_b128<base>(f[1], ka[S0 + 1]);
+  ds_b128<base>(f[2], ka[S0 + 2]);
+  ds_b128<base>(f[3], ka[S0 + 3]);
+}
+// V^T fragments for P slice (t, s) of stage BUF: f[2*db + h] (h = rows r0 / r0+8)
+template <int BUF, int T, int S>
+__device__ __forceinline__ void read_v8(u32x2* f, const uint32_t* va) {
+  constexpr int base = BUF * STAGE_BYTES + TILE_BYTES + T * 8192 + S * 4096;
+  ds_tr64<base>(f[0], va[0]); ds_tr64<base>(f[1], va[1]);
+  ds_tr64<base>(f[2], va[2]); ds_tr64<base>(f[3], va[3]);
+  ds_tr64<base>(f[4], va[4]); ds_tr64<base>(f[5], va[5]);
+  ds_tr64<base>(f[6], va[6]); ds_tr64<base>(f[7], va[7]);
+}
+__device__ __forceinline__ void mfma_k4(f32x16& acc, const u32x4* f, const bf16x8* qf) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(f[0]), qf[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(f[1]), qf[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(f[2]), qf[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(f[3]), qf[3], acc, 0, 0, 0);
+}
+__device__ __forceinline__ void mfma_v8(f32x16* O, const u32x2* f, bf16x8 pb) {
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+    O[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(f[2 * db], f[2 * db + 1]), pb, O[db], 0, 0, 0);
+}
+__device__ __forceinline__ bf16x8 pslice(const f32x16& S, int s) {
+  bf16x8 pb;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) pb[j] = f2bf(S[8 * s + j]);
+  return pb;
+}
+
+struct V3State {
+  f32x16 O[4];
+  float m_run, l_run;
+};
+
+template <int BUF>
+__device__ __forceinline__ void attn_v3_block(V3State& st, const bf16x8* qf, const uint32_t* ka, const uint32_t* va,
+                                              int kb, int kv_len, float c, int hi) {
+  // S^T[key][query] = K · Q^T, K fragments two groups ahead
+  u32x4 ka0[4], ka1[4], kb0[4], kb1[4];
+  f32x16 S[2];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { S[0][r] = 0.f; S[1][r] = 0.f; }
+  read_k4<BUF, 0, 0>(ka0, ka);
+  read_k4<BUF, 0, 4>(ka1, ka);
+  read_k4<BUF, 1, 0>(kb0, ka);
+  wait_k<8>(ka0);
+  mfma_k4(S[0], ka0, qf);
+  read_k4<BUF, 1, 4>(kb1, ka);
+  wait_k<8>(ka1);
+  mfma_k4(S[0], ka1, qf + 4);
+  wait_k<4>(kb0);
+  mfma_k4(S[1], kb0, qf);
+  wait_k<0>(kb1);
+  mfma_k4(S[1], kb1, qf + 4);
+  // first two V^T slices under the softmax
+  u32x2 v0[8], v1[8];
+  read_v8<BUF, 0, 0>(v0, va);
+  read_v8<BUF, 0, 1>(v1, va);
+
+  if (kb * KVB + KVB > kv_len) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb * KVB + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+        if (key >= kv_len) S[t][r] = -INFINITY;
+      }
+  }
+  float mx = S[0][0];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[t][r]);
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * c;
+  if (!__all(mx <= st.m_run + RESCALE_THR)) {  // wave-uniform, before this block's P exists
+    const float m_new = fmaxf(st.m_run, mx);
+    const float alpha = __builtin_amdgcn_exp2f(st.m_run - m_new);
+    st.l_run *= alpha;
+    st.m_run = m_new;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st.O[db][r] *= alpha;
+  }
+  float ps = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = __builtin_amdgcn_exp2f(fmaf(S[t][r], c, -st.m_run));
+      S[t][r] = p;
+      ps += p;
+    }
+  st.l_run += ps;
+
+  // O^T[d][query] += V^T · P^T, slice g = 2t + s
+  wait_v<8>(v0);
+  mfma_v8(st.O, v0, pslice(S[0], 0));
+  read_v8<BUF, 1, 0>(v0, va);
+  wait_v<8>(v1);
+  mfma_v8(st.O, v1, pslice(S[0], 1));
+  read_v8<BUF, 1, 1>(v1, va);
+  wait_v<8>(v0);
+  mfma_v8(st.O, v0, pslice(S[1], 0));
+  wait_v<0>(v1);
+  mfma_v8(st.O, v1, pslice(S[1], 1));
+}
+
+__global__ __launch_bounds__(512) void attn_fwd_v3_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int* sg = a.segs + blockIdx.z * 4;
+  const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
+  const int qb = blockIdx.x, h = blockIdx.y;
+  if (qb * QB >= q_len || kv_len <= 0) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5;
+
+  const int qi = qb * QB + wave * 32 + (lane & 31);
+  const int qc = min(qi, q_len - 1);
+  const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * hi;
+  bf16x8 qf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
+
+  const bf16* kbase = a.k + h * D;
+  const bf16* vbase = a.v + h * D;
+  int srow[2], schunk[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    srow[i] = (wave * 2 + i) * 4 + (lane >> 4);
+    schunk[i] = (lane & 15) ^ gsw(srow[i]);
+  }
+  auto stage = [&](int kb, int buf) {
+    char* base = smem + buf * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long key = kv_row0 + min(kb * KVB + srow[i], kv_len - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(kbase + key * a.ks + schunk[i] * 8),
+                                       LDS_PTR(base + (wave * 2 + i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(vbase + key * a.vs + schunk[i] * 8),
+                                       LDS_PTR(base + TILE_BYTES + (wave * 2 + i) * 1024), 16, 0, 0);
+    }
+  };
+
+  // per-lane LDS byte addresses of stage 0 (t = s = 0); every other read is +immediate
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
+  uint32_t ka[8], va[8];
+  {
+    const int row = lane & 31;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) ka[s] = lds0 + row * 256 + (((2 * s + hi) ^ gsw(row)) << 4);
+    const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int r = 4 * hi + q4 + 8 * hh;
+        const int col = db * 32 + 16 * ((lane >> 4) & 1) + 4 * p4;
+        va[2 * db + hh] = lds0 + r * 256 + (((col >> 3) ^ gsw(r)) << 4) + 8 * ((col >> 2) & 1);
+      }
+  }
+
+  V3State st;
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) st.O[db][r] = 0.f;
+  st.m_run = -INFINITY;
+  st.l_run = 0.f;
+
+  const int nkb = (kv_len + KVB - 1) / KVB;
+  stage(0, 0);
+  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  for (int kb = 0; kb < nkb; kb += 2) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kb + 1 < nkb) stage(kb + 1, 1);
+    attn_v3_block<0>(st, qf, ka, va, kb, kv_len, a.c, hi);
+    if (kb + 1 >= nkb) break;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kb + 2 < nkb) stage(kb + 2, 0);
+    attn_v3_block<1>(st, qf, ka, va, kb + 1, kv_len, a.c, hi);
+  }
+
+  const float lt = st.l_run + __shfl_xor(st.l_run, 32, 64);
+  const float inv = 1.0f / lt;
+  if (qi < q_len) {
+    bf16* op = a.o + (long)(q_row0 + qi) * a.os + h * D;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const int d0 = db * 32 + 8 * r4 + 4 * hi;
+        float v0 = st.O[db][4 * r4 + 0] * inv, v1 = st.O[db][4 * r4 + 1] * inv;
+        float v2 = st.O[db][4 * r4 + 2] * inv, v3 = st.O[db][4 * r4 + 3] * inv;
+        if (a.accumulate) {
+          const bf16x4 old = *(const bf16x4*)(op + d0);
+          v0 += bf2f(old[0]); v1 += bf2f(old[1]); v2 += bf2f(old[2]); v3 += bf2f(old[3]);
+        }
+        *(bf16x4*)(op + d0) = (bf16x4){f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
+      }
+  }
+}
+
+// ---- v4: v3's reads plus a two-group ping-pong (cdna_hip_programming.md §5.5 T5/T16,
+// MI355X_MICROARCH.md "Two waves per SIMD").  Each SIMD holds one wave of group 0 (waves 0-3) and
+// one of group 1 (waves 4-7); group 1 runs one barrier behind, so in every barrier interval one
+// wave of the pair is in its matrix segment (P_j·V_j then K_{j+1}·Q^T: 32 MFMAs) while the other
+// is in its softmax segment (VALU).  K and V live in separate 2-slot rings: K_{j+2} and V_{j+1}
+// are issued in interval 2j+1 (group 0 inside its matrix segment, group 1 inside its softmax) and
+// retired by each issuer's vmcnt(0) before barrier 2j+2, after which both groups read them.
+constexpr int V4_K0 = 0, V4_V0 = 2 * TILE_BYTES;  // K slots 0/1, then V slots 0/1 (64 KB)
+
+template <int SLOT>
+__device__ __forceinline__ void v4_issue_k(const bf16* kb, long ks, const int* srow, const int* schunk, int kv_row0,
+                                           int blk, int kv_len, char* smem, int wave) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const long key = kv_row0 + min(blk * KVB + srow[i], kv_len - 1);
+    __builtin_amdgcn_global_load_lds((const void*)(kb + key * ks + schunk[i] * 8),
+                                     LDS_PTR(smem + V4_K0 + SLOT * TILE_BYTES + (wave * 2 + i) * 1024), 16, 0, 0);
+  }
+}
+template <int SLOT>
+__device__ __forceinline__ void v4_issue_v(const bf16* vb, long vs, const int* srow, const int* schunk, int kv_row0,
+                                           int blk, int kv_len, char* smem, int wave) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const long key = kv_row0 + min(blk * KVB + srow[i], kv_len - 1);
+    __builtin_amdgcn_global_load_lds((const void*)(vb + key * vs + schunk[i] * 8),
+                                     LDS_PTR(smem + V4_V0 + SLOT * TILE_BYTES + (wave * 2 + i) * 1024), 16, 0, 0);
+  }
+}
+
+template <int SLOT, int T, int S0>
+__device__ __forceinline__ void v4_read_k4(u32x4* f, const uint32_t* ka) {
+  constexpr int base = V4_K0 + SLOT * TILE_BYTES + T * 8192;
+  ds_b128<base>(f[0], ka[S0 + 0]);
+  ds_b128<base>(f[1], ka[S0 + 1]);
+  ds_b128<base>(f[2], ka[S0 + 2]);
+  ds_b128<base>(f[3], ka[S0 + 3]);
+}
+template <int SLOT, int T, int S>
+__device__ __forceinline__ void v4_read_v8(u32x2* f, const uint32_t* va) {
+  constexpr int base = V4_V0 + SLOT * TILE_BYTES + T * 8192 + S * 4096;
+  ds_tr64<base>(f[0], va[0]); ds_tr64<base>(f[1], va[1]);
+  ds_tr64<base>(f[2], va[2]); ds_tr64<base>(f[3], va[3]);
+  ds_tr64<base>(f[4], va[4]); ds_tr64<base>(f[5], va[5]);
+  ds_tr64<base>(f[6], va[6]); ds_tr64<base>(f[7], va[7]);
+}
+
+// S^T of one block from K slot SLOT (prologue / tail of the matrix segment)
+template <int SLOT>
+__device__ __forceinline__ void v4_qk(f32x16* S, const bf16x8* qf, const uint32_t* ka) {
+  u32x4 ka0[4], ka1[4], kb0[4], kb1[4];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { S[0][r] = 0.f; S[1][r] = 0.f; }
+  v4_read_k4<SLOT, 0, 0>(ka0, ka);
+  v4_read_k4<SLOT, 0, 4>(ka1, ka);
+  wait_k<4>(ka0);
+  mfma_k4(S[0], ka0, qf);
+  __builtin_amdgcn_sched_barrier(0);
+  v4_read_k4<SLOT, 1, 0>(kb0, ka);
+  wait_k<4>(ka1);
+  mfma_k4(S[0], ka1, qf + 4);
+  __builtin_amdgcn_sched_barrier(0);
+  v4_read_k4<SLOT, 1, 4>(kb1, ka);
+  wait_k<4>(kb0);
+  mfma_k4(S[1], kb0, qf);
+  __builtin_amdgcn_sched_barrier(0);
+  wait_k<0>(kb1);
+  mfma_k4(S[1], kb1, qf + 4);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// softmax segment of block kb: S -> P (fp32, in place), deferred rescale of O / l
+__device__ __forceinline__ void v4_softmax(V3State& st, f32x16* S, int kb, int kv_len, float c, int hi) {
+  if (kb * KVB + KVB > kv_len) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb * KVB + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+        if (key >= kv_len) S[t][r] = -INFINITY;
+      }
+  }
+  float mx = S[0][0];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[t][r]);
+  {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+    mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * c;
+  }
+  if (!__all(mx <= st.m_run + RESCALE_THR)) {
+    const float m_new = fmaxf(st.m_run, mx);
+    const float alpha = __builtin_amdgcn_exp2f(st.m_run - m_new);
+    st.l_run *= alpha;
+    st.m_run = m_new;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st.O[db][r] *= alpha;
+  }
+  float ps = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = __builtin_amdgcn_exp2f(fmaf(S[t][r], c, -st.m_run));
+      S[t][r] = p;
+      ps += p;
+    }
+  st.l_run += ps;
+}
+
+// matrix segment of block j: O += V_j^T P_j^T (V slot VS), then S = K_{j+1} Q^T (K slot VS ^ 1)
+template <int VS>
+__device__ __forceinline__ void v4_matrix(V3State& st, f32x16* S, const bf16x8* qf, const uint32_t* ka,
+                                          const uint32_t* va, bool next) {
+  u32x2 v0[8], v1[8];
+  v4_read_v8<VS, 0, 0>(v0, va);
+  v4_read_v8<VS, 0, 1>(v1, va);
+  wait_v<8>(v0);
+  mfma_v8(st.O, v0, pslice(S[0], 0));
+  __builtin_amdgcn_sched_barrier(0);
+  v4_read_v8<VS, 1, 0>(v0, va);
+  wait_v<8>(v1);
+  mfma_v8(st.O, v1, pslice(S[0], 1));
+  __builtin_amdgcn_sched_barrier(0);
+  v4_read_v8<VS, 1, 1>(v1, va);
+  wait_v<8>(v0);
+  mfma_v8(st.O, v0, pslice(S[1], 0));
+  __builtin_amdgcn_sched_barrier(0);
+  wait_v<0>(v1);
+  mfma_v8(st.O, v1, pslice(S[1], 1));
+  __builtin_amdgcn_sched_barrier(0);
+  if (next) v4_qk<VS ^ 1>(S, qf, ka);
+}
+
+template <bool G1>
+__device__ __forceinline__ void v4_loop(V3State& st, const bf16x8* qf, const uint32_t* ka, const uint32_t* va,
+                                        const bf16* kb, const bf16* vb, long ks, long vs, const int* srow,
+                                        const int* schunk, int kv_row0, int kv_len, float c, int hi, char* smem,
+                                        int wave) {
+  const int nkb = (kv_len + KVB - 1) / KVB;
+  f32x16 S[2];
+  // prologue: K_0, V_0 -> slot 0, K_1 -> slot 1; S = K_0 Q^T
+  v4_issue_k<0>(kb, ks, srow, schunk, kv_row0, 0, kv_len, smem, wave);
+  v4_issue_v<0>(vb, vs, srow, schunk, kv_row0, 0, kv_len, smem, wave);
+  if (nkb > 1) v4_issue_k<1>(kb, ks, srow, schunk, kv_row0, 1, kv_len, smem, wave);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  v4_qk<0>(S, qf, ka);
+  if (G1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind
+#define SA_V4_STEP(PAR, J)                                                                              \
+  {                                                                                                     \
+    const int j = (J);                                                                                  \
+    v4_softmax(st, S, j, kv_len, c, hi);                                                                \
+    if (G1) {                                                                                           \
+      if (j + 2 < nkb) v4_issue_k<PAR>(kb, ks, srow, schunk, kv_row0, j + 2, kv_len, smem, wave);       \
+      if (j + 1 < nkb) v4_issue_v<PAR ^ 1>(vb, vs, srow, schunk, kv_row0, j + 1, kv_len, smem, wave);   \
+    } else {                                                                                            \
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                                  \
+    }                                                                                                   \
+    __builtin_amdgcn_s_barrier();                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                                                  \
+    if (!G1) {                                                                                          \
+      if (j + 2 < nkb) v4_issue_k<PAR>(kb, ks, srow, schunk, kv_row0, j + 2, kv_len, smem, wave);       \
+      if (j + 1 < nkb) v4_issue_v<PAR ^ 1>(vb, vs, srow, schunk, kv_row0, j + 1, kv_len, smem, wave);   \
+    }                                                                                                   \
+    v4_matrix<PAR>(st, S, qf, ka, va, j + 1 < nkb);                                                     \
+    if (G1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                           \
+    __builtin_amdgcn_s_barrier();                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                                                  \
+  }
+  for (int j0 = 0; j0 < nkb; j0 += 2) {
+    SA_V4_STEP(0, j0)
+    if (j0 + 1 >= nkb) break;
+    SA_V4_STEP(1, j0 + 1)
+  }
+#undef SA_V4_STEP
+  if (!G1) __builtin_amdgcn_s_barrier();  // balance group 1's extra barrier
+}
+
+__global__ __launch_bounds__(512) void attn_fwd_v4_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int* sg = a.segs + blockIdx.z * 4;
+  const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
+  const int qb = blockIdx.x, h = blockIdx.y;
+  if (qb * QB >= q_len || kv_len <= 0) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5;
+
+  const int qi = qb * QB + wave * 32 + (lane & 31);
+  const int qc = min(qi, q_len - 1);
+  const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * hi;
+  bf16x8 qf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
+
+  int srow[2], schunk[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    srow[i] = (wave * 2 + i) * 4 + (lane >> 4);
+    schunk[i] = (lane & 15) ^ gsw(srow[i]);
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
+  uint32_t ka[8], va[8];
+  {
+    const int row = lane & 31;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) ka[s] = lds0 + row * 256 + (((2 * s + hi) ^ gsw(row)) << 4);
+    const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int r = 4 * hi + q4 + 8 * hh;
+        const int col = db * 32 + 16 * ((lane >> 4) & 1) + 4 * p4;
+        va[2 * db + hh] = lds0 + r * 256 + (((col >> 3) ^ gsw(r)) << 4) + 8 * ((col >> 2) & 1);
+      }
+  }
+
+  V3State st;
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) st.O[db][r] = 0.f;
+  st.m_run = -INFINITY;
+  st.l_run = 0.f;
+
+  const bf16* kbase = a.k + h * D;
+  const bf16* vbase = a.v + h * D;
+  if (wave >= 4)
+    v4_loop<true>(st, qf, ka, va, kbase, vbase, a.ks, a.vs, srow, schunk, kv_row0, kv_len, a.c, hi, smem, wave);
+  else
+    v4_loop<false>(st, qf, ka, va, kbase, vbase, a.ks, a.vs, srow, schunk, kv_row0, kv_len, a.c, hi, smem, wave);
+
+  const float lt = st.l_run + __shfl_xor(st.l_run, 32, 64);
+  const float inv = 1.0f / lt;
+  if (qi < q_len) {
+    bf16* op = a.o + (long)(q_row0 + qi) * a.os + h * D;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const int d0 = db * 32 + 8 * r4 + 4 * hi;
+        float v0 = st.O[db][4 * r4 + 0] * inv, v1 = st.O[db][4 * r4 + 1] * inv;
+        float v2 = st.O[db][4 * r4 + 2] * inv, v3 = st.O[db][4 * r4 + 3] * inv;
+        if (a.accumulate) {
+          const bf16x4 old = *(const bf16x4*)(op + d0);
+          v0 += bf2f(old[0]); v1 += bf2f(old[1]); v2 += bf2f(old[2]); v3 += bf2f(old[3]);
+        }
+        *(bf16x4*)(op + d0) = (bf16x4){f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
+      }
+  }
+}
+
 // ---- small-query attention for head dims the MFMA kernel does not take (vocal projector, D=192,
 // 17 queries per frame vs 1024 latent tokens: vocal_projector_fantasy_1B.py:259-270).  One wave
 // per (segment, head, query): scores for all keys in LDS, exact softmax, lane-parallel P·V.
@@ -433,10 +970,13 @@ extern "C" int sa_attn_small(const void* q, const void* k, const void* v, void* 
   return SA_OK;
 }
 
-int g_attn_variant = -1;  // 0 = v1 (2-deep ring), 1 = v2 (3-deep ring, pipelined QK^T, deferred rescale)
+int g_attn_variant = -1;  // 0 = v1 (2-deep ring), 1 = v2 (3-deep ring, pipelined QK^T, deferred rescale),
+                          // 2 = v1 + static priority, half-swap max, deferred rescale,
+                          // 3 = v1 structure with asm LDS reads + counted waits (v3),
+                          // 4 = v3 reads + two-group ping-pong (v4)
 
 extern "C" int sa_attn_set_variant(int variant) {
-  if (variant < 0 || variant > 1) return SA_ERR_ARG;
+  if (variant < 0 || variant > 4) return SA_ERR_ARG;
   g_attn_variant = variant;
   return SA_OK;
 }
@@ -451,11 +991,17 @@ extern "C" int sa_attn_fwd(const void* q, const void* k, const void* v, void* o,
   static bool attr = false;
   if (g_attn_variant < 0) {
     const char* e = getenv("SA_ATTN_VARIANT");
-    g_attn_variant = e ? atoi(e) : 0;
+    g_attn_variant = e ? atoi(e) : 3;
   }
-  const bool v1 = g_attn_variant == 0;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_v3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_v4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES_V2);
     attr = true;
@@ -463,8 +1009,14 @@ extern "C" int sa_attn_fwd(const void* q, const void* k, const void* v, void* o,
   AttnArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, segs,
              q_stride, k_stride, v_stride, o_stride, scale * 1.4426950408889634f, accumulate};
   dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
-  if (v1)
-    hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+  if (g_attn_variant == 0)
+    hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+  else if (g_attn_variant == 2)
+    hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+  else if (g_attn_variant == 3)
+    hipLaunchKernelGGL(attn_fwd_v3_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+  else if (g_attn_variant == 4)
+    hipLaunchKernelGGL(attn_fwd_v4_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(attn_fwd_v2_kernel, grid, dim3(512), LDS_BYTES_V2, (hipStream_t)stream, a);
   SA_LAUNCH_CHECK();

@@ -265,6 +265,204 @@ __global__ __launch_bounds__(512) void gemm_phased_kernel(GemmArgs g) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// ping-pong kernel (cdna_hip_programming.md "The 256² 8-phase template"): same tile, waves and
+// quadrant phases as gemm_phased_kernel, but every phase is {ds_read the phase's fragments, issue one
+// half-tile, counted vmcnt} barrier {16 MFMAs} barrier, and waves 4-7 run one barrier behind waves
+// 0-3, so on each SIMD one wave reads while its partner multiplies.  Two K-tiles per iteration
+// (E = 2i in buffer 0, O = 2i+1 in buffer 1); phase ph issues, in order,
+//   A1(O) | A0(E+2) B0(E+2) B1(E+2) A1(E+2) | A0(O+2) B0(O+2) B1(O+2)
+// so every half-tile is read >= 6 phases after it is issued: vmcnt(10) (5 half-tiles of 2 glds
+// still in flight) before each phase's first barrier retires whatever the next phase reads.  Each
+// slot is restaged >= 2 phases after its last read, except A0 (1 phase), whose reads are retired by
+// an lgkmcnt(0) before the reading phase's first barrier.
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int qm = wave >> 2, qn = wave & 3;
+  const bool g1 = qm == 1;
+  const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
+  const int wg = xcd_remap(blockIdx.x, nm * nn);
+  const int mt = wg / nn, nt = wg % nn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const long bz = blockIdx.z;
+  const bf16* A = g.A + bz * g.sA;
+  const bf16* W = g.W + bz * g.sW;
+  const int nk = g.K / BK;
+
+  long goff[4][2];
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int j = i * 8 + wave;
+      const int row = j * 8 + (lane >> 3);
+      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+      if (h < 2) {
+        const int r = min(m0 + h * 128 + row, g.M - 1);
+        goff[h][i] = (long)r * g.lda + chunk * 8;
+      } else {
+        const int r = min(n0 + (h - 2) * 128 + row, g.N - 1);
+        goff[h][i] = (long)r * g.ldw + chunk * 8;
+      }
+    }
+  // half-tile h: 0 = A0, 1 = A1, 2 = B0, 3 = B1
+  auto issue = [&](int h, int kt) {
+    if (kt >= nk) return;
+    const long k0 = (long)kt * BK;
+    const bf16* base = h < 2 ? A : W;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int j = i * 8 + wave;
+      __builtin_amdgcn_global_load_lds((const void*)(base + goff[h][i] + k0),
+                                       LDS_PTR(smem + (kt & 1) * STAGE_BYTES + h * HALF_BYTES + j * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][4][2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) acc[q][m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // prologue = phases 1..7 of iteration -1
+  issue(0, 0); issue(2, 0); issue(3, 0); issue(1, 0);
+  issue(0, 1); issue(2, 1); issue(3, 1);
+  if (nk >= 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (g1) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  bf16x8 a[4][2], b0[2][2], b1[2][2];
+  const int c0 = lane >> 4;
+  auto read_a = [&](const char* S, int half) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        a[m][kk] = *(const bf16x8*)(S + half * HALF_BYTES + swz128(qm * 64 + m * 16 + (lane & 15), kk * 4 + c0));
+  };
+  auto read_b = [&](bf16x8 (&b)[2][2], const char* S, int half) {
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        b[n][kk] = *(const bf16x8*)(S + (2 + half) * HALF_BYTES + swz128(qn * 32 + n * 16 + (lane & 15), kk * 4 + c0));
+  };
+  auto mma = [&](f32x4 (&c)[4][2], const bf16x8 (&b)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) c[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m][kk], b[n][kk], c[m][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+#define SA_PP_MID(FULL)                                                   \
+  if (FULL) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");             \
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                   \
+  __builtin_amdgcn_s_barrier();                                           \
+  __builtin_amdgcn_sched_barrier(0);
+#define SA_PP_END()                                                       \
+  __builtin_amdgcn_sched_barrier(0);                                      \
+  __builtin_amdgcn_s_barrier();                                           \
+  __builtin_amdgcn_sched_barrier(0);
+
+  const int iters = (nk + 1) / 2;
+  for (int it = 0; it < iters; ++it) {
+    const int E = 2 * it, O = E + 1;
+    const bool full = O + 2 < nk;
+    const bool has_o = O < nk;
+    const char* S0 = smem;
+    const char* S1 = smem + STAGE_BYTES;
+    // ph0: A0 x B0 of E
+    read_a(S0, 0);
+    read_b(b0, S0, 0);
+    issue(1, O);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    SA_PP_MID(full)
+    mma(acc[0], b0);
+    SA_PP_END()
+    // ph1: A0 x B1
+    read_b(b1, S0, 1);
+    issue(0, E + 2);
+    SA_PP_MID(full)
+    mma(acc[1], b1);
+    SA_PP_END()
+    // ph2: A1 x B1
+    read_a(S0, 1);
+    issue(2, E + 2);
+    SA_PP_MID(full)
+    mma(acc[2], b1);
+    SA_PP_END()
+    // ph3: A1 x B0
+    issue(3, E + 2);
+    SA_PP_MID(full)
+    mma(acc[3], b0);
+    SA_PP_END()
+    // ph4..7: the same on O (buffer 1)
+    if (has_o) {
+      read_a(S1, 0);
+      read_b(b0, S1, 0);
+    }
+    issue(1, E + 2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    SA_PP_MID(full)
+    if (has_o) mma(acc[0], b0);
+    SA_PP_END()
+    if (has_o) read_b(b1, S1, 1);
+    issue(0, O + 2);
+    SA_PP_MID(full)
+    if (has_o) mma(acc[1], b1);
+    SA_PP_END()
+    if (has_o) read_a(S1, 1);
+    issue(2, O + 2);
+    SA_PP_MID(full)
+    if (has_o) mma(acc[2], b1);
+    SA_PP_END()
+    issue(3, O + 2);
+    SA_PP_MID(full)
+    if (has_o) mma(acc[3], b0);
+    SA_PP_END()
+  }
+#undef SA_PP_MID
+#undef SA_PP_END
+  if (!g1) __builtin_amdgcn_s_barrier();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  float* strip = (float*)(smem + wave * (16 * 36 * 4));
+  const int er = lane >> 2, ec = (lane & 3) * 8;
+  const int qa[4] = {0, 0, 1, 1}, qb[4] = {0, 1, 1, 0};
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) strip[((lane >> 4) * 4 + i) * 36 + n * 16 + (lane & 15)] = acc[q][m][n][i];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      float v[8];
+      const f32x4 t0 = *(const f32x4*)(strip + er * 36 + ec);
+      const f32x4 t1 = *(const f32x4*)(strip + er * 36 + ec + 4);
+      v[0] = t0[0]; v[1] = t0[1]; v[2] = t0[2]; v[3] = t0[3];
+      v[4] = t1[0]; v[5] = t1[1]; v[6] = t1[2]; v[7] = t1[3];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      const int grow = m0 + qa[q] * 128 + qm * 64 + m * 16 + er;
+      const int gcol = n0 + qb[q] * 128 + qn * 32 + ec;
+      if (grow < g.M && gcol < g.N) epi_row<EPI, 8>(g, v, bz, grow, gcol);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // w4 kernel: 4 waves x (128x128 per wave), one wave per SIMD with the 256 accumulators in AGPRs.
 // K is staged in 32-deep sub-tiles (A 256x32 + B 256x32 = 32 KB) through a 4-slot LDS ring: while
 // sub-tile s is multiplied, s+1 is already landed (its fragments are read between the MFMAs of s)
@@ -471,20 +669,22 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(GemmArgs g) {
   }
 }
 
-int g_gemm_variant = -1;  // 0 = v1 (2-phase), 1 = phased (8 waves), 2 = w4 (4 waves, AGPR accumulators)
+int g_gemm_variant = -1;  // 0 = v1 (2-phase), 1 = phased (8 waves), 2 = w4 (4 waves, AGPR accumulators),
+                          // 3 = ping-pong 8-phase
 
 template <int EPI>
 int launch(const GemmArgs& g, int batch, hipStream_t st) {
   static int attr = 0;
   if (g_gemm_variant < 0) {
     const char* e = getenv("SA_GEMM_VARIANT");
-    g_gemm_variant = e ? atoi(e) : 2;
+    g_gemm_variant = e ? atoi(e) : 1;
   }
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_phased_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_w4_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, W4_LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     attr = 1;
   }
   const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
@@ -492,8 +692,10 @@ int launch(const GemmArgs& g, int batch, hipStream_t st) {
     hipLaunchKernelGGL(gemm_nt_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
   else if (g_gemm_variant == 1)
     hipLaunchKernelGGL(gemm_phased_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
-  else
+  else if (g_gemm_variant == 2)
     hipLaunchKernelGGL(gemm_w4_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(256), W4_LDS, st, g);
+  else
+    hipLaunchKernelGGL(gemm_pp_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
   SA_LAUNCH_CHECK();
   return SA_OK;
 }
@@ -501,7 +703,7 @@ int launch(const GemmArgs& g, int batch, hipStream_t st) {
 }  // namespace
 
 extern "C" int sa_gemm_set_variant(int variant) {
-  if (variant < 0 || variant > 2) return SA_ERR_ARG;
+  if (variant < 0 || variant > 3) return SA_ERR_ARG;
   g_gemm_variant = variant;
   return SA_OK;
 }

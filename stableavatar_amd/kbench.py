@@ -39,9 +39,10 @@ def main(which=("gemm", "attn")):
             out = torch.empty(M, N, device=dev, dtype=torch.float32 if epi == ops.EPI_RES_F32 else torch.bfloat16)
             gate = torch.randn(3, N, device=dev)
             ref = None
-            times = {0: [], 1: [], 2: []}
+            gvars = (1, 3)
+            times = {v: [] for v in gvars}
             for rnd in range(3):
-                for v in (0, 1, 2):
+                for v in gvars:
                     call("sa_gemm_set_variant", v)
                     if epi == ops.EPI_RES_F32:
                         out.zero_()
@@ -57,32 +58,33 @@ def main(which=("gemm", "attn")):
                         assert err < 1e-2, (name, v, err)
             fl = 2.0 * M * N * K
             r = {"kernel": f"gemm_{name}", "M": M, "N": N, "K": K}
-            for v in (0, 1, 2):
+            for v in gvars:
                 ms = sorted(times[v])[1]
                 r[f"v{v}_ms"] = round(ms, 4)
                 r[f"v{v}_tflops"] = round(fl / ms / 1e9, 1)
             res.append(r)
             print(json.dumps(r), flush=True)
             del x, w, out
-        call("sa_gemm_set_variant", 2)
+        call("sa_gemm_set_variant", 1)
     if "attnvar" in which:
         L, H, D = 21504, 12, 128
         qkv = torch.randn(3 * L, 3 * H * D, device=dev).bfloat16()
         segs = torch.tensor([[b * L, L, b * L, L] for b in range(3)], dtype=torch.int32, device=dev)
         q, k, v_ = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
         outs = {}
-        times = {0: [], 1: []}
+        variants = (0, 3, 4)
+        times = {v: [] for v in variants}
         for rnd in range(3):
-            for v in (0, 1):
+            for v in variants:
                 call("sa_attn_set_variant", v)
                 o = torch.empty(3 * L, H * D, device=dev, dtype=torch.bfloat16)
                 times[v].append(_time(lambda: ops.attention(q, k, v_, o, segs, 3, L, H), iters=3, warmup=1))
                 outs[v] = o.float()
-        err = ((outs[1] - outs[0]).norm() / outs[0].norm()).item()
         fl = 4.0 * 3 * H * L * L * D
-        r = {"kernel": "attn_self", "err_v1_v0": err}
-        for v in (0, 1):
+        r = {"kernel": "attn_self"}
+        for v in variants:
             ms = sorted(times[v])[1]
+            r[f"err_v{v}_v0"] = ((outs[v] - outs[0]).norm() / outs[0].norm()).item()
             r[f"v{v}_ms"] = round(ms, 3)
             r[f"v{v}_tflops"] = round(fl / ms / 1e9, 1)
         res.append(r)
