@@ -4,7 +4,9 @@ the Wan-2.1 1.3B StableAvatar model + the 3-D causal VAE decode to 81 frames.
 
 One bench "step" = one whole clip (50 DiT forwards at B=3, L=21504 + 50 fused CFG/Euler steps +
 VAE decode), inputs resident in HBM.  `python bench.py --gpus N --steps K --warmup W`; for N>1 it is
-launched by torch.distributed.run, one process per GPU.  Rank 0 prints ONE JSON line.
+launched by torch.distributed.run, one process per GPU: by default every rank denoises its own clip
+(replicas, weak scaling); with --sp all ranks denoise ONE clip with Ulysses sequence parallelism over
+RCCL (strong scaling).  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -34,6 +36,9 @@ def parse():
     p.add_argument("--sample-steps", type=int, default=50)
     p.add_argument("--overlap", type=int, default=15)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--sp", action="store_true",
+                   help="N>1: one clip sequence-parallel over all ranks (Ulysses, strong scaling) instead of "
+                        "one clip per rank (replicas, weak scaling)")
     return p.parse_args()
 
 
@@ -118,8 +123,11 @@ def main():
     from stableavatar_amd.pipeline import WanI2VTalkingInferenceLongPipeline, window_schedule
     from stableavatar_amd.scheduler import FlowMatchEulerDiscreteScheduler
 
+    sp_mode = args.sp and world > 1
     dit, vae = build(dev, seed=0)
-    latents, y, ctx, clip, a = make_inputs(dev, args.frames, args.size, seed=42 + rank)
+    if sp_mode:
+        dit.enable_multi_gpus_inference()
+    latents, y, ctx, clip, a = make_inputs(dev, args.frames, args.size, seed=42 + (0 if sp_mode else rank))
     sched = FlowMatchEulerDiscreteScheduler(1000, shift=5.0)
     sched.set_timesteps(args.sample_steps, device=dev)
     pipe = WanI2VTalkingInferenceLongPipeline(vae=vae, transformer=dit, scheduler=sched)
@@ -161,10 +169,16 @@ def main():
         dt = tt.item()
     attn_ms = sum(e0.elapsed_time(e1) for e0, e1 in events) / max(len(events), 1)
     attn_flop = flops.self_attention_flops(B=3, L=seq_len)
+    parallelism = f"replicas{world}" if world > 1 else "single"
+    if sp_mode:
+        from stableavatar_amd import sp
+        plan = sp.make_plan(world, rank, 12)
+        attn_flop /= world  # this rank's (head group, query part) share
+        parallelism = f"ulysses{plan.G}" + (f"x{plan.R}qsplit" if plan.R > 1 else "")
     achieved = attn_flop / (attn_ms * 1e-3)
     n_fwd = args.sample_steps * len(window_schedule(T, fpb, args.overlap))
     path_flop = n_fwd * flops.dit_forward_flops(B=3, L=seq_len, n_frames=fpb) + flops.vae_decode_flops(T, h, h)
-    frames_total = world * args.frames * args.steps
+    frames_total = (1 if sp_mode else world) * args.frames * args.steps
     value = frames_total / dt
     if rank == 0:
         cpu = None
@@ -172,18 +186,18 @@ def main():
             cpu = cpu_baseline(args.size, args.frames, args.sample_steps)
         out = {"metric": METRIC, "value": round(value, 4), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 1), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+               "scaling": "strong" if sp_mode else "weak", "vs_baseline": None, "dtype": "bf16",
                "data": "synthetic (random-init weights by name-keyed seed; synthetic text/CLIP/wav2vec features "
                        "and conditioning latents; CPU-generated initial noise)",
                "config": {"workload": f"Wan-1.3B StableAvatar {args.size}x{args.size}x{args.frames}f, "
                                       f"{args.sample_steps} steps, CFG x3, single audio clip, VAE decode",
-                          "global_batch": 3 * world, "seq_len": seq_len, "dit_forwards_per_clip": n_fwd,
-                          "parallelism": f"replicas{world}" if world > 1 else "single"},
-               "roofline": {"bound": "mfma", "kernel": "attn_fwd_kernel (self-attention)",
+                          "global_batch": 3 * (1 if sp_mode else world), "seq_len": seq_len,
+                          "dit_forwards_per_clip": n_fwd, "parallelism": parallelism},
+               "roofline": {"bound": "mfma", "kernel": "attn_fwd (self-attention, flash, D=128)",
                             "achieved": round(achieved / 1e12, 1), "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
                             "frac": round(achieved / PEAK_BF16, 4), "traffic": None,
                             "launch_ms": round(attn_ms, 3), "flop_per_launch": attn_flop},
-               "path_mfma_frac": round(path_flop * args.steps / dt / PEAK_BF16, 4),
+               "path_mfma_frac": round(path_flop * args.steps / dt / PEAK_BF16 / (world if sp_mode else 1), 4),
                "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     if world > 1:

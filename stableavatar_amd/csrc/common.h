@@ -41,16 +41,19 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 __device__ __forceinline__ float gelu_tanh(float x) {
-  // 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3)))  (nn.GELU(approximate='tanh'))
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float y = k0 * (x + k1 * x * x * x);
-  float t = 1.0f - 2.0f / (__expf(2.0f * y) + 1.0f);
-  return 0.5f * x * (1.0f + t);
+  // 0.5 x (1 + tanh(u)) = x / (1 + exp(-2u)),  u = sqrt(2/pi) (x + 0.044715 x^3)
+  // (nn.GELU(approximate='tanh')); 4 VALU + exp2 + rcp per element
+  const float c0 = -2.0f * 0.7978845608028654f * 1.4426950408889634f;  // -2 sqrt(2/pi) log2(e)
+  const float c1 = c0 * 0.044715f;
+  const float e = __builtin_amdgcn_exp2f(x * fmaf(c1, x * x, c0));
+  return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
 }
-__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float silu(float x) {
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+}
 
 // bijective XCD-aware remap of a flat workgroup id (cdna_hip_programming.md §5 "XCD swizzle must be bijective")
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {

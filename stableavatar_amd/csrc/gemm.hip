@@ -677,7 +677,7 @@ int launch(const GemmArgs& g, int batch, hipStream_t st) {
   static int attr = 0;
   if (g_gemm_variant < 0) {
     const char* e = getenv("SA_GEMM_VARIANT");
-    g_gemm_variant = e ? atoi(e) : 1;
+    g_gemm_variant = e ? atoi(e) : 3;
   }
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);

@@ -65,7 +65,7 @@ def main(which=("gemm", "attn")):
             res.append(r)
             print(json.dumps(r), flush=True)
             del x, w, out
-        call("sa_gemm_set_variant", 1)
+        call("sa_gemm_set_variant", 3)
     if "attnvar" in which:
         L, H, D = 21504, 12, 128
         qkv = torch.randn(3 * L, 3 * H * D, device=dev).bfloat16()

@@ -23,7 +23,7 @@ from types import SimpleNamespace
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import ops, sp
 
 
 def rope_params(max_seq_len: int, dim: int, theta: float = 10000.0) -> torch.Tensor:
@@ -479,21 +479,24 @@ class WanTransformer3DFantasyModel(nn.Module):
         Hh, Ww = lat.shape[3], lat.shape[4]
         hp, wp = Hh // 2, Ww // 2
         real = Fw * hp * wp
-        Lp = int(seq_len)
-        if self.sp_world_size > 1:
-            Lp = int(math.ceil(Lp / self.sp_world_size)) * self.sp_world_size
+        NS, rank = self.sp_world_size, self.sp_world_rank
+        Lp = sp.padded_len(int(seq_len), NS)
         assert real <= Lp, "seq_len smaller than the token count"
-        M = B * Lp
-        ws = self._workspace(M, dev)
+        Lc = Lp // NS  # tokens of each CFG row held by this rank (all of them without SP)
+        ws = self._workspace(B * Lc, dev)
 
-        # patch embedding (1B:972-983): im2col + GEMM, padding rows zero
+        # patch embedding (1B:972-983): im2col + GEMM, padding rows zero; with SP every rank embeds
+        # the whole sequence (the vocal projector reads it, 1B:1004-1009) and keeps its chunk (1B:1019)
         cols = torch.empty(B, Lp, pk.kpad, device=dev, dtype=torch.bfloat16)
         ops.patch_im2col(lat, y, B, Fw, Hh, Ww, cols, pk.kpad, Lp, x_frame_offset=frame_offset,
                          x_batch_broadcast=broadcast)
-        call_gemm_batched(cols, pk.w_pe, pk.b_pe, ws.x, B, real, Lp, dim, pk.kpad)
+        xfull = ws.x if NS == 1 else torch.empty(B * Lp, dim, device=dev, dtype=torch.float32)
+        call_gemm_batched(cols, pk.w_pe, pk.b_pe, xfull, B, real, Lp, dim, pk.kpad)
         if real < Lp:
             for b in range(B):
-                ops.fill_(ws.x[b * Lp + real:(b + 1) * Lp], 0.0)
+                ops.fill_(xfull[b * Lp + real:(b + 1) * Lp], 0.0)
+        if NS > 1:
+            ws.x.view(B, Lc, dim).copy_(xfull.view(B, Lp, dim)[:, rank * Lc:(rank + 1) * Lc])
 
         # time embedding (fp32, 1B:986-990)
         tt = t.to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
@@ -526,7 +529,7 @@ class WanTransformer3DFantasyModel(nn.Module):
         voc_rows = []
         for r in range(rows_v):
             src = B - 1 if rows_v == 1 else r
-            ops.cast_bf16(ws.x[src * Lp:(src + 1) * Lp], lat_row)
+            ops.cast_bf16(xfull[src * Lp:(src + 1) * Lp], lat_row)
             vv, Fn, nper = self._vocal(pk, vocal_embeddings[src], video_sample_n_frames, lat_row, Lp,
                                        e0[src:src + 1], e[src:src + 1], dev)
             voc_rows.append(vv)
@@ -540,55 +543,69 @@ class WanTransformer3DFantasyModel(nn.Module):
         vctx = vctx.view(B * Fn * nper, dim)
 
         G = Lp // n_fr
-        segs_self = self._segs.get(("self", B, Lp), [[b * Lp, Lp, b * Lp, Lp] for b in range(B)], dev)
-        segs_txt = self._segs.get(("txt", B, Lp, ctx.text_len),
-                                  [[b * Lp, Lp, b * ctx.text_len, ctx.text_len] for b in range(B)], dev)
-        segs_img = self._segs.get(("img", B, Lp, ctx.img_len),
-                                  [[b * Lp, Lp, b * ctx.img_len, ctx.img_len] for b in range(B)], dev)
-        segs_voc = self._segs.get(("voc", B, Lp, n_fr, nper),
-                                  [[b * Lp + f * G, G, (b * n_fr + f) * nper, nper]
-                                   for b in range(B) for f in range(n_fr)], dev)
+        if NS > 1:
+            plan = sp.make_plan(NS, rank, H_)
+            exch = sp.UlyssesExchange(plan, self.sp_group)
+            Lq, hg = plan.G * Lc, plan.hg
+            segs_self = self._segs.get(("self_sp", B, Lp, Lq), [[b * Lq, Lq, b * Lp, Lp] for b in range(B)], dev)
+            o_sp = torch.empty(B * Lq, hg * self.d, device=dev, dtype=torch.bfloat16)
+        else:
+            segs_self = self._segs.get(("self", B, Lp), [[b * Lp, Lp, b * Lp, Lp] for b in range(B)], dev)
+        segs_txt = self._segs.get(("txt", B, Lc, ctx.text_len), sp.local_segments(B, Lc, ctx.text_len), dev)
+        segs_img = self._segs.get(("img", B, Lc, ctx.img_len), sp.local_segments(B, Lc, ctx.img_len), dev)
+        voc_list = sp.vocal_segments(B, Lp, Lc, rank, n_fr, nper)
+        segs_voc = self._segs.get(("voc", B, Lp, Lc, rank, n_fr, nper), voc_list, dev)
+        voc_n, voc_q = len(voc_list), max(s_[1] for s_ in voc_list)
         x = ws.x
         kvv = torch.empty(B * n_fr * nper, 2 * dim, device=dev, dtype=torch.bfloat16)  # per-frame vocal K|V
         grid = (Fw, hp, wp)
         for li, L in enumerate(pk.layers):
             em = emod[li]  # [B, 6, dim]
             # self-attention (1B:675-679)
-            ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 0], scale=em[:, 1], rows_per_batch=Lp)
+            ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 0], scale=em[:, 1], rows_per_batch=Lc)
             ops.linear(ws.mod, L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv)
-            ops.qk_rmsnorm_rope(ws.qkv, 0, dim, L.nq, L.nk, dim, self.eps, rope=pk.rope, rows_per_batch=Lp,
-                                grid=grid, head_dim=self.d, n_frame_pairs=self.d // 2 - 2 * (self.d // 6),
-                                n_height_pairs=self.d // 6)
-            if self._events is not None:
+            ops.qk_rmsnorm_rope(ws.qkv, 0, dim, L.nq, L.nk, dim, self.eps, rope=pk.rope, rows_per_batch=Lc,
+                                tok_offset=rank * Lc, grid=grid, head_dim=self.d,
+                                n_frame_pairs=self.d // 2 - 2 * (self.d // 6), n_height_pairs=self.d // 6)
+            if NS > 1:  # Ulysses: tokens -> heads, full-sequence attention, heads -> tokens
+                q_sp, kv_sp = exch.to_heads(ws.qkv, B, Lc, self.d)
+                args_ = (q_sp, kv_sp[:, :hg * self.d], kv_sp[:, hg * self.d:], o_sp, segs_self, B, Lq, hg)
+            else:
+                args_ = (ws.qkv[:, :dim], ws.qkv[:, dim:2 * dim], ws.qkv[:, 2 * dim:], ws.att, segs_self, B, Lp, H_)
+            if self._events is not None:  # bench.py: HIP events around the self-attention kernel
                 ev0 = torch.cuda.Event(enable_timing=True)
                 ev0.record()
-            ops.attention(ws.qkv[:, :dim], ws.qkv[:, dim:2 * dim], ws.qkv[:, 2 * dim:], ws.att, segs_self, B, Lp, H_)
+            ops.attention(*args_)
             if self._events is not None:
                 ev1 = torch.cuda.Event(enable_timing=True)
                 ev1.record()
                 self._events.append((ev0, ev1))
-            ops.linear(ws.att, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2], rows_per_batch=Lp)
+            if NS > 1:
+                exch.to_tokens(o_sp, B, Lc, self.d, ws.att)
+            ops.linear(ws.att, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2], rows_per_batch=Lc)
             # cross-attention: text + image + per-frame vocal (1B:534-605, 684)
             ops.layernorm_mod(x, ws.mod, self.eps, weight=L.n3w, bias=L.n3b)
             qc = ws.qkv[:, :dim]
             ops.linear(ws.mod, L.w_cq, L.b_cq, ops.EPI_BF16, out=qc)
             ops.qk_rmsnorm_rope(qc, 0, -1, L.cnq, None, dim, self.eps)
             kvt, kvi = ctx.kv[li]
-            ops.attention(qc, kvt[:, :dim], kvt[:, dim:], ws.att, segs_txt, B, Lp, H_)
+            ops.attention(qc, kvt[:, :dim], kvt[:, dim:], ws.att, segs_txt, B, Lc, H_)
             if kvi is not None:
-                ops.attention(qc, kvi[:, :dim], kvi[:, dim:], ws.att, segs_img, B, Lp, H_, accumulate=True)
+                ops.attention(qc, kvi[:, :dim], kvi[:, dim:], ws.att, segs_img, B, Lc, H_, accumulate=True)
             ops.linear(vctx, L.w_kv_v, L.b_kv_v, ops.EPI_BF16, out=kvv)
-            ops.attention(qc, kvv[:, :dim], kvv[:, dim:], ws.att, segs_voc, B * n_fr, G, H_, accumulate=True)
+            ops.attention(qc, kvv[:, :dim], kvv[:, dim:], ws.att, segs_voc, voc_n, voc_q, H_, accumulate=True)
             ops.linear(ws.att, L.w_co, L.b_co, ops.EPI_RES_F32, out=x, residual=x)
             # FFN (1B:687-691)
-            ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 3], scale=em[:, 4], rows_per_batch=Lp)
+            ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 3], scale=em[:, 4], rows_per_batch=Lc)
             ops.linear(ws.mod, L.w_f0, L.b_f0, ops.EPI_GELU_TANH_BF16, out=ws.ffn)
-            ops.linear(ws.ffn, L.w_f2, L.b_f2, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 5], rows_per_batch=Lp)
+            ops.linear(ws.ffn, L.w_f2, L.b_f2, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 5], rows_per_batch=Lc)
 
         # head (1B:715-723) + unpatchify (1B:1161-1184)
         hm = hmod[0]
-        ops.layernorm_mod(x, ws.mod, self.eps, shift=hm[:, 0], scale=hm[:, 1], rows_per_batch=Lp)
+        ops.layernorm_mod(x, ws.mod, self.eps, shift=hm[:, 0], scale=hm[:, 1], rows_per_batch=Lc)
         ho = ops.linear(ws.mod, pk.w_head, pk.b_head, ops.EPI_BF16)
+        if NS > 1:  # every rank gets the whole prediction (1B:1150-1152)
+            ho = sp.gather_tokens(ho, B, Lc, NS, self.sp_group)
         if out is None:
             out = torch.empty(B, self.out_dim, Fw, Hh, Ww, device=dev, dtype=torch.bfloat16)
         ops.unpatchify(ho, Lp, B, self.out_dim, Fw, Hh, Ww, out)

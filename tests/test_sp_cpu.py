@@ -1,0 +1,102 @@
+"""Sequence-parallel exchange (stableavatar_amd/sp.py) on CPU with gloo, world sizes 2/3/4/8.
+
+Pins the identity the reference's SP path is meant to hold (xfuser row): attention
+over the token-sharded, head-exchanged layout equals single-device full attention (1B:158-207 SDPA),
+plus the single-GPU frame grouping of the per-frame vocal attention and the head all-gather.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from stableavatar_amd import sp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _sdpa(q, k, v):
+    # q [B, Lq, h, D], k/v [B, Lk, h, D] -> [B, Lq, h, D], fp32 softmax(QK^T/sqrt(D))V
+    s = torch.einsum("bqhd,bkhd->bhqk", q, k) / q.shape[-1] ** 0.5
+    return torch.einsum("bhqk,bkhd->bqhd", s.softmax(-1), v)
+
+
+def _worker(rank, world, port, B, Lp, H, D, q_ret):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(7)
+        qkv = torch.randn(B, Lp, 3, H, D, generator=g)
+        ref = _sdpa(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2])          # [B, Lp, H, D]
+        plan = sp.make_plan(world, rank, H)
+        Lc = Lp // world
+        mine = qkv[:, rank * Lc:(rank + 1) * Lc].reshape(B * Lc, 3 * H * D).contiguous()
+        ex = sp.UlyssesExchange(plan)
+        q, kv = ex.to_heads(mine, B, Lc, D)
+        hg = plan.hg
+        Lq = q.shape[0] // B
+        assert Lq == Lp // plan.R
+        qh = q.view(B, Lq, hg, D)
+        kvh = kv.view(B, Lp, 2, hg, D)
+        o = _sdpa(qh, kvh[:, :, 0], kvh[:, :, 1]).reshape(B * Lq, hg * D).contiguous()
+        out = torch.empty(B * Lc, H * D)
+        ex.to_tokens(o, B, Lc, D, out)
+        err = (out.view(B, Lc, H, D) - ref[:, rank * Lc:(rank + 1) * Lc]).abs().max().item()
+        full = sp.gather_tokens(out, B, Lc, world)
+        gerr = (full.view(B, Lp, H, D) - ref).abs().max().item()
+        q_ret.put((rank, err, gerr, plan.G, plan.R))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_ulysses_exchange_matches_full_attention(world):
+    B, H, D = 3, 12, 16
+    Lp = sp.padded_len(48, world)
+    ctx = mp.get_context("spawn")
+    qret = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, B, Lp, H, D, qret)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [qret.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, err, gerr, G, R in res:
+        assert err < 1e-5 and gerr < 1e-5, (rank, err, gerr)
+        assert G * R == world and H % G == 0
+
+
+def test_plan_shapes():
+    assert (sp.make_plan(8, 5, 12).G, sp.make_plan(8, 5, 12).R) == (4, 2)
+    assert (sp.make_plan(2, 1, 12).G, sp.make_plan(2, 1, 12).R) == (2, 1)
+    assert (sp.make_plan(4, 0, 12).G, sp.make_plan(4, 0, 12).R) == (4, 1)
+    assert sp.padded_len(21504, 8) == 21504 and sp.padded_len(21505, 8) == 21512
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_vocal_segments_use_global_frames(world):
+    """Union over ranks of the local segments == the single-GPU grouping q.view(B*F, -1) (1B:576)."""
+    B, n_fr, nper, G = 3, 21, 17, 1024
+    Lp = n_fr * G
+    Lc = Lp // world
+    seen = {}
+    for r in range(world):
+        for q0, ql, k0, kl in sp.vocal_segments(B, Lp, Lc, r, n_fr, nper):
+            b = q0 // Lc
+            for t in range(q0 - b * Lc, q0 - b * Lc + ql):
+                gt = r * Lc + t
+                seen[(b, gt)] = (k0, kl)
+    assert len(seen) == B * Lp
+    for (b, gt), (k0, kl) in seen.items():
+        assert k0 == (b * n_fr + gt // G) * nper and kl == nper
