@@ -130,6 +130,16 @@ def main(which=("gemm", "attn")):
         res.append({"kernel": "attn_self", "L": L, "ms": round(ms, 3), "tflops": round(fl / ms / 1e9, 1),
                     "torch_sdpa_ms": round(ms_ref, 3), "torch_tflops": round(fl / ms_ref / 1e9, 1)})
         print(json.dumps(res[-1]), flush=True)
+    if "attn1" in which:  # 3 bare self-attention launches (PMC passes: FETCH_SIZE / WRITE_SIZE)
+        L, H, D = 21504, 12, 128
+        qkv = torch.randn(3 * L, 3 * H * D, device=dev).bfloat16()
+        o = torch.empty(3 * L, H * D, device=dev, dtype=torch.bfloat16)
+        segs = torch.tensor([[b * L, L, b * L, L] for b in range(3)], dtype=torch.int32, device=dev)
+        for _ in range(3):
+            ops.attention(qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:], o, segs, 3, L, H)
+        torch.cuda.synchronize()
+        res.append({"kernel": "attn_self_x3", "algorithmic_bytes_per_launch": 4 * 3 * L * H * D * 2})
+        print(json.dumps(res[-1]), flush=True)
     if "dit" in which:
         res.append(bench_dit())
         print(json.dumps(res[-1]), flush=True)
