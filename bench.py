@@ -169,6 +169,13 @@ def main():
         dt = tt.item()
     attn_ms = sum(e0.elapsed_time(e1) for e0, e1 in events) / max(len(events), 1)
     attn_flop = flops.self_attention_flops(B=3, L=seq_len)
+    traffic, traffic_src = None, None
+    tpath = os.path.join(ROOT, "profiles", "pmc_attn_traffic.json")
+    if os.path.exists(tpath) and not args.sp and seq_len == 21504:
+        with open(tpath) as f:
+            tj = json.load(f)
+        traffic = tj["hbm_bytes_per_launch"]
+        traffic_src = f"profiles/pmc_attn_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, {tj['kernel'][:60]})"
     parallelism = f"replicas{world}" if world > 1 else "single"
     if sp_mode:
         from stableavatar_amd import sp
@@ -195,7 +202,8 @@ def main():
                           "dit_forwards_per_clip": n_fwd, "parallelism": parallelism},
                "roofline": {"bound": "mfma", "kernel": "attn_fwd (self-attention, flash, D=128)",
                             "achieved": round(achieved / 1e12, 1), "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
-                            "frac": round(achieved / PEAK_BF16, 4), "traffic": None,
+                            "frac": round(achieved / PEAK_BF16, 4), "traffic": traffic, "traffic_source": traffic_src,
+                            "algorithmic_bytes": 4 * 3 * seq_len * 1536 * 2,
                             "launch_ms": round(attn_ms, 3), "flop_per_launch": attn_flop},
                "path_mfma_frac": round(path_flop * args.steps / dt / PEAK_BF16 / (world if sp_mode else 1), 4),
                "cpu_baseline": cpu}

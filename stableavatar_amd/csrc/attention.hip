@@ -552,9 +552,13 @@ __device__ __forceinline__ void attn_v3_block(V3State& st, const bf16x8* qf, con
 
 __global__ __launch_bounds__(512) void attn_fwd_v3_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int* sg = a.segs + blockIdx.z * 4;
+  // XCD-aware order (T1): consecutive query blocks of one (segment, head) share an XCD, so its L2
+  // serves their common K/V stream
+  const int nx = gridDim.x, ny = gridDim.y;
+  const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
+  const int qb = flat % nx, h = (flat / nx) % ny, seg = flat / (nx * ny);
+  const int* sg = a.segs + seg * 4;
   const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
-  const int qb = blockIdx.x, h = blockIdx.y;
   if (qb * QB >= q_len || kv_len <= 0) return;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);

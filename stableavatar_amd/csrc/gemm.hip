@@ -63,12 +63,18 @@ __device__ __forceinline__ void epi_row(const GemmArgs& g, float* v, long bz, in
   if (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16) {
     bf16* C = (bf16*)g.C + bz * g.sC + (long)grow * g.ldc + gcol;
     if (full) {
+      if constexpr (NC % 8 == 0) {
 #pragma unroll
-      for (int h = 0; h < NC / 8; ++h) {
-        bf16x8 o;
+        for (int h = 0; h < NC / 8; ++h) {
+          bf16x8 o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = f2bf(v[8 * h + j]);
-        *(bf16x8*)(C + 8 * h) = o;
+          for (int j = 0; j < 8; ++j) o[j] = f2bf(v[8 * h + j]);
+          *(bf16x8*)(C + 8 * h) = o;
+        }
+      } else {
+#pragma unroll
+        for (int h = 0; h < NC / 4; ++h)
+          *(bf16x4*)(C + 4 * h) = (bf16x4){f2bf(v[4 * h]), f2bf(v[4 * h + 1]), f2bf(v[4 * h + 2]), f2bf(v[4 * h + 3])};
       }
     } else {
       for (int j = 0; j < NC; ++j) if (gcol + j < g.N) C[j] = f2bf(v[j]);
@@ -275,7 +281,9 @@ __global__ __launch_bounds__(512) void gemm_phased_kernel(GemmArgs g) {
 // still in flight) before each phase's first barrier retires whatever the next phase reads.  Each
 // slot is restaged >= 2 phases after its last read, except A0 (1 phase), whose reads are retired by
 // an lgkmcnt(0) before the reading phase's first barrier.
-template <int EPI>
+// DIRECT: operands swapped in the MFMA (C^T = W·A^T), so each lane holds 4 consecutive output
+// columns of one row and the epilogue stores straight from the accumulators (no LDS transpose).
+template <int EPI, bool DIRECT>
 __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -360,7 +368,12 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int n = 0; n < 2; ++n) c[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m][kk], b[n][kk], c[m][n], 0, 0, 0);
+        for (int n = 0; n < 2; ++n) {
+          if constexpr (DIRECT)
+            c[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[n][kk], a[m][kk], c[m][n], 0, 0, 0);
+          else
+            c[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m][kk], b[n][kk], c[m][n], 0, 0, 0);
+        }
     __builtin_amdgcn_s_setprio(0);
   };
 #define SA_PP_MID(FULL)                                                   \
@@ -434,6 +447,21 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
 #undef SA_PP_END
   if (!g1) __builtin_amdgcn_s_barrier();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (DIRECT) {
+    const int qa[4] = {0, 0, 1, 1}, qb[4] = {0, 1, 1, 0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          const int grow = m0 + qa[q] * 128 + qm * 64 + m * 16 + (lane & 15);
+          const int gcol = n0 + qb[q] * 128 + qn * 32 + n * 16 + (lane >> 4) * 4;
+          float v[4] = {acc[q][m][n][0], acc[q][m][n][1], acc[q][m][n][2], acc[q][m][n][3]};
+          if (grow < g.M && gcol < g.N) epi_row<EPI, 4>(g, v, bz, grow, gcol);
+        }
+    return;
+  }
   __syncthreads();
 
   float* strip = (float*)(smem + wave * (16 * 36 * 4));
@@ -670,7 +698,7 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(GemmArgs g) {
 }
 
 int g_gemm_variant = -1;  // 0 = v1 (2-phase), 1 = phased (8 waves), 2 = w4 (4 waves, AGPR accumulators),
-                          // 3 = ping-pong 8-phase
+                          // 3 = ping-pong 8-phase, 4 = ping-pong with direct (operand-swapped) epilogue
 
 template <int EPI>
 int launch(const GemmArgs& g, int batch, hipStream_t st) {
@@ -684,7 +712,10 @@ int launch(const GemmArgs& g, int batch, hipStream_t st) {
     (void)hipFuncSetAttribute((const void*)gemm_phased_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_w4_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, W4_LDS);
-    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
     attr = 1;
   }
   const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
@@ -694,8 +725,10 @@ int launch(const GemmArgs& g, int batch, hipStream_t st) {
     hipLaunchKernelGGL(gemm_phased_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
   else if (g_gemm_variant == 2)
     hipLaunchKernelGGL(gemm_w4_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(256), W4_LDS, st, g);
+  else if (g_gemm_variant == 3)
+    hipLaunchKernelGGL((gemm_pp_kernel<EPI, false>), dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
   else
-    hipLaunchKernelGGL(gemm_pp_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
+    hipLaunchKernelGGL((gemm_pp_kernel<EPI, true>), dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
   SA_LAUNCH_CHECK();
   return SA_OK;
 }
@@ -703,7 +736,7 @@ int launch(const GemmArgs& g, int batch, hipStream_t st) {
 }  // namespace
 
 extern "C" int sa_gemm_set_variant(int variant) {
-  if (variant < 0 || variant > 3) return SA_ERR_ARG;
+  if (variant < 0 || variant > 4) return SA_ERR_ARG;
   g_gemm_variant = variant;
   return SA_OK;
 }

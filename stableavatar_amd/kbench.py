@@ -39,7 +39,7 @@ def main(which=("gemm", "attn")):
             out = torch.empty(M, N, device=dev, dtype=torch.float32 if epi == ops.EPI_RES_F32 else torch.bfloat16)
             gate = torch.randn(3, N, device=dev)
             ref = None
-            gvars = (1, 3)
+            gvars = (3, 4)
             times = {v: [] for v in gvars}
             for rnd in range(3):
                 for v in gvars:
@@ -72,7 +72,7 @@ def main(which=("gemm", "attn")):
         segs = torch.tensor([[b * L, L, b * L, L] for b in range(3)], dtype=torch.int32, device=dev)
         q, k, v_ = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
         outs = {}
-        variants = (0, 3, 4)
+        variants = (0, 3)
         times = {v: [] for v in variants}
         for rnd in range(3):
             for v in variants:
