@@ -37,8 +37,10 @@ int sa_gemm_bf16(const void* A, int64_t lda, int64_t strideA, const void* W, int
                  int64_t gate_bstride, int rows_per_batch, void* stream);
 
 /* Kernel-variant selection for A/B benchmarking in one process (also env SA_GEMM_VARIANT /
- * SA_ATTN_VARIANT).  gemm: 0 = 2-phase 8-wave, 1 = 4-phase 8-wave, 2 = 4-wave AGPR (default);
- * attention: 0 = 2-deep ring (default), 1 = 3-deep ring with pipelined QK^T. */
+ * SA_ATTN_VARIANT).  gemm: 0 = 2-phase 8-wave, 1 = 4-phase 8-wave, 2 = 4-wave AGPR, 3 = 8-phase
+ * ping-pong (default), 4 = ping-pong with operand-swapped direct epilogue; attention: 0 = 2-deep ring,
+ * 1 = 3-deep ring with pipelined QK^T, 2 = 0 + deferred rescale, 3 = asm LDS reads with counted waits +
+ * XCD order (default), 4 = 3 + two-group ping-pong. */
 int sa_gemm_set_variant(int variant);
 int sa_attn_set_variant(int variant);
 
@@ -50,6 +52,17 @@ int sa_attn_set_variant(int variant);
 int sa_attn_fwd(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg, int max_q_len,
                 int heads, int head_dim, int64_t q_stride, int64_t k_stride, int64_t v_stride, int64_t o_stride,
                 float scale, int accumulate, void* stream);
+
+/* The three attentions of WanI2VTalkingCrossAttention.forward (1B:556-603) in one launch: per batch
+ * row b, queries q[b*q_len + i] attend to text k/v rows [b*t_len, +t_len), image rows [b*i_len, +i_len)
+ * and the vocal rows of their latent frame, [(b*n_frames + f)*nper, +nper) with
+ * f = (tok_offset + i) / tokens_per_frame (1B:575-586 on the unsharded sequence); the outputs are
+ * summed as bf16((bf16(text) + bf16(img))) + bf16(vocal) (1B:602) into o.  head_dim 128;
+ * tokens_per_frame and tok_offset multiples of 256. */
+int sa_attn_cross3(const void* q, int64_t q_stride, const void* kt, const void* vt, int64_t t_stride, int t_len,
+                   const void* ki, const void* vi, int64_t i_stride, int i_len, const void* kv, const void* vv,
+                   int64_t v_stride, int nper, int tokens_per_frame, int n_frames, int tok_offset, void* o,
+                   int64_t o_stride, int batch, int q_len, int heads, float scale, void* stream);
 
 /* attention for head dims other than 128 and few queries per segment (vocal projector D=192,
  * vocal_projector_fantasy_1B.py:259-270): exact softmax, fp32 math, kv_len <= 4096, head_dim <= 256. */

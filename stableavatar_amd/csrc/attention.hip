@@ -909,6 +909,158 @@ __global__ __launch_bounds__(512) void attn_fwd_v4_kernel(AttnArgs a) {
   }
 }
 
+// ---- fused cross-attention of WanI2VTalkingCrossAttention (1B:556-603): per query block, the text
+// (1B:564-570), image (1B:556-562) and per-frame vocal (1B:575-586) attentions run back to back over
+// one K/V block stream, each with its own online softmax, and the three outputs are summed with the
+// reference's bf16 rounding, (bf16(text) + bf16(img)) + bf16(vocal) (1B:602), so Q is read once and O
+// written once.  A query block must lie inside one latent frame (tokens_per_frame % 256 == 0).
+struct Cross3Args {
+  const bf16* q; long qs;
+  const bf16* kt; const bf16* vt; long ts; int t_len;
+  const bf16* ki; const bf16* vi; long is; int i_len;
+  const bf16* kv; const bf16* vv; long vs; int nper, tpf, n_frames, tok_offset;
+  bf16* o; long os;
+  int q_len;
+  float c;
+};
+
+__global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nx = gridDim.x, ny = gridDim.y;
+  const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
+  const int qb = flat % nx, h = (flat / nx) % ny, b = flat / (nx * ny);
+  if (qb * QB >= a.q_len) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5;
+  const int q_row0 = b * a.q_len;
+  const int frame = (a.tok_offset + qb * QB) / a.tpf;
+
+  const int qi = qb * QB + wave * 32 + (lane & 31);
+  const int qc = min(qi, a.q_len - 1);
+  const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * hi;
+  bf16x8 qf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
+
+  // block stream: text blocks, image blocks, vocal block(s)
+  const int nT = (a.t_len + KVB - 1) / KVB, nI = (a.i_len + KVB - 1) / KVB, nV = (a.nper + KVB - 1) / KVB;
+  const int ntot = nT + nI + nV;
+  int srow[2], schunk[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    srow[i] = (wave * 2 + i) * 4 + (lane >> 4);
+    schunk[i] = (lane & 15) ^ gsw(srow[i]);
+  }
+  auto stage = [&](int j, int buf) {
+    const bf16 *kb, *vb;
+    long st;
+    int row0, len, blk;
+    if (j < nT) {
+      kb = a.kt; vb = a.vt; st = a.ts; row0 = b * a.t_len; len = a.t_len; blk = j;
+    } else if (j < nT + nI) {
+      kb = a.ki; vb = a.vi; st = a.is; row0 = b * a.i_len; len = a.i_len; blk = j - nT;
+    } else {
+      kb = a.kv; vb = a.vv; st = a.vs; row0 = (b * a.n_frames + frame) * a.nper; len = a.nper; blk = j - nT - nI;
+    }
+    char* base = smem + buf * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long key = row0 + min(blk * KVB + srow[i], len - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(kb + key * st + h * D + schunk[i] * 8),
+                                       LDS_PTR(base + (wave * 2 + i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(vb + key * st + h * D + schunk[i] * 8),
+                                       LDS_PTR(base + TILE_BYTES + (wave * 2 + i) * 1024), 16, 0, 0);
+    }
+  };
+
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
+  uint32_t ka[8], va[8];
+  {
+    const int row = lane & 31;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) ka[s] = lds0 + row * 256 + (((2 * s + hi) ^ gsw(row)) << 4);
+    const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int r = 4 * hi + q4 + 8 * hh;
+        const int col = db * 32 + 16 * ((lane >> 4) & 1) + 4 * p4;
+        va[2 * db + hh] = lds0 + r * 256 + (((col >> 3) ^ gsw(r)) << 4) + 8 * ((col >> 2) & 1);
+      }
+  }
+
+  V3State st;
+  auto reset = [&]() {
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st.O[db][r] = 0.f;
+    st.m_run = -INFINITY;
+    st.l_run = 0.f;
+  };
+  reset();
+  bf16x2 acc[32];  // running (text + img) + vocal, bf16 as in the reference
+  // finish source `src` (0 text, 1 image, 2 vocal): bf16(O / l) folded into acc
+  auto finish = [&](int src) {
+    const float lt = st.l_run + __shfl_xor(st.l_run, 32, 64);
+    const float inv = 1.0f / lt;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const bf16 x0 = f2bf(st.O[db][r] * inv), x1 = f2bf(st.O[db][r + 1] * inv);
+        bf16x2& s = acc[db * 8 + r / 2];
+        if (src == 0) {
+          s = (bf16x2){x0, x1};
+        } else {
+          s = (bf16x2){f2bf(bf2f(s[0]) + bf2f(x0)), f2bf(bf2f(s[1]) + bf2f(x1))};
+        }
+      }
+    reset();
+  };
+
+  stage(0, 0);
+  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  for (int j = 0; j < ntot; j += 2) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (j + 1 < ntot) stage(j + 1, 1);
+    {
+      const int src = j < nT ? 0 : (j < nT + nI ? 1 : 2);
+      const int kb = src == 0 ? j : (src == 1 ? j - nT : j - nT - nI);
+      const int len = src == 0 ? a.t_len : (src == 1 ? a.i_len : a.nper);
+      attn_v3_block<0>(st, qf, ka, va, kb, len, a.c, hi);
+      if (j == nT - 1 || j == nT + nI - 1 || j == ntot - 1) finish(src);
+    }
+    if (j + 1 >= ntot) break;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (j + 2 < ntot) stage(j + 2, 0);
+    {
+      const int jj = j + 1;
+      const int src = jj < nT ? 0 : (jj < nT + nI ? 1 : 2);
+      const int kb = src == 0 ? jj : (src == 1 ? jj - nT : jj - nT - nI);
+      const int len = src == 0 ? a.t_len : (src == 1 ? a.i_len : a.nper);
+      attn_v3_block<1>(st, qf, ka, va, kb, len, a.c, hi);
+      if (jj == nT - 1 || jj == nT + nI - 1 || jj == ntot - 1) finish(src);
+    }
+  }
+
+  if (qi < a.q_len) {
+    bf16* op = a.o + (long)(q_row0 + qi) * a.os + h * D;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const int d0 = db * 32 + 8 * r4 + 4 * hi;
+        const bf16x2 lo = acc[db * 8 + 2 * r4], hv = acc[db * 8 + 2 * r4 + 1];
+        *(bf16x4*)(op + d0) = (bf16x4){lo[0], lo[1], hv[0], hv[1]};
+      }
+  }
+}
+
 // ---- small-query attention for head dims the MFMA kernel does not take (vocal projector, D=192,
 // 17 queries per frame vs 1024 latent tokens: vocal_projector_fantasy_1B.py:259-270).  One wave
 // per (segment, head, query): scores for all keys in LDS, exact softmax, lane-parallel P·V.
@@ -1023,6 +1175,36 @@ extern "C" int sa_attn_fwd(const void* q, const void* k, const void* v, void* o,
     hipLaunchKernelGGL(attn_fwd_v4_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(attn_fwd_v2_kernel, grid, dim3(512), LDS_BYTES_V2, (hipStream_t)stream, a);
+  SA_LAUNCH_CHECK();
+  return SA_OK;
+}
+
+extern "C" int sa_attn_cross3(const void* q, int64_t q_stride, const void* kt, const void* vt, int64_t t_stride,
+                              int t_len, const void* ki, const void* vi, int64_t i_stride, int i_len, const void* kv,
+                              const void* vv, int64_t v_stride, int nper, int tokens_per_frame, int n_frames,
+                              int tok_offset, void* o, int64_t o_stride, int batch, int q_len, int heads,
+                              float scale, void* stream) {
+  if (!q || !kt || !vt || !ki || !vi || !kv || !vv || !o) return SA_ERR_ARG;
+  if (batch <= 0 || q_len <= 0 || heads <= 0 || t_len <= 0 || i_len <= 0 || nper <= 0 || n_frames <= 0)
+    return SA_ERR_ARG;
+  if (tokens_per_frame <= 0 || tokens_per_frame % QB != 0 || tok_offset < 0 || tok_offset % QB != 0 ||
+      (long)n_frames * tokens_per_frame < (long)tok_offset + q_len)
+    return SA_ERR_ARG;
+  if ((q_stride | t_stride | i_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
+  if ((((uintptr_t)q) | ((uintptr_t)kt) | ((uintptr_t)vt) | ((uintptr_t)ki) | ((uintptr_t)vi) | ((uintptr_t)kv) |
+       ((uintptr_t)vv) | ((uintptr_t)o)) & 15)
+    return SA_ERR_ARG;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)attn_cross3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
+    attr = true;
+  }
+  Cross3Args a{(const bf16*)q, q_stride, (const bf16*)kt, (const bf16*)vt, t_stride, t_len, (const bf16*)ki,
+               (const bf16*)vi, i_stride, i_len, (const bf16*)kv, (const bf16*)vv, v_stride, nper,
+               tokens_per_frame, n_frames, tok_offset, (bf16*)o, o_stride, q_len, scale * 1.4426950408889634f};
+  dim3 grid((q_len + QB - 1) / QB, heads, batch);
+  hipLaunchKernelGGL(attn_cross3_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
   SA_LAUNCH_CHECK();
   return SA_OK;
 }

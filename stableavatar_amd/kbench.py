@@ -140,6 +140,22 @@ def main(which=("gemm", "attn")):
         torch.cuda.synchronize()
         res.append({"kernel": "attn_self_x3", "algorithmic_bytes_per_launch": 4 * 3 * L * H * D * 2})
         print(json.dumps(res[-1]), flush=True)
+    if "gemm1" in which:  # one launch of each DiT GEMM shape (PMC passes)
+        for (N, K, epi, name) in [(4608, 1536, ops.EPI_BF16, "qkv"), (1536, 1536, ops.EPI_RES_F32, "o_proj"),
+                                  (8960, 1536, ops.EPI_GELU_TANH_BF16, "ffn_up"),
+                                  (1536, 8960, ops.EPI_RES_F32, "ffn_down")]:
+            x = torch.randn(M, K, device=dev).bfloat16()
+            w = (torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
+            b = torch.randn(N, device=dev)
+            out = torch.zeros(M, N, device=dev, dtype=torch.float32 if epi == ops.EPI_RES_F32 else torch.bfloat16)
+            if epi == ops.EPI_RES_F32:
+                ops.linear(x, w, b, epi, out=out, residual=out)
+            else:
+                ops.linear(x, w, b, epi, out=out)
+            torch.cuda.synchronize()
+            del x, w, out
+        res.append({"kernel": "gemm_x4"})
+        print(json.dumps(res[-1]), flush=True)
     if "dit" in which:
         res.append(bench_dit())
         print(json.dumps(res[-1]), flush=True)

@@ -88,6 +88,22 @@ def attention(q, k, v, out, segs, nseg, max_q_len, heads, head_dim=128, scale=No
     return out
 
 
+def attention_cross3(q, kt, vt, t_len, ki, vi, i_len, kv, vv, nper, tokens_per_frame, n_frames, out, batch, q_len,
+                     heads, tok_offset=0, head_dim=128, scale=None):
+    """Text + image + per-frame vocal cross-attention summed in bf16 (1B:556-603), one launch."""
+    for t, n in ((q, "q"), (kt, "kt"), (vt, "vt"), (ki, "ki"), (vi, "vi"), (kv, "kv"), (vv, "vv"), (out, "out")):
+        _check(t, torch.bfloat16, f"attention_cross3.{n}")
+        assert t.stride(-1) == 1
+    assert kt.stride(0) == vt.stride(0) and ki.stride(0) == vi.stride(0) and kv.stride(0) == vv.stride(0)
+    if scale is None:
+        scale = head_dim ** -0.5
+    call("sa_attn_cross3", q.data_ptr(), q.stride(0), kt.data_ptr(), vt.data_ptr(), kt.stride(0), t_len,
+         ki.data_ptr(), vi.data_ptr(), ki.stride(0), i_len, kv.data_ptr(), vv.data_ptr(), kv.stride(0), nper,
+         tokens_per_frame, n_frames, tok_offset, out.data_ptr(), out.stride(0), batch, q_len, heads, float(scale),
+         _stream())
+    return out
+
+
 def layernorm_mod(x, out, eps, weight=None, bias=None, shift=None, scale=None, gate=None, rows_per_batch=0):
     """Row LayerNorm (+affine) (+y*(1+scale[b])+shift[b]) (+x+y*gate[b]).  x/out 2-D f32|bf16."""
     M, C = x.shape

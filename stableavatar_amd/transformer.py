@@ -556,6 +556,8 @@ class WanTransformer3DFantasyModel(nn.Module):
         voc_list = sp.vocal_segments(B, Lp, Lc, rank, n_fr, nper)
         segs_voc = self._segs.get(("voc", B, Lp, Lc, rank, n_fr, nper), voc_list, dev)
         voc_n, voc_q = len(voc_list), max(s_[1] for s_ in voc_list)
+        use_cross3 = (ctx.img_len > 0 and G % 256 == 0 and (rank * Lc) % 256 == 0
+                      and os.environ.get("SA_CROSS3", "1") != "0")
         x = ws.x
         kvv = torch.empty(B * n_fr * nper, 2 * dim, device=dev, dtype=torch.bfloat16)  # per-frame vocal K|V
         grid = (Fw, hp, wp)
@@ -589,11 +591,16 @@ class WanTransformer3DFantasyModel(nn.Module):
             ops.linear(ws.mod, L.w_cq, L.b_cq, ops.EPI_BF16, out=qc)
             ops.qk_rmsnorm_rope(qc, 0, -1, L.cnq, None, dim, self.eps)
             kvt, kvi = ctx.kv[li]
-            ops.attention(qc, kvt[:, :dim], kvt[:, dim:], ws.att, segs_txt, B, Lc, H_)
-            if kvi is not None:
-                ops.attention(qc, kvi[:, :dim], kvi[:, dim:], ws.att, segs_img, B, Lc, H_, accumulate=True)
             ops.linear(vctx, L.w_kv_v, L.b_kv_v, ops.EPI_BF16, out=kvv)
-            ops.attention(qc, kvv[:, :dim], kvv[:, dim:], ws.att, segs_voc, voc_n, voc_q, H_, accumulate=True)
+            if use_cross3:  # text + image + vocal in one launch, bf16 sum as 1B:602
+                ops.attention_cross3(qc, kvt[:, :dim], kvt[:, dim:], ctx.text_len, kvi[:, :dim], kvi[:, dim:],
+                                     ctx.img_len, kvv[:, :dim], kvv[:, dim:], nper, G, n_fr, ws.att, B, Lc, H_,
+                                     tok_offset=rank * Lc)
+            else:
+                ops.attention(qc, kvt[:, :dim], kvt[:, dim:], ws.att, segs_txt, B, Lc, H_)
+                if kvi is not None:
+                    ops.attention(qc, kvi[:, :dim], kvi[:, dim:], ws.att, segs_img, B, Lc, H_, accumulate=True)
+                ops.attention(qc, kvv[:, :dim], kvv[:, dim:], ws.att, segs_voc, voc_n, voc_q, H_, accumulate=True)
             ops.linear(ws.att, L.w_co, L.b_co, ops.EPI_RES_F32, out=x, residual=x)
             # FFN (1B:687-691)
             ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 3], scale=em[:, 4], rows_per_batch=Lc)

@@ -69,3 +69,22 @@ def test_dit_full_dims_vs_oracle():
         ref = odit.forward(P, cfg, inp["x"], inp["t"], inp["context"], inp["seq_len"], inp["clip_fea"], inp["y"],
                            inp["vocal"], inp["n_frames"])
     assert rel(out, ref) < 2e-2 and cos(out, ref) > 0.9995, (rel(out, ref), cos(out, ref))
+
+
+def test_dit_fused_cross_attention_matches_unfused(monkeypatch):
+    """256 tokens per latent frame enables the one-launch text+image+vocal cross-attention; it must
+    agree with the three-launch path (both bf16, rel-L2 <= 1e-2)."""
+    from stableavatar_amd import synthetic as syn
+    m = make_model(DIT_SMALL)
+    B, Fw, H, W = 3, 2, 32, 32
+    lat = syn.seeded_normal((1, 16, Fw, H, W), 111)
+    inp = dict(x=torch.cat([lat] * 3), y=syn.seeded_normal((B, 20, Fw, H, W), 112),
+               context=[syn.seeded_normal((20, 64), 113)] * 2 + [syn.seeded_normal((25, 64), 114)],
+               clip_fea=syn.seeded_normal((1, 257, 1280), 115).expand(3, -1, -1).contiguous(),
+               vocal=torch.cat([torch.zeros(1, 15, 768), syn.seeded_normal((1, 15, 768), 116).repeat(2, 1, 1)]),
+               t=torch.full((3,), 500.0), seq_len=Fw * (H // 2) * (W // 2), n_frames=5)
+    monkeypatch.setenv("SA_CROSS3", "1")
+    fused = run(m, inp)
+    monkeypatch.setenv("SA_CROSS3", "0")
+    ref = run(m, inp)
+    assert rel(fused, ref) < 1e-2 and cos(fused, ref) > 0.9999, (rel(fused, ref), cos(fused, ref))

@@ -120,6 +120,37 @@ def test_attention_spike_rescale():
     assert rel(o, _ref_attn(q, k, v, D ** -0.5)) < 1e-2
 
 
+@pytest.mark.parametrize("tok_offset", [0, 256])
+def test_attention_cross3(tok_offset):
+    """fused text + image + per-frame vocal cross-attention (1B:556-603) vs fp32 torch with the
+    reference's bf16 sum (bf16(text) + bf16(img)) + bf16(vocal)"""
+    from stableavatar_amd import ops
+    B, H, D, tpf, F, nper, tl, il = 2, 2, 128, 256, 3, 17, 512, 257
+    Lq = F * tpf - tok_offset
+    q = torch.randn(B * Lq, H * D, device=dev).bfloat16()
+    kvt = torch.randn(B * tl, 2 * H * D, device=dev).bfloat16()
+    kvi = torch.randn(B * il, 2 * H * D, device=dev).bfloat16()
+    kvv = torch.randn(B * F * nper, 2 * H * D, device=dev).bfloat16()
+    o = torch.empty(B * Lq, H * D, device=dev, dtype=torch.bfloat16)
+    HD = H * D
+    ops.attention_cross3(q, kvt[:, :HD], kvt[:, HD:], tl, kvi[:, :HD], kvi[:, HD:], il, kvv[:, :HD], kvv[:, HD:],
+                         nper, tpf, F, o, B, Lq, H, tok_offset=tok_offset)
+    sc = D ** -0.5
+    for b in range(B):
+        for h in range(H):
+            sl, sv = slice(h * D, (h + 1) * D), slice(HD + h * D, HD + (h + 1) * D)
+            qq = q[b * Lq:(b + 1) * Lq, sl]
+            t = _ref_attn(qq, kvt[b * tl:(b + 1) * tl, sl], kvt[b * tl:(b + 1) * tl, sv], sc).bfloat16()
+            i = _ref_attn(qq, kvi[b * il:(b + 1) * il, sl], kvi[b * il:(b + 1) * il, sv], sc).bfloat16()
+            vo = torch.empty(Lq, D, device=dev)
+            for r0 in range(0, Lq, 64):
+                f = (tok_offset + r0) // tpf
+                kr = slice((b * F + f) * nper, (b * F + f + 1) * nper)
+                vo[r0:r0 + 64] = _ref_attn(qq[r0:r0 + 64], kvv[kr, sl], kvv[kr, sv], sc)
+            ref = (t + i) + vo.bfloat16()
+            assert rel(o[b * Lq:(b + 1) * Lq, sl], ref) < 1e-2, (b, h)
+
+
 def test_layernorm_modulate():
     from stableavatar_amd import ops
     M, C, B = 1000, 1536, 2
