@@ -474,16 +474,25 @@ __device__ __forceinline__ bf16x8 pslice(const f32x16& S, int s) {
 struct V3State {
   f32x16 O[4];
   float m_run, l_run;
+  f32x16 negm;  // -m broadcast (NEGM blocks only)
 };
 
-template <int BUF>
+// NEGM (cdna_hip_programming.md App. B "row constants as the initial accumulator"): Q is prescaled
+// by c = scale·log2(e) and the QK^T chain starts from -m (st.negm), so S' = c·S - m comes out of the
+// MFMA and p = exp2(S') needs no VALU subtract; the row max runs relative to m.
+template <int BUF, bool NEGM = false>
 __device__ __forceinline__ void attn_v3_block(V3State& st, const bf16x8* qf, const uint32_t* ka, const uint32_t* va,
                                               int kb, int kv_len, float c, int hi) {
   // S^T[key][query] = K · Q^T, K fragments two groups ahead
   u32x4 ka0[4], ka1[4], kb0[4], kb1[4];
   f32x16 S[2];
+  if constexpr (NEGM) {
+    S[0] = st.negm;
+    S[1] = st.negm;
+  } else {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) { S[0][r] = 0.f; S[1][r] = 0.f; }
+    for (int r = 0; r < 16; ++r) { S[0][r] = 0.f; S[1][r] = 0.f; }
+  }
   read_k4<BUF, 0, 0>(ka0, ka);
   read_k4<BUF, 0, 4>(ka1, ka);
   read_k4<BUF, 1, 0>(kb0, ka);
@@ -510,6 +519,42 @@ __device__ __forceinline__ void attn_v3_block(V3State& st, const bf16x8* qf, con
         if (key >= kv_len) S[t][r] = -INFINITY;
       }
   }
+  if constexpr (NEGM) {
+    float mx = S[0][0];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[t][r]);
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));  // max of c·S - m over the block
+    }
+    const bool first = kb == 0;
+    if (first || !__all(mx <= RESCALE_THR)) {  // wave-uniform; the first block sets m exactly
+      const float delta = first ? mx : fmaxf(mx, 0.f);
+      const float alpha = __builtin_amdgcn_exp2f(-delta);
+      st.l_run *= alpha;
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) st.O[db][r] *= alpha;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        st.negm[r] -= delta;
+        S[0][r] -= delta;
+        S[1][r] -= delta;
+      }
+    }
+    float ps0 = 0.f, ps1 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      S[0][r] = __builtin_amdgcn_exp2f(S[0][r]);
+      S[1][r] = __builtin_amdgcn_exp2f(S[1][r]);
+      ps0 += S[0][r];
+      ps1 += S[1][r];
+    }
+    st.l_run += ps0 + ps1;
+  } else {
   float mx = S[0][0];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -536,6 +581,7 @@ __device__ __forceinline__ void attn_v3_block(V3State& st, const bf16x8* qf, con
       ps += p;
     }
   st.l_run += ps;
+  }
 
   // O^T[d][query] += V^T · P^T, slice g = 2t + s
   wait_v<8>(v0);
@@ -550,6 +596,7 @@ __device__ __forceinline__ void attn_v3_block(V3State& st, const bf16x8* qf, con
   mfma_v8(st.O, v1, pslice(S[1], 1));
 }
 
+template <bool NEGM>
 __global__ __launch_bounds__(512) void attn_fwd_v3_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // XCD-aware order (T1): consecutive query blocks of one (segment, head) share an XCD, so its L2
@@ -570,24 +617,40 @@ __global__ __launch_bounds__(512) void attn_fwd_v3_kernel(AttnArgs a) {
   bf16x8 qf[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
+  if constexpr (NEGM) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[s][j] = f2bf(bf2f(qf[s][j]) * a.c);
+  }
 
   const bf16* kbase = a.k + h * D;
   const bf16* vbase = a.v + h * D;
   int srow[2], schunk[2];
+  const bf16 *kp[2], *vp[2];  // this lane's source of block 0; full blocks advance by a uniform step
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     srow[i] = (wave * 2 + i) * 4 + (lane >> 4);
     schunk[i] = (lane & 15) ^ gsw(srow[i]);
+    const long key = kv_row0 + min(srow[i], kv_len - 1);
+    kp[i] = kbase + key * a.ks + schunk[i] * 8;
+    vp[i] = vbase + key * a.vs + schunk[i] * 8;
   }
   auto stage = [&](int kb, int buf) {
     char* base = smem + buf * STAGE_BYTES;
+    const bool full = kb * KVB + KVB <= kv_len;  // wave-uniform
+    const long ko = (long)kb * KVB * a.ks, vo = (long)kb * KVB * a.vs;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const long key = kv_row0 + min(kb * KVB + srow[i], kv_len - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(kbase + key * a.ks + schunk[i] * 8),
-                                       LDS_PTR(base + (wave * 2 + i) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(vbase + key * a.vs + schunk[i] * 8),
-                                       LDS_PTR(base + TILE_BYTES + (wave * 2 + i) * 1024), 16, 0, 0);
+      const bf16 *ksrc = kp[i] + ko, *vsrc = vp[i] + vo;
+      if (!full) {
+        const long key = kv_row0 + min(kb * KVB + srow[i], kv_len - 1);
+        ksrc = kbase + key * a.ks + schunk[i] * 8;
+        vsrc = vbase + key * a.vs + schunk[i] * 8;
+      }
+      __builtin_amdgcn_global_load_lds((const void*)ksrc, LDS_PTR(base + (wave * 2 + i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)vsrc, LDS_PTR(base + TILE_BYTES + (wave * 2 + i) * 1024), 16,
+                                       0, 0);
     }
   };
 
@@ -614,8 +677,10 @@ __global__ __launch_bounds__(512) void attn_fwd_v3_kernel(AttnArgs a) {
   for (int db = 0; db < 4; ++db)
 #pragma unroll
     for (int r = 0; r < 16; ++r) st.O[db][r] = 0.f;
-  st.m_run = -INFINITY;
+  st.m_run = NEGM ? 0.f : -INFINITY;
   st.l_run = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) st.negm[r] = 0.f;
 
   const int nkb = (kv_len + KVB - 1) / KVB;
   stage(0, 0);
@@ -624,12 +689,12 @@ __global__ __launch_bounds__(512) void attn_fwd_v3_kernel(AttnArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (kb + 1 < nkb) stage(kb + 1, 1);
-    attn_v3_block<0>(st, qf, ka, va, kb, kv_len, a.c, hi);
+    attn_v3_block<0, NEGM>(st, qf, ka, va, kb, kv_len, a.c, hi);
     if (kb + 1 >= nkb) break;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (kb + 2 < nkb) stage(kb + 2, 0);
-    attn_v3_block<1>(st, qf, ka, va, kb + 1, kv_len, a.c, hi);
+    attn_v3_block<1, NEGM>(st, qf, ka, va, kb + 1, kv_len, a.c, hi);
   }
 
   const float lt = st.l_run + __shfl_xor(st.l_run, 32, 64);
@@ -1129,10 +1194,11 @@ extern "C" int sa_attn_small(const void* q, const void* k, const void* v, void* 
 int g_attn_variant = -1;  // 0 = v1 (2-deep ring), 1 = v2 (3-deep ring, pipelined QK^T, deferred rescale),
                           // 2 = v1 + static priority, half-swap max, deferred rescale,
                           // 3 = v1 structure with asm LDS reads + counted waits (v3),
-                          // 4 = v3 reads + two-group ping-pong (v4)
+                          // 4 = v3 reads + two-group ping-pong (v4), 5 = v3 with prescaled Q and -m as
+                          // the QK^T initial accumulator
 
 extern "C" int sa_attn_set_variant(int variant) {
-  if (variant < 0 || variant > 4) return SA_ERR_ARG;
+  if (variant < 0 || variant > 5) return SA_ERR_ARG;
   g_attn_variant = variant;
   return SA_OK;
 }
@@ -1154,7 +1220,9 @@ extern "C" int sa_attn_fwd(const void* q, const void* k, const void* v, void* o,
                               LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_v3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)attn_fwd_v3_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_v3_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
@@ -1170,7 +1238,9 @@ extern "C" int sa_attn_fwd(const void* q, const void* k, const void* v, void* o,
   else if (g_attn_variant == 2)
     hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
   else if (g_attn_variant == 3)
-    hipLaunchKernelGGL(attn_fwd_v3_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(attn_fwd_v3_kernel<false>, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+  else if (g_attn_variant == 5)
+    hipLaunchKernelGGL(attn_fwd_v3_kernel<true>, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
   else if (g_attn_variant == 4)
     hipLaunchKernelGGL(attn_fwd_v4_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
   else

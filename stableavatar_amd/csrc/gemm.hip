@@ -448,18 +448,61 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
   if (!g1) __builtin_amdgcn_s_barrier();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (DIRECT) {
+    // per quadrant: issue every residual / gate / bias load of its 8 fragments first, then combine and
+    // store (R may alias C element-for-element, so loads of a fragment must precede its store)
     const int qa[4] = {0, 0, 1, 1}, qb[4] = {0, 1, 1, 0};
+    constexpr bool RES = EPI == EPI_RES_F32;
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < 4; ++q) {
+      const int rb = m0 + qa[q] * 128 + qm * 64 + (lane & 15);
+      const int cb = n0 + qb[q] * 128 + qn * 32 + (lane >> 4) * 4;
+      f32x4 bv[2], rv[4][2], gv[4][2];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int c = cb + n * 16;
+        bv[n] = (g.bias && c + 4 <= g.N) ? *(const f32x4*)(g.bias + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
         for (int n = 0; n < 2; ++n) {
-          const int grow = m0 + qa[q] * 128 + qm * 64 + m * 16 + (lane & 15);
-          const int gcol = n0 + qb[q] * 128 + qn * 32 + n * 16 + (lane >> 4) * 4;
-          float v[4] = {acc[q][m][n][0], acc[q][m][n][1], acc[q][m][n][2], acc[q][m][n][3]};
-          if (grow < g.M && gcol < g.N) epi_row<EPI, 4>(g, v, bz, grow, gcol);
+          const int row = rb + m * 16, c = cb + n * 16;
+          const bool ok = row < g.M && c + 4 <= g.N;
+          rv[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+          gv[m][n] = (f32x4){1.f, 1.f, 1.f, 1.f};
+          if (RES && ok) {
+            rv[m][n] = *(const f32x4*)(g.R + bz * g.sR + (long)row * g.ldr + c);
+            if (g.gate) gv[m][n] = *(const f32x4*)(g.gate + (long)(row / g.rows_per_batch) * g.gate_bstride + c);
+          }
         }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          const int row = rb + m * 16, c = cb + n * 16;
+          if (row >= g.M || c >= g.N) continue;
+          if (c + 4 > g.N) {  // ragged right edge: element-wise path
+            float v[4] = {acc[q][m][n][0], acc[q][m][n][1], acc[q][m][n][2], acc[q][m][n][3]};
+            epi_row<EPI, 4>(g, v, bz, row, c);
+            continue;
+          }
+          f32x4 o;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float t = acc[q][m][n][i] + bv[n][i];
+            if constexpr (EPI == EPI_SILU_F32) t = silu(t);
+            if constexpr (EPI == EPI_GELU_BF16) t = gelu_tanh(t);
+            if constexpr (EPI == EPI_GELU_ERF_BF16) t = gelu_erf(t);
+            o[i] = RES ? rv[m][n][i] + t * gv[m][n][i] : t;
+          }
+          if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16) {
+            bf16* C = (bf16*)g.C + bz * g.sC + (long)row * g.ldc + c;
+            *(bf16x4*)C = (bf16x4){f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
+          } else {
+            *(f32x4*)((float*)g.C + bz * g.sC + (long)row * g.ldc + c) = o;
+          }
+        }
+    }
     return;
   }
   __syncthreads();
@@ -705,7 +748,7 @@ int launch(const GemmArgs& g, int batch, hipStream_t st) {
   static int attr = 0;
   if (g_gemm_variant < 0) {
     const char* e = getenv("SA_GEMM_VARIANT");
-    g_gemm_variant = e ? atoi(e) : 3;
+    g_gemm_variant = e ? atoi(e) : 4;
   }
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
@@ -725,8 +768,12 @@ int launch(const GemmArgs& g, int batch, hipStream_t st) {
     hipLaunchKernelGGL(gemm_phased_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
   else if (g_gemm_variant == 2)
     hipLaunchKernelGGL(gemm_w4_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(256), W4_LDS, st, g);
-  else if (g_gemm_variant == 3)
-    hipLaunchKernelGGL((gemm_pp_kernel<EPI, false>), dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
+  else if (g_gemm_variant == 3) {
+    // fp32 outputs store straight from the (operand-swapped) accumulators; bf16 outputs go through
+    // the LDS transpose for 16-B row stores
+    constexpr bool F32_OUT = EPI == EPI_RES_F32 || EPI == EPI_F32 || EPI == EPI_SILU_F32;
+    hipLaunchKernelGGL((gemm_pp_kernel<EPI, F32_OUT>), dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
+  }
   else
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, true>), dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
   SA_LAUNCH_CHECK();

@@ -65,14 +65,14 @@ def main(which=("gemm", "attn")):
             res.append(r)
             print(json.dumps(r), flush=True)
             del x, w, out
-        call("sa_gemm_set_variant", 3)
+        call("sa_gemm_set_variant", 4)
     if "attnvar" in which:
         L, H, D = 21504, 12, 128
         qkv = torch.randn(3 * L, 3 * H * D, device=dev).bfloat16()
         segs = torch.tensor([[b * L, L, b * L, L] for b in range(3)], dtype=torch.int32, device=dev)
         q, k, v_ = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
         outs = {}
-        variants = (0, 3)
+        variants = (0, 3, 5)
         times = {v: [] for v in variants}
         for rnd in range(3):
             for v in variants:
