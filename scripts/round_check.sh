@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU check used between edits: tests (failures reported, not fatal), kernel A/B, bench, rocprof.
+# GPU check used between edits: tests (failures reported, not fatal), bench, rocprof, extra kbench.
 # Stops at the first GPU fault / abort / timeout (gpustep exit 99).
 set -u
 mkdir -p gpurun_out
@@ -11,3 +11,5 @@ scripts/gpustep.sh 300 gpurun_out/bench_$tag.log python bench.py; rc=$?; echo "b
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$tag -o run -- python bench.py > gpurun_out/prof_$tag.log 2>&1
 echo "prof rc=$?"
+[ -n "${2:-}" ] && scripts/gpustep.sh 300 gpurun_out/kbx_$tag.log python -m stableavatar_amd.kbench $2
+echo done

@@ -1213,7 +1213,7 @@ extern "C" int sa_attn_fwd(const void* q, const void* k, const void* v, void* o,
   static bool attr = false;
   if (g_attn_variant < 0) {
     const char* e = getenv("SA_ATTN_VARIANT");
-    g_attn_variant = e ? atoi(e) : 3;
+    g_attn_variant = e ? atoi(e) : 5;
   }
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -130,6 +130,18 @@ def main(which=("gemm", "attn")):
         res.append({"kernel": "attn_self", "L": L, "ms": round(ms, 3), "tflops": round(fl / ms / 1e9, 1),
                     "torch_sdpa_ms": round(ms_ref, 3), "torch_tflops": round(fl / ms_ref / 1e9, 1)})
         print(json.dumps(res[-1]), flush=True)
+    if "gemmsq" in which:  # square shapes of the guide's GEMM template figures (random [-1, 1) operands)
+        for n in (4096, 8192):
+            x = (torch.rand(n, n, device=dev) * 2 - 1).bfloat16()
+            w = (torch.rand(n, n, device=dev) * 2 - 1).bfloat16()
+            out = torch.empty(n, n, device=dev, dtype=torch.bfloat16)
+            ms = _time(lambda: ops.linear(x, w, None, ops.EPI_BF16, out=out), iters=10, warmup=3)
+            ms_ref = _time(lambda: torch.nn.functional.linear(x, w), iters=10, warmup=3)
+            fl = 2.0 * n ** 3
+            res.append({"kernel": f"gemm_sq{n}", "ms": round(ms, 4), "tflops": round(fl / ms / 1e9, 1),
+                        "torch_tflops": round(fl / ms_ref / 1e9, 1)})
+            print(json.dumps(res[-1]), flush=True)
+            del x, w, out
     if "attn1" in which:  # 3 bare self-attention launches (PMC passes: FETCH_SIZE / WRITE_SIZE)
         L, H, D = 21504, 12, 128
         qkv = torch.randn(3 * L, 3 * H * D, device=dev).bfloat16()
