@@ -43,6 +43,8 @@ int sa_gemm_bf16(const void* A, int64_t lda, int64_t strideA, const void* W, int
  * XCD order (default), 4 = 3 + two-group ping-pong. */
 int sa_gemm_set_variant(int variant);
 int sa_attn_set_variant(int variant);
+/* GEMM tile raster: runs of group_m tile rows walked column-major (0 = env SA_GEMM_GROUP_M / default). */
+int sa_gemm_set_group_m(int group_m);
 
 /* attention(q,k,v,...) of wan/models/wan_fantasy_transformer3d_1B.py:158-207 (SDPA path, no mask,
  * q_lens/k_lens ignored) for head_dim 128.  Rows of q/k/v/o are flat [rows, stride] bf16 matrices,

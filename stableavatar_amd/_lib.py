@@ -17,6 +17,7 @@ HEADER = PKG.parent / "include" / "stableavatar_hip.h"
 SIGNATURES = {
     "sa_gemm_bf16": "pllpllpplliiiiipllplip",
     "sa_gemm_set_variant": "i",
+    "sa_gemm_set_group_m": "i",
     "sa_attn_set_variant": "i",
     "sa_attn_fwd": "pppppiiiillllfip",
     "sa_layernorm_mod": "pliplipppplpiiifp",

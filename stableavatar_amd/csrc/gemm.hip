@@ -29,7 +29,20 @@ struct GemmArgs {
   const float* gate; long gate_bstride;  // gate[(m / rows_per_batch) * gate_bstride + n]
   int rows_per_batch;
   int M, N, K;
+  int group_m;  // tile raster: runs of group_m tile rows, column-major inside a run (L2 reuse per XCD)
 };
+
+// flat tile id -> (tile row, tile col): consecutive ids walk down a column of group_m tile rows, then
+// the next column, so the 32 tiles one XCD holds at a time (xcd_remap gives it a contiguous id range)
+// form a group_m x (32 / group_m) block that shares A rows and W rows in that XCD's L2
+__device__ __forceinline__ void tile_coords(int wg, int nm, int nn, int gm, int& mt, int& nt) {
+  const int per = gm * nn;
+  const int first = (wg / per) * gm;
+  const int gsz = min(nm - first, gm);
+  const int r = wg % per;
+  mt = first + r % gsz;
+  nt = r / gsz;
+}
 
 constexpr int BM = 256, BN = 256, BK = 64;
 constexpr int HALF_BYTES = 128 * BK * 2;        // 16 KB
@@ -118,7 +131,8 @@ __global__ __launch_bounds__(512) void gemm_phased_kernel(GemmArgs g) {
   const int qm = wave >> 2, qn = wave & 3;  // this wave's 64x32 sub-tile inside each 128x128 quadrant
   const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
   const int wg = xcd_remap(blockIdx.x, nm * nn);
-  const int mt = wg / nn, nt = wg % nn;
+  int mt, nt;
+  tile_coords(wg, nm, nn, g.group_m, mt, nt);
   const int m0 = mt * BM, n0 = nt * BN;
   const long bz = blockIdx.z;
   const bf16* A = g.A + bz * g.sA;
@@ -292,7 +306,8 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
   const bool g1 = qm == 1;
   const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
   const int wg = xcd_remap(blockIdx.x, nm * nn);
-  const int mt = wg / nn, nt = wg % nn;
+  int mt, nt;
+  tile_coords(wg, nm, nn, g.group_m, mt, nt);
   const int m0 = mt * BM, n0 = nt * BN;
   const long bz = blockIdx.z;
   const bf16* A = g.A + bz * g.sA;
@@ -551,7 +566,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs g) {
   const int wm = wave >> 1, wn = wave & 1;
   const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
   const int wg = xcd_remap(blockIdx.x, nm * nn);
-  const int mt = wg / nn, nt = wg % nn;
+  int mt, nt;
+  tile_coords(wg, nm, nn, g.group_m, mt, nt);
   const int m0 = mt * BM, n0 = nt * BN;
   const long bz = blockIdx.z;
   const bf16* A = g.A + bz * g.sA;
@@ -665,7 +681,8 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(GemmArgs g) {
   const int wm = wave >> 2, wn = wave & 3;
   const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
   const int wg = xcd_remap(blockIdx.x, nm * nn);
-  const int mt = wg / nn, nt = wg % nn;
+  int mt, nt;
+  tile_coords(wg, nm, nn, g.group_m, mt, nt);
   const int m0 = mt * BM, n0 = nt * BN;
   const long bz = blockIdx.z;
   const bf16* A = g.A + bz * g.sA;
@@ -740,8 +757,702 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(GemmArgs g) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// s4 kernel: one wave per SIMD (4 waves, 2x2, 128x128 per wave, 256 accumulators in AGPRs), the
+// structure hipBLASLt's MT256x256x64 kernel has on gfx950 (rocprof: 256 threads, 130 KB LDS), with
+// our own schedule.  K is staged in 32-deep sub-tiles (A 256x32 + B 256x32 = 32 KB) through a 4-slot
+// LDS ring by buffer_load ... lds (per-lane voffset fixed, the K step in soffset: no address VALU).
+// Step s: vmcnt(8) (sub-tile s+1 landed; s+2 still flying) + one barrier, then the 64 MFMAs of
+// sub-tile s from registers, with the 16 ds_read_b128 of sub-tile s+1's fragments placed two per
+// four MFMAs in the first half and the 8 DMA pieces of sub-tile s+3 (into the slot of s-1) one per
+// four MFMAs in the second half.  Past the end of K the DMA re-reads the last sub-tile and the
+// fragment reads hit a dead slot, so every step issues the same 8 pieces and vmcnt(8) is exact.
+// MFMAs and LDS reads are inline asm (cdna_hip_programming.md §5.7): hipcc keeps them in program
+// order, the accumulators stay in AGPRs ("+a"), and the fragment waits are explicit.  Operands are
+// swapped in the MFMA (C^T = W·A^T) so each lane holds 4 consecutive output columns of one row.
+constexpr int S4_SLOT = 2 * 256 * 64;  // A + B sub-tile, 64-B rows (32 KB)
+constexpr int S4_LDS = 4 * S4_SLOT;    // 128 KB
+
+template <int OFF>
+__device__ __forceinline__ void s4_ds(u32x4& d, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF));
+}
+__device__ __forceinline__ void s4_mma(f32x4& c, const u32x4& w, const u32x4& x) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(w), "v"(x) : "memory");
+}
+__device__ __forceinline__ void s4_wait_frags(u32x4 (&a)[8], u32x4 (&b)[8]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]));
+  asm volatile("" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]), "+v"(b[6]), "+v"(b[7]));
+}
+
+struct S4Ctx {
+  __amdgpu_buffer_rsrc_t ra, rw;
+  int aoff[4], woff[4];
+  uint32_t lds_dma;           // wave-uniform LDS byte address of this wave's piece 0 in slot 0
+  uint32_t ard[2], wrd[2];    // per-lane fragment read bases (slots 0-1, slots 2-3)
+};
+
+// DMA of sub-tile s (clamped to the last one) into slot SLOT; PIECE selects one of the 8 pieces
+template <int SLOT, int PIECE>
+__device__ __forceinline__ void s4_dma(const S4Ctx& c, int ks) {
+  constexpr int i = PIECE & 3;
+  if constexpr (PIECE < 4)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(c.ra, LDS_PTR((uintptr_t)(c.lds_dma + SLOT * S4_SLOT + i * 4096)), 16,
+                                             c.aoff[i], ks, 0, 0);
+  else
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rw, LDS_PTR((uintptr_t)(c.lds_dma + SLOT * S4_SLOT + 256 * 64 + i * 4096)),
+                                             16, c.woff[i], ks, 0, 0);
+}
+
+// fragment read R (0..15: A frags 0-7, then W frags 0-7) of slot SLOT
+template <int SLOT, int R>
+__device__ __forceinline__ void s4_read(const S4Ctx& c, u32x4 (&a)[8], u32x4 (&b)[8]) {
+  constexpr int off = (SLOT & 1) * S4_SLOT + (R & 7) * 1024;
+  if constexpr (R < 8)
+    s4_ds<off>(a[R], c.ard[SLOT >> 1]);
+  else
+    s4_ds<off>(b[R & 7], c.wrd[SLOT >> 1]);
+}
+
+template <int SLOT, int Q, int ABL>
+__device__ __forceinline__ void s4_quarter(const S4Ctx& c, f32x4 (&acc)[8][8], u32x4 (&ac)[8], u32x4 (&bc)[8],
+                                           u32x4 (&an)[8], u32x4 (&bn)[8], int ks3) {
+  // Q = 0..7: MFMA row i = Q; reads of the next fragments in Q 0-3, DMA pieces in Q 4-7
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s4_mma(acc[Q][j], bc[j], ac[Q]);
+  if constexpr (Q < 4) {
+    if constexpr (!(ABL & 2)) {
+      s4_read<(SLOT + 1) & 3, 4 * Q + 0>(c, an, bn);
+      s4_read<(SLOT + 1) & 3, 4 * Q + 1>(c, an, bn);
+    }
+  } else {
+    if constexpr (!(ABL & 1)) s4_dma<(SLOT + 3) & 3, 2 * (Q - 4)>(c, ks3);
+  }
+#pragma unroll
+  for (int j = 4; j < 8; ++j) s4_mma(acc[Q][j], bc[j], ac[Q]);
+  if constexpr (Q < 4) {
+    if constexpr (!(ABL & 2)) {
+      s4_read<(SLOT + 1) & 3, 4 * Q + 2>(c, an, bn);
+      s4_read<(SLOT + 1) & 3, 4 * Q + 3>(c, an, bn);
+    }
+  } else {
+    if constexpr (!(ABL & 1)) s4_dma<(SLOT + 3) & 3, 2 * (Q - 4) + 1>(c, ks3);
+  }
+}
+
+template <int SLOT, int ABL>
+__device__ __forceinline__ void s4_step(const S4Ctx& c, f32x4 (&acc)[8][8], u32x4 (&ac)[8], u32x4 (&bc)[8],
+                                        u32x4 (&an)[8], u32x4 (&bn)[8], int s, int ns) {
+  if constexpr (ABL & 1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  s4_wait_frags(ac, bc);
+  const int ks3 = min(s + 3, ns - 1) * 64;
+  s4_quarter<SLOT, 0, ABL>(c, acc, ac, bc, an, bn, ks3);
+  s4_quarter<SLOT, 1, ABL>(c, acc, ac, bc, an, bn, ks3);
+  s4_quarter<SLOT, 2, ABL>(c, acc, ac, bc, an, bn, ks3);
+  s4_quarter<SLOT, 3, ABL>(c, acc, ac, bc, an, bn, ks3);
+  s4_quarter<SLOT, 4, ABL>(c, acc, ac, bc, an, bn, ks3);
+  s4_quarter<SLOT, 5, ABL>(c, acc, ac, bc, an, bn, ks3);
+  s4_quarter<SLOT, 6, ABL>(c, acc, ac, bc, an, bn, ks3);
+  s4_quarter<SLOT, 7, ABL>(c, acc, ac, bc, an, bn, ks3);
+}
+
+// ABL (measurement builds only): 1 = no DMA in the loop, 2 = no fragment reads in the loop (results
+// are wrong; the schedule's cost anatomy is what is measured)
+template <int EPI, int ABL = 0>
+__global__ __launch_bounds__(256, 1) void gemm_s4_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
+  const int wg = xcd_remap(blockIdx.x, nm * nn);
+  int mt, nt;
+  tile_coords(wg, nm, nn, g.group_m, mt, nt);
+  const int m0 = mt * BM, n0 = nt * BN;
+  const long bz = blockIdx.z;
+  S4Ctx c;
+  c.ra = __builtin_amdgcn_make_buffer_rsrc((void*)(g.A + bz * g.sA + (long)m0 * g.lda), (short)0, 0x7fffffff, 0x00020000);
+  c.rw = __builtin_amdgcn_make_buffer_rsrc((void*)(g.W + bz * g.sW + (long)n0 * g.ldw), (short)0, 0x7fffffff, 0x00020000);
+  // DMA piece i (0..3) of each operand: rows (i*4+wave)*16 + lane/4, 16-B chunk lane%4 (source-swizzled)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (i * 4 + wave) * 16 + (lane >> 2);
+    const int chunk = (lane & 3) ^ ((row >> 1) & 3);
+    c.aoff[i] = (min(m0 + row, g.M - 1) - m0) * (int)g.lda * 2 + chunk * 16;
+    c.woff[i] = (min(n0 + row, g.N - 1) - n0) * (int)g.ldw * 2 + chunk * 16;
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
+  c.lds_dma = __builtin_amdgcn_readfirstlane(lds0 + wave * 1024);
+  // fragment reads: row r = w*128 + i*16 + lane%16, chunk lane/16 -> the swizzle term is independent of i
+  const int fr = lane & 15, fc = lane >> 4;
+  c.ard[0] = lds0 + (wm * 128 + fr) * 64 + ((fc ^ ((fr >> 1) & 3)) << 4);
+  c.wrd[0] = lds0 + 256 * 64 + (wn * 128 + fr) * 64 + ((fc ^ ((fr >> 1) & 3)) << 4);
+  c.ard[1] = c.ard[0] + 2 * S4_SLOT;
+  c.wrd[1] = c.wrd[0] + 2 * S4_SLOT;
+  const int ns = g.K / 32;  // multiple of 4 (launcher: K % 128 == 0); a mid-loop exit makes hipcc spill
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  u32x4 a0[8], b0[8], a1[8], b1[8];
+#define SA_S4_DMA_ALL(SLOT, S)                                                                   \
+  {                                                                                              \
+    const int ks = min((S), ns - 1) * 64;                                                        \
+    s4_dma<SLOT, 0>(c, ks); s4_dma<SLOT, 1>(c, ks); s4_dma<SLOT, 2>(c, ks); s4_dma<SLOT, 3>(c, ks); \
+    s4_dma<SLOT, 4>(c, ks); s4_dma<SLOT, 5>(c, ks); s4_dma<SLOT, 6>(c, ks); s4_dma<SLOT, 7>(c, ks); \
+  }
+  SA_S4_DMA_ALL(0, 0)
+  SA_S4_DMA_ALL(1, 1)
+  SA_S4_DMA_ALL(2, 2)
+#undef SA_S4_DMA_ALL
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  s4_read<0, 0>(c, a0, b0); s4_read<0, 1>(c, a0, b0); s4_read<0, 2>(c, a0, b0); s4_read<0, 3>(c, a0, b0);
+  s4_read<0, 4>(c, a0, b0); s4_read<0, 5>(c, a0, b0); s4_read<0, 6>(c, a0, b0); s4_read<0, 7>(c, a0, b0);
+  s4_read<0, 8>(c, a0, b0); s4_read<0, 9>(c, a0, b0); s4_read<0, 10>(c, a0, b0); s4_read<0, 11>(c, a0, b0);
+  s4_read<0, 12>(c, a0, b0); s4_read<0, 13>(c, a0, b0); s4_read<0, 14>(c, a0, b0); s4_read<0, 15>(c, a0, b0);
+
+  for (int s = 0; s < ns; s += 4) {
+    s4_step<0, ABL>(c, acc, a0, b0, a1, b1, s, ns);
+    s4_step<1, ABL>(c, acc, a1, b1, a0, b0, s + 1, ns);
+    s4_step<2, ABL>(c, acc, a0, b0, a1, b1, s + 2, ns);
+    s4_step<3, ABL>(c, acc, a1, b1, a0, b0, s + 3, ns);
+  }
+  // drain: DMA, the (dead) last fragment reads, and the MFMA -> v_accvgpr_read hazard
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  // epilogue: per 16-row block a [16][128] fp32 strip per wave (b128 writes of the 4-column lane
+  // vectors), read back 16 consecutive columns per lane for the fused epilogue and 16-B stores
+  float* strip = (float*)(smem + wave * (16 * 132 * 4));
+  const int er = lane >> 2, ec = (lane & 3) * 32;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) *(f32x4*)(strip + fr * 132 + j * 16 + fc * 4) = acc[i][j];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const int grow = m0 + wm * 128 + i * 16 + er;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 t = *(const f32x4*)(strip + er * 132 + ec + h * 16 + q * 4);
+        v[4 * q] = t[0]; v[4 * q + 1] = t[1]; v[4 * q + 2] = t[2]; v[4 * q + 3] = t[3];
+      }
+      const int gcol = n0 + wn * 128 + ec + h * 16;
+      if (grow < g.M && gcol < g.N) epi_row<EPI, 16>(g, v, bz, grow, gcol);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// epilogue shared by the one-wave-per-SIMD kernels: per 16-row block a [16][128] fp32 strip per wave
+// (b128 writes of the operand-swapped 4-column lane vectors), read back 16 consecutive columns per
+// lane for the fused epilogue and 16-B stores.  LDS must be free (caller drains DMA + barrier).
+template <int EPI>
+__device__ __forceinline__ void s4_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8], char* smem, int wave, int lane,
+                                            int m0, int n0, long bz) {
+  const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fc = lane >> 4;
+  float* strip = (float*)(smem + wave * (16 * 132 * 4));
+  const int er = lane >> 2, ec = (lane & 3) * 32;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) *(f32x4*)(strip + fr * 132 + j * 16 + fc * 4) = acc[i][j];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const int grow = m0 + wm * 128 + i * 16 + er;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 t = *(const f32x4*)(strip + er * 132 + ec + h * 16 + q * 4);
+        v[4 * q] = t[0]; v[4 * q + 1] = t[1]; v[4 * q + 2] = t[2]; v[4 * q + 3] = t[3];
+      }
+      const int gcol = n0 + wn * 128 + ec + h * 16;
+      if (grow < g.M && gcol < g.N) epi_row<EPI, 16>(g, v, bz, grow, gcol);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// s5 kernel: s4's one-wave-per-SIMD 128x128 wave tiles, but K-tiles of 64 (128-B rows, so every
+// 1-KB DMA piece is 8 whole cache lines; the 64-B rows of s4 halve the line per request and the
+// DMA issue then throttles the wave) in a 2-stage ring (64 KB per stage: A 256 rows, W 256 rows).
+// Step t (stage t&1), fragments of (t, k 0-31) already in registers:
+//   half 0: 64 MFMAs, with the 16 reads of (t, k 32-63) in its first 32
+//   mid:    vmcnt(0) (tile t+1 landed) + lgkmcnt(0) + one barrier: t+1 visible, stage t&1 free
+//   half 1: 64 MFMAs, with the 16 reads of (t+1, k 0-31) and the 16 DMA pieces of tile t+2 (into
+//           stage t&1) in its first 32
+// so a DMA piece has from half 1 of step t to the middle of step t+1 to land.
+constexpr int S5_STAGE = 2 * 256 * 128;  // 64 KB
+constexpr int S5_LDS = 2 * S5_STAGE;     // 128 KB
+
+struct S5Ctx {
+  __amdgpu_buffer_rsrc_t ra, rw;
+  int aoff[8], woff[8];
+  uint32_t lds_dma;          // wave-uniform LDS address of piece 0 (stage 0)
+  uint32_t ard[2][2], wrd[2][2];  // [stage][k half] per-lane fragment read bases
+};
+
+template <int STAGE, int PIECE>
+__device__ __forceinline__ void s5_dma(const S5Ctx& c, int ks) {
+  constexpr int i = PIECE & 7;
+  if constexpr (PIECE < 8)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(c.ra, LDS_PTR((uintptr_t)(c.lds_dma + STAGE * S5_STAGE + i * 4096)), 16,
+                                             c.aoff[i], ks, 0, 0);
+  else
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        c.rw, LDS_PTR((uintptr_t)(c.lds_dma + STAGE * S5_STAGE + 256 * 128 + i * 4096)), 16, c.woff[i], ks, 0, 0);
+}
+
+template <int STAGE, int KH, int R>
+__device__ __forceinline__ void s5_read(const S5Ctx& c, u32x4 (&a)[8], u32x4 (&b)[8]) {
+  if constexpr (R < 8)
+    s4_ds<(R & 7) * 2048>(a[R], c.ard[STAGE][KH]);
+  else
+    s4_ds<(R & 7) * 2048>(b[R & 7], c.wrd[STAGE][KH]);
+}
+
+// one 64-MFMA half: MFMA row Q uses (ac[Q], bc[0..7]); the first 4 rows carry the reads of the
+// next fragments (stage RS, k half RK) and, when DMA, 4 DMA pieces each of tile ks into stage DS
+template <int RS, int RK, bool DMA, int DS>
+__device__ __forceinline__ void s5_half(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&ac)[8], u32x4 (&bc)[8],
+                                        u32x4 (&an)[8], u32x4 (&bn)[8], int ks) {
+#define SA_S5_ROW(Q)                                                                        \
+  {                                                                                         \
+    s4_mma(acc[Q][0], bc[0], ac[Q]); s4_mma(acc[Q][1], bc[1], ac[Q]);                       \
+    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q>(c, an, bn); }                             \
+    if constexpr (DMA && Q < 4) { s5_dma<DS, 4 * Q>(c, ks); }                               \
+    s4_mma(acc[Q][2], bc[2], ac[Q]); s4_mma(acc[Q][3], bc[3], ac[Q]);                       \
+    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 1>(c, an, bn); }                         \
+    if constexpr (DMA && Q < 4) { s5_dma<DS, 4 * Q + 1>(c, ks); }                           \
+    s4_mma(acc[Q][4], bc[4], ac[Q]); s4_mma(acc[Q][5], bc[5], ac[Q]);                       \
+    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 2>(c, an, bn); }                         \
+    if constexpr (DMA && Q < 4) { s5_dma<DS, 4 * Q + 2>(c, ks); }                           \
+    s4_mma(acc[Q][6], bc[6], ac[Q]); s4_mma(acc[Q][7], bc[7], ac[Q]);                       \
+    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 3>(c, an, bn); }                         \
+    if constexpr (DMA && Q < 4) { s5_dma<DS, 4 * Q + 3>(c, ks); }                           \
+  }
+  SA_S5_ROW(0) SA_S5_ROW(1) SA_S5_ROW(2) SA_S5_ROW(3) SA_S5_ROW(4) SA_S5_ROW(5) SA_S5_ROW(6) SA_S5_ROW(7)
+#undef SA_S5_ROW
+}
+
+template <int S>
+__device__ __forceinline__ void s5_step(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8], u32x4 (&b0)[8],
+                                        u32x4 (&a1)[8], u32x4 (&b1)[8], int t, int nk) {
+  s4_wait_frags(a0, b0);
+  s5_half<S, 1, false, 0>(c, acc, a0, b0, a1, b1, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  s4_wait_frags(a1, b1);
+  __builtin_amdgcn_s_barrier();
+  s5_half<S ^ 1, 0, true, S>(c, acc, a1, b1, a0, b0, min(t + 2, nk - 1) * 128);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_s5_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
+  const int wg = xcd_remap(blockIdx.x, nm * nn);
+  int mt, nt;
+  tile_coords(wg, nm, nn, g.group_m, mt, nt);
+  const int m0 = mt * BM, n0 = nt * BN;
+  const long bz = blockIdx.z;
+  S5Ctx c;
+  c.ra = __builtin_amdgcn_make_buffer_rsrc((void*)(g.A + bz * g.sA + (long)m0 * g.lda), (short)0, 0x7fffffff, 0x00020000);
+  c.rw = __builtin_amdgcn_make_buffer_rsrc((void*)(g.W + bz * g.sW + (long)n0 * g.ldw), (short)0, 0x7fffffff, 0x00020000);
+  // DMA piece i (0..7) of each operand: rows (i*4+wave)*8 + lane/8, 16-B chunk lane%8 (source-swizzled)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = (i * 4 + wave) * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    c.aoff[i] = (min(m0 + row, g.M - 1) - m0) * (int)g.lda * 2 + chunk * 16;
+    c.woff[i] = (min(n0 + row, g.N - 1) - n0) * (int)g.ldw * 2 + chunk * 16;
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
+  c.lds_dma = __builtin_amdgcn_readfirstlane(lds0 + wave * 1024);
+  // fragment (row r = w*128 + i*16 + lane%16, chunk 4*kh + lane/16): the swizzle term is independent of i
+  const int fr = lane & 15, fc = lane >> 4;
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      const int sw = ((4 * kh + fc) ^ ((fr >> 1) & 7)) << 4;
+      c.ard[st][kh] = lds0 + st * S5_STAGE + (wm * 128 + fr) * 128 + sw;
+      c.wrd[st][kh] = lds0 + st * S5_STAGE + 256 * 128 + (wn * 128 + fr) * 128 + sw;
+    }
+  const int nk = g.K / 64;  // even (launcher: K % 128 == 0); a mid-loop exit makes hipcc spill
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  u32x4 a0[8], b0[8], a1[8], b1[8];
+#define SA_S5_DMA_ALL(STAGE, T)                                                                       \
+  {                                                                                                   \
+    const int ks = (T) * 128;                                                                         \
+    s5_dma<STAGE, 0>(c, ks); s5_dma<STAGE, 1>(c, ks); s5_dma<STAGE, 2>(c, ks); s5_dma<STAGE, 3>(c, ks);     \
+    s5_dma<STAGE, 4>(c, ks); s5_dma<STAGE, 5>(c, ks); s5_dma<STAGE, 6>(c, ks); s5_dma<STAGE, 7>(c, ks);     \
+    s5_dma<STAGE, 8>(c, ks); s5_dma<STAGE, 9>(c, ks); s5_dma<STAGE, 10>(c, ks); s5_dma<STAGE, 11>(c, ks);   \
+    s5_dma<STAGE, 12>(c, ks); s5_dma<STAGE, 13>(c, ks); s5_dma<STAGE, 14>(c, ks); s5_dma<STAGE, 15>(c, ks); \
+  }
+  SA_S5_DMA_ALL(0, 0)
+  SA_S5_DMA_ALL(1, 1)
+#undef SA_S5_DMA_ALL
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  s5_read<0, 0, 0>(c, a0, b0); s5_read<0, 0, 1>(c, a0, b0); s5_read<0, 0, 2>(c, a0, b0); s5_read<0, 0, 3>(c, a0, b0);
+  s5_read<0, 0, 4>(c, a0, b0); s5_read<0, 0, 5>(c, a0, b0); s5_read<0, 0, 6>(c, a0, b0); s5_read<0, 0, 7>(c, a0, b0);
+  s5_read<0, 0, 8>(c, a0, b0); s5_read<0, 0, 9>(c, a0, b0); s5_read<0, 0, 10>(c, a0, b0); s5_read<0, 0, 11>(c, a0, b0);
+  s5_read<0, 0, 12>(c, a0, b0); s5_read<0, 0, 13>(c, a0, b0); s5_read<0, 0, 14>(c, a0, b0); s5_read<0, 0, 15>(c, a0, b0);
+
+  for (int t = 0; t < nk; t += 2) {
+    s5_step<0>(c, acc, a0, b0, a1, b1, t, nk);
+    s5_step<1>(c, acc, a0, b0, a1, b1, t + 1, nk);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  s4_epilogue<EPI>(g, acc, smem, wave, lane, m0, n0, bz);
+}
+
+// ------------------------------------------------------------------------------------------------
+// s6 kernel: s5 with register staging instead of LDS-DMA (measured: the LDS-DMA path caps the
+// one-wave-per-SIMD loop well below the MFMA rate, s5 972 TF vs 1709 TF with the DMA removed, at
+// 8192^3).  Tile t+2 is fetched by 16 buffer_load_dwordx4 per wave into 64 staging VGPRs in the
+// first half of step t and written (ds_write_b128, same swizzled image as the DMA) into stage t&1
+// in the second half, after the mid barrier has freed it; hipcc counts these loads itself.
+template <int STAGE, int P>
+__device__ __forceinline__ void s6_load(const S5Ctx& c, u32x4 (&stg)[16], int ks) {
+  constexpr int i = P & 7;
+  if constexpr (P < 8)
+    stg[P] = __builtin_amdgcn_raw_buffer_load_b128(c.ra, c.aoff[i], ks, 0);
+  else
+    stg[P] = __builtin_amdgcn_raw_buffer_load_b128(c.rw, c.woff[i], ks, 0);
+}
+template <int STAGE, int P>
+__device__ __forceinline__ void s6_store(char* lds_lane, const u32x4 (&stg)[16]) {
+  // lds_lane = smem + wave*1024 + lane*16; piece P of operand (P>>3) at +(P&7)*4096
+  constexpr int off = STAGE * S5_STAGE + (P >> 3) * 256 * 128 + (P & 7) * 4096;
+  *(u32x4*)(lds_lane + off) = stg[P];
+}
+
+template <int RS, int RK, int MODE, int DS>
+__device__ __forceinline__ void s6_half(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&ac)[8], u32x4 (&bc)[8],
+                                        u32x4 (&an)[8], u32x4 (&bn)[8], u32x4 (&stg)[16], char* lds_lane, int ks) {
+  // MODE 0: reads of the next fragments in rows 0-3, global loads (tile ks) in rows 4-7
+  // MODE 1: reads in rows 0-3, staged ds_writes into stage DS in rows 4-7
+#define SA_S6_ROW(Q)                                                                          \
+  {                                                                                           \
+    s4_mma(acc[Q][0], bc[0], ac[Q]); s4_mma(acc[Q][1], bc[1], ac[Q]);                         \
+    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q>(c, an, bn); }                               \
+    else if constexpr (MODE == 0) { s6_load<DS, 4 * (Q - 4)>(c, stg, ks); }                   \
+    else { s6_store<DS, 4 * (Q - 4)>(lds_lane, stg); }                                        \
+    s4_mma(acc[Q][2], bc[2], ac[Q]); s4_mma(acc[Q][3], bc[3], ac[Q]);                         \
+    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 1>(c, an, bn); }                           \
+    else if constexpr (MODE == 0) { s6_load<DS, 4 * (Q - 4) + 1>(c, stg, ks); }               \
+    else { s6_store<DS, 4 * (Q - 4) + 1>(lds_lane, stg); }                                    \
+    s4_mma(acc[Q][4], bc[4], ac[Q]); s4_mma(acc[Q][5], bc[5], ac[Q]);                         \
+    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 2>(c, an, bn); }                           \
+    else if constexpr (MODE == 0) { s6_load<DS, 4 * (Q - 4) + 2>(c, stg, ks); }               \
+    else { s6_store<DS, 4 * (Q - 4) + 2>(lds_lane, stg); }                                    \
+    s4_mma(acc[Q][6], bc[6], ac[Q]); s4_mma(acc[Q][7], bc[7], ac[Q]);                         \
+    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 3>(c, an, bn); }                           \
+    else if constexpr (MODE == 0) { s6_load<DS, 4 * (Q - 4) + 3>(c, stg, ks); }               \
+    else { s6_store<DS, 4 * (Q - 4) + 3>(lds_lane, stg); }                                    \
+  }
+  SA_S6_ROW(0) SA_S6_ROW(1) SA_S6_ROW(2) SA_S6_ROW(3) SA_S6_ROW(4) SA_S6_ROW(5) SA_S6_ROW(6) SA_S6_ROW(7)
+#undef SA_S6_ROW
+}
+
+template <int S>
+__device__ __forceinline__ void s6_step(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8], u32x4 (&b0)[8],
+                                        u32x4 (&a1)[8], u32x4 (&b1)[8], u32x4 (&stg)[16], char* lds_lane, int t,
+                                        int nk) {
+  s4_wait_frags(a0, b0);
+  s6_half<S, 1, 0, S>(c, acc, a0, b0, a1, b1, stg, lds_lane, min(t + 2, nk - 1) * 128);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of stage S and its ds_writes
+  s4_wait_frags(a1, b1);
+  __builtin_amdgcn_s_barrier();
+  s6_half<S ^ 1, 0, 1, S>(c, acc, a1, b1, a0, b0, stg, lds_lane, 0);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_s6_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
+  const int wg = xcd_remap(blockIdx.x, nm * nn);
+  int mt, nt;
+  tile_coords(wg, nm, nn, g.group_m, mt, nt);
+  const int m0 = mt * BM, n0 = nt * BN;
+  const long bz = blockIdx.z;
+  S5Ctx c;
+  c.ra = __builtin_amdgcn_make_buffer_rsrc((void*)(g.A + bz * g.sA + (long)m0 * g.lda), (short)0, 0x7fffffff, 0x00020000);
+  c.rw = __builtin_amdgcn_make_buffer_rsrc((void*)(g.W + bz * g.sW + (long)n0 * g.ldw), (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = (i * 4 + wave) * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    c.aoff[i] = (min(m0 + row, g.M - 1) - m0) * (int)g.lda * 2 + chunk * 16;
+    c.woff[i] = (min(n0 + row, g.N - 1) - n0) * (int)g.ldw * 2 + chunk * 16;
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
+  char* lds_lane = smem + wave * 1024 + lane * 16;
+  const int fr = lane & 15, fc = lane >> 4;
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      const int sw = ((4 * kh + fc) ^ ((fr >> 1) & 7)) << 4;
+      c.ard[st][kh] = lds0 + st * S5_STAGE + (wm * 128 + fr) * 128 + sw;
+      c.wrd[st][kh] = lds0 + st * S5_STAGE + 256 * 128 + (wn * 128 + fr) * 128 + sw;
+    }
+  const int nk = g.K / 64;  // even (launcher: K % 128 == 0)
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  u32x4 a0[8], b0[8], a1[8], b1[8], stg[16];
+#define SA_S6_FILL(STAGE, T)                                                                              \
+  {                                                                                                       \
+    const int ks = (T) * 128;                                                                             \
+    s6_load<STAGE, 0>(c, stg, ks); s6_load<STAGE, 1>(c, stg, ks); s6_load<STAGE, 2>(c, stg, ks);          \
+    s6_load<STAGE, 3>(c, stg, ks); s6_load<STAGE, 4>(c, stg, ks); s6_load<STAGE, 5>(c, stg, ks);          \
+    s6_load<STAGE, 6>(c, stg, ks); s6_load<STAGE, 7>(c, stg, ks); s6_load<STAGE, 8>(c, stg, ks);          \
+    s6_load<STAGE, 9>(c, stg, ks); s6_load<STAGE, 10>(c, stg, ks); s6_load<STAGE, 11>(c, stg, ks);        \
+    s6_load<STAGE, 12>(c, stg, ks); s6_load<STAGE, 13>(c, stg, ks); s6_load<STAGE, 14>(c, stg, ks);       \
+    s6_load<STAGE, 15>(c, stg, ks);                                                                       \
+    s6_store<STAGE, 0>(lds_lane, stg); s6_store<STAGE, 1>(lds_lane, stg); s6_store<STAGE, 2>(lds_lane, stg);     \
+    s6_store<STAGE, 3>(lds_lane, stg); s6_store<STAGE, 4>(lds_lane, stg); s6_store<STAGE, 5>(lds_lane, stg);     \
+    s6_store<STAGE, 6>(lds_lane, stg); s6_store<STAGE, 7>(lds_lane, stg); s6_store<STAGE, 8>(lds_lane, stg);     \
+    s6_store<STAGE, 9>(lds_lane, stg); s6_store<STAGE, 10>(lds_lane, stg); s6_store<STAGE, 11>(lds_lane, stg);   \
+    s6_store<STAGE, 12>(lds_lane, stg); s6_store<STAGE, 13>(lds_lane, stg); s6_store<STAGE, 14>(lds_lane, stg);  \
+    s6_store<STAGE, 15>(lds_lane, stg);                                                                   \
+  }
+  SA_S6_FILL(0, 0)
+  SA_S6_FILL(1, 1)
+#undef SA_S6_FILL
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  s5_read<0, 0, 0>(c, a0, b0); s5_read<0, 0, 1>(c, a0, b0); s5_read<0, 0, 2>(c, a0, b0); s5_read<0, 0, 3>(c, a0, b0);
+  s5_read<0, 0, 4>(c, a0, b0); s5_read<0, 0, 5>(c, a0, b0); s5_read<0, 0, 6>(c, a0, b0); s5_read<0, 0, 7>(c, a0, b0);
+  s5_read<0, 0, 8>(c, a0, b0); s5_read<0, 0, 9>(c, a0, b0); s5_read<0, 0, 10>(c, a0, b0); s5_read<0, 0, 11>(c, a0, b0);
+  s5_read<0, 0, 12>(c, a0, b0); s5_read<0, 0, 13>(c, a0, b0); s5_read<0, 0, 14>(c, a0, b0); s5_read<0, 0, 15>(c, a0, b0);
+
+  for (int t = 0; t < nk; t += 2) {
+    s6_step<0>(c, acc, a0, b0, a1, b1, stg, lds_lane, t, nk);
+    s6_step<1>(c, acc, a0, b0, a1, b1, stg, lds_lane, t + 1, nk);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  s4_epilogue<EPI>(g, acc, smem, wave, lane, m0, n0, bz);
+}
+
+// ------------------------------------------------------------------------------------------------
+// s7 kernel: s6 made persistent.  One workgroup per CU walks output tiles u = blockIdx.x + k*gridDim.x
+// and the K pipeline runs on across tile seams: in the last two K steps of tile u the staged loads
+// fetch K-tiles 0 and 1 of tile u+gridDim.x, and the last step's fragment reads take that tile's
+// first fragments, so the next tile starts with its operands already in LDS and registers (no
+// prologue) while the epilogue of tile u runs from a private LDS strip (the 4 x 4.3 KB above the
+// 128-KB ring).  Rows past M / N read as zeros from the buffer range check (num_records), so the
+// per-lane load offsets are the same for every tile.
+template <int S>
+__device__ __forceinline__ void s7_step(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8], u32x4 (&b0)[8],
+                                        u32x4 (&a1)[8], u32x4 (&b1)[8], u32x4 (&stg)[16], char* lds_lane, int ks) {
+  s4_wait_frags(a0, b0);
+  s6_half<S, 1, 0, S>(c, acc, a0, b0, a1, b1, stg, lds_lane, ks);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  s4_wait_frags(a1, b1);
+  __builtin_amdgcn_s_barrier();
+  s6_half<S ^ 1, 0, 1, S>(c, acc, a1, b1, a0, b0, stg, lds_lane, 0);
+}
+
+constexpr int S7_STRIP = 16 * 68 * 4;             // [16 rows][64 (+4) cols] fp32 per wave
+constexpr int S7_LDS = S5_LDS + 4 * S7_STRIP;     // 145 KB
+
+template <int EPI>
+__device__ __forceinline__ void s7_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8], char* smem, int wave, int lane,
+                                            int m0, int n0, long bz) {
+  const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fc = lane >> 4;
+  float* strip = (float*)(smem + S5_LDS + wave * S7_STRIP);
+  const int er = lane >> 2, ec = (lane & 3) * 16;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int grow = m0 + wm * 128 + i * 16 + er;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) *(f32x4*)(strip + fr * 68 + j * 16 + fc * 4) = acc[i][4 * h + j];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 t = *(const f32x4*)(strip + er * 68 + ec + q * 4);
+        v[4 * q] = t[0]; v[4 * q + 1] = t[1]; v[4 * q + 2] = t[2]; v[4 * q + 3] = t[3];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      const int gcol = n0 + wn * 128 + h * 64 + ec;
+      if (grow < g.M && gcol < g.N) epi_row<EPI, 16>(g, v, bz, grow, gcol);
+    }
+  }
+}
+
+__device__ __forceinline__ void s7_tile(const GemmArgs& g, int u, int total, int G, int nm, int nn, int& m0, int& n0,
+                                        long& bz, __amdgpu_buffer_rsrc_t& ra, __amdgpu_buffer_rsrc_t& rw) {
+  // rounds of G tiles; within a round the XCD remap hands each XCD a contiguous run of tile ids
+  const int per = nm * nn;
+  const int round = u / G;
+  const int nwg = min(G, total - round * G);
+  const int w = round * G + xcd_remap(u - round * G, nwg);
+  bz = w / per;
+  int mt, nt;
+  tile_coords(w - (int)bz * per, nm, nn, g.group_m, mt, nt);
+  m0 = mt * BM;
+  n0 = nt * BN;
+  const int rows_a = min(BM, g.M - m0), rows_w = min(BN, g.N - n0);
+  ra = __builtin_amdgcn_make_buffer_rsrc((void*)(g.A + bz * g.sA + (long)m0 * g.lda), (short)0,
+                                         (int)(rows_a * g.lda * 2), 0x00020000);
+  rw = __builtin_amdgcn_make_buffer_rsrc((void*)(g.W + bz * g.sW + (long)n0 * g.ldw), (short)0,
+                                         (int)(rows_w * g.ldw * 2), 0x00020000);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_s7_kernel(GemmArgs g, int batch) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
+  const int total = nm * nn * batch, G = gridDim.x;
+  int u = blockIdx.x;
+  S5Ctx c;
+  int m0, n0;
+  long bz;
+  s7_tile(g, u, total, G, nm, nn, m0, n0, bz, c.ra, c.rw);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = (i * 4 + wave) * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    c.aoff[i] = row * (int)g.lda * 2 + chunk * 16;
+    c.woff[i] = row * (int)g.ldw * 2 + chunk * 16;
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
+  char* lds_lane = smem + wave * 1024 + lane * 16;
+  const int fr = lane & 15, fc = lane >> 4;
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      const int sw = ((4 * kh + fc) ^ ((fr >> 1) & 7)) << 4;
+      c.ard[st][kh] = lds0 + st * S5_STAGE + (wm * 128 + fr) * 128 + sw;
+      c.wrd[st][kh] = lds0 + st * S5_STAGE + 256 * 128 + (wn * 128 + fr) * 128 + sw;
+    }
+  const int nk = g.K / 64;  // even (launcher: K % 128 == 0)
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  u32x4 a0[8], b0[8], a1[8], b1[8], stg[16];
+#define SA_S7_FILL(STAGE, T)                                                                              \
+  {                                                                                                       \
+    const int ks = (T) * 128;                                                                             \
+    s6_load<STAGE, 0>(c, stg, ks); s6_load<STAGE, 1>(c, stg, ks); s6_load<STAGE, 2>(c, stg, ks);          \
+    s6_load<STAGE, 3>(c, stg, ks); s6_load<STAGE, 4>(c, stg, ks); s6_load<STAGE, 5>(c, stg, ks);          \
+    s6_load<STAGE, 6>(c, stg, ks); s6_load<STAGE, 7>(c, stg, ks); s6_load<STAGE, 8>(c, stg, ks);          \
+    s6_load<STAGE, 9>(c, stg, ks); s6_load<STAGE, 10>(c, stg, ks); s6_load<STAGE, 11>(c, stg, ks);        \
+    s6_load<STAGE, 12>(c, stg, ks); s6_load<STAGE, 13>(c, stg, ks); s6_load<STAGE, 14>(c, stg, ks);       \
+    s6_load<STAGE, 15>(c, stg, ks);                                                                       \
+    s6_store<STAGE, 0>(lds_lane, stg); s6_store<STAGE, 1>(lds_lane, stg); s6_store<STAGE, 2>(lds_lane, stg);     \
+    s6_store<STAGE, 3>(lds_lane, stg); s6_store<STAGE, 4>(lds_lane, stg); s6_store<STAGE, 5>(lds_lane, stg);     \
+    s6_store<STAGE, 6>(lds_lane, stg); s6_store<STAGE, 7>(lds_lane, stg); s6_store<STAGE, 8>(lds_lane, stg);     \
+    s6_store<STAGE, 9>(lds_lane, stg); s6_store<STAGE, 10>(lds_lane, stg); s6_store<STAGE, 11>(lds_lane, stg);   \
+    s6_store<STAGE, 12>(lds_lane, stg); s6_store<STAGE, 13>(lds_lane, stg); s6_store<STAGE, 14>(lds_lane, stg);  \
+    s6_store<STAGE, 15>(lds_lane, stg);                                                                   \
+  }
+  SA_S7_FILL(0, 0)
+  SA_S7_FILL(1, 1)
+#undef SA_S7_FILL
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  s5_read<0, 0, 0>(c, a0, b0); s5_read<0, 0, 1>(c, a0, b0); s5_read<0, 0, 2>(c, a0, b0); s5_read<0, 0, 3>(c, a0, b0);
+  s5_read<0, 0, 4>(c, a0, b0); s5_read<0, 0, 5>(c, a0, b0); s5_read<0, 0, 6>(c, a0, b0); s5_read<0, 0, 7>(c, a0, b0);
+  s5_read<0, 0, 8>(c, a0, b0); s5_read<0, 0, 9>(c, a0, b0); s5_read<0, 0, 10>(c, a0, b0); s5_read<0, 0, 11>(c, a0, b0);
+  s5_read<0, 0, 12>(c, a0, b0); s5_read<0, 0, 13>(c, a0, b0); s5_read<0, 0, 14>(c, a0, b0); s5_read<0, 0, 15>(c, a0, b0);
+
+  while (true) {
+    const int un = u + G;
+    const bool has_next = un < total;
+    __amdgpu_buffer_rsrc_t cra = c.ra, crw = c.rw, nra = c.ra, nrw = c.rw;
+    int nm0 = m0, nn0 = n0;
+    long nbz = bz;
+    if (has_next) s7_tile(g, un, total, G, nm, nn, nm0, nn0, nbz, nra, nrw);
+    for (int t = 0; t < nk; t += 2) {
+      {
+        const bool nx = t + 2 >= nk;  // stage the next tile's K-tile t+2-nk (or re-read the last one)
+        c.ra = nx ? nra : cra;
+        c.rw = nx ? nrw : crw;
+        s7_step<0>(c, acc, a0, b0, a1, b1, stg, lds_lane, (nx ? (has_next ? t + 2 - nk : nk - 1) : t + 2) * 128);
+      }
+      {
+        const bool nx = t + 3 >= nk;
+        c.ra = nx ? nra : cra;
+        c.rw = nx ? nrw : crw;
+        s7_step<1>(c, acc, a0, b0, a1, b1, stg, lds_lane, (nx ? (has_next ? t + 3 - nk : nk - 1) : t + 3) * 128);
+      }
+    }
+    asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // MFMA -> v_accvgpr_read
+    s7_epilogue<EPI>(g, acc, smem, wave, lane, m0, n0, bz);
+    if (!has_next) break;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    u = un;
+    m0 = nm0;
+    n0 = nn0;
+    bz = nbz;
+    c.ra = nra;
+    c.rw = nrw;
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
+int g_num_cus = 0;
+
 int g_gemm_variant = -1;  // 0 = v1 (2-phase), 1 = phased (8 waves), 2 = w4 (4 waves, AGPR accumulators),
-                          // 3 = ping-pong 8-phase, 4 = ping-pong with direct (operand-swapped) epilogue
+                          // 3 = ping-pong 8-phase, 4 = ping-pong with direct (operand-swapped) epilogue,
+                          // 5 = s4 (one wave per SIMD, buffer-DMA ring, scheduled interleave),
+                          // 6-8 = s4 measurement ablations, 9 = s5 (s4 with 128-B rows, 2-stage ring),
+                          // 10 = s6 (s5 with register-staged loads), 11 = s7 (persistent s6)
 
 template <int EPI>
 int launch(const GemmArgs& g, int batch, hipStream_t st) {
@@ -755,6 +1466,10 @@ int launch(const GemmArgs& g, int batch, hipStream_t st) {
     (void)hipFuncSetAttribute((const void*)gemm_phased_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_w4_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, W4_LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_s4_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S4_LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_s5_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S5_LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_s6_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S5_LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_s7_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S7_LDS);
     (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -773,8 +1488,40 @@ int launch(const GemmArgs& g, int batch, hipStream_t st) {
     // the LDS transpose for 16-B row stores
     constexpr bool F32_OUT = EPI == EPI_RES_F32 || EPI == EPI_F32 || EPI == EPI_SILU_F32;
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, F32_OUT>), dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
-  }
-  else
+  } else if (g_gemm_variant == 5 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
+             (long)BN * g.ldw * 2 < 0x7fffffffL)
+    hipLaunchKernelGGL(gemm_s4_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(256), S4_LDS, st, g);
+  else if (g_gemm_variant == 9 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
+           (long)BN * g.ldw * 2 < 0x7fffffffL)
+    hipLaunchKernelGGL(gemm_s5_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(256), S5_LDS, st, g);
+  else if (g_gemm_variant == 10 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
+           (long)BN * g.ldw * 2 < 0x7fffffffL)
+    hipLaunchKernelGGL(gemm_s6_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(256), S5_LDS, st, g);
+  else if (g_gemm_variant == 11 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
+           (long)BN * g.ldw * 2 < 0x7fffffffL) {
+    if (!g_num_cus) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_num_cus <= 0)
+        g_num_cus = 256;
+    }
+    const int total = nm * nn * batch;
+    hipLaunchKernelGGL(gemm_s7_kernel<EPI>, dim3(min(total, g_num_cus)), dim3(256), S7_LDS, st, g, batch);
+  } else if (g_gemm_variant >= 6 && g_gemm_variant <= 8 && EPI == EPI_BF16 && g.K % 128 == 0) {
+    static int attr_abl = 0;
+    if (!attr_abl) {
+      (void)hipFuncSetAttribute((const void*)gemm_s4_kernel<EPI, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S4_LDS);
+      (void)hipFuncSetAttribute((const void*)gemm_s4_kernel<EPI, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, S4_LDS);
+      (void)hipFuncSetAttribute((const void*)gemm_s4_kernel<EPI, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, S4_LDS);
+      attr_abl = 1;
+    }
+    if (g_gemm_variant == 6)
+      hipLaunchKernelGGL((gemm_s4_kernel<EPI, 1>), dim3(nm * nn, 1, batch), dim3(256), S4_LDS, st, g);
+    else if (g_gemm_variant == 7)
+      hipLaunchKernelGGL((gemm_s4_kernel<EPI, 2>), dim3(nm * nn, 1, batch), dim3(256), S4_LDS, st, g);
+    else
+      hipLaunchKernelGGL((gemm_s4_kernel<EPI, 3>), dim3(nm * nn, 1, batch), dim3(256), S4_LDS, st, g);
+  } else
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, true>), dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
   SA_LAUNCH_CHECK();
   return SA_OK;
@@ -782,8 +1529,15 @@ int launch(const GemmArgs& g, int batch, hipStream_t st) {
 
 }  // namespace
 
+int g_group_m_override = 0;
+extern "C" int sa_gemm_set_group_m(int gm) {
+  if (gm < 0) return SA_ERR_ARG;
+  g_group_m_override = gm;
+  return SA_OK;
+}
+
 extern "C" int sa_gemm_set_variant(int variant) {
-  if (variant < 0 || variant > 4) return SA_ERR_ARG;
+  if (variant < 0 || variant > 11) return SA_ERR_ARG;
   g_gemm_variant = variant;
   return SA_OK;
 }
@@ -796,8 +1550,18 @@ extern "C" int sa_gemm_bf16(const void* A, int64_t lda, int64_t strideA, const v
   if (K % BK != 0 || lda % 8 != 0 || ldw % 8 != 0) return SA_ERR_ARG;
   if ((((uintptr_t)A) & 15) || (((uintptr_t)W) & 15)) return SA_ERR_ARG;
   if (epilogue == EPI_RES_F32 && (!residual || (gate && rows_per_batch <= 0))) return SA_ERR_ARG;
+  static int group_m_env = -1;
+  if (group_m_env < 0) {
+    const char* e = getenv("SA_GEMM_GROUP_M");
+    group_m_env = e ? atoi(e) : 0;
+    if (group_m_env < 0) group_m_env = 0;
+  }
+  // measured (kbench gemmvar, 64512-row DiT GEMMs): runs of 8 tile rows help the wide-N GEMMs
+  // (QKV +2.3 %, FFN-up +2.8 %, 8192^3 +5 %) and cost the N = 1536 ones up to 2.7 %
+  const int group_m = group_m_env ? group_m_env : (N >= 4096 ? 8 : 1);
   GemmArgs g{(const bf16*)A, lda, strideA, (const bf16*)W, ldw, strideW, bias, C, ldc, strideC,
-             residual, ldr, strideR, gate, gate_bstride, rows_per_batch > 0 ? rows_per_batch : 1, M, N, K};
+             residual, ldr, strideR, gate, gate_bstride, rows_per_batch > 0 ? rows_per_batch : 1, M, N, K,
+             g_group_m_override > 0 ? g_group_m_override : group_m};
   hipStream_t st = (hipStream_t)stream;
   switch (epilogue) {
     case EPI_BF16: return launch<EPI_BF16>(g, batch, st);

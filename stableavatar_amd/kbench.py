@@ -30,34 +30,43 @@ def main(which=("gemm", "attn")):
     M = 3 * 21504
     res = []
     if "gemmvar" in which:  # A/B of the GEMM variants in one process (rule: interleaved rounds)
-        for (N, K, epi, name) in [(4608, 1536, ops.EPI_BF16, "qkv"), (1536, 1536, ops.EPI_RES_F32, "o_proj"),
-                                  (8960, 1536, ops.EPI_GELU_TANH_BF16, "ffn_up"),
-                                  (1536, 8960, ops.EPI_RES_F32, "ffn_down")]:
-            x = torch.randn(M, K, device=dev).bfloat16()
-            w = (torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
+        import os
+        # variant spec "V" or "V:G" (G = tile-raster group_m)
+        gvars = tuple(os.environ.get("SA_KB_GVARS", "3,4").split(","))
+        for (Mx, N, K, epi, name) in [(M, 4608, 1536, ops.EPI_BF16, "qkv"), (M, 1536, 1536, ops.EPI_RES_F32, "o_proj"),
+                                      (M, 8960, 1536, ops.EPI_GELU_TANH_BF16, "ffn_up"),
+                                      (M, 1536, 8960, ops.EPI_RES_F32, "ffn_down"),
+                                      (8192, 8192, 8192, ops.EPI_BF16, "sq8192")]:
+            if os.environ.get("SA_KB_SHAPES") and name not in os.environ["SA_KB_SHAPES"].split(","):
+                continue
+            x = (torch.rand(Mx, K, device=dev) * 2 - 1).bfloat16()
+            w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).bfloat16()
             b = torch.randn(N, device=dev)
-            out = torch.empty(M, N, device=dev, dtype=torch.float32 if epi == ops.EPI_RES_F32 else torch.bfloat16)
+            out = torch.empty(Mx, N, device=dev, dtype=torch.float32 if epi == ops.EPI_RES_F32 else torch.bfloat16)
             gate = torch.randn(3, N, device=dev)
             ref = None
-            gvars = (3, 4)
             times = {v: [] for v in gvars}
             for rnd in range(3):
                 for v in gvars:
-                    call("sa_gemm_set_variant", v)
+                    vv, _, gm = v.partition(":")
+                    call("sa_gemm_set_variant", int(vv))
+                    call("sa_gemm_set_group_m", int(gm or 0))
                     if epi == ops.EPI_RES_F32:
                         out.zero_()
                         fn = lambda: ops.linear(x, w, b, epi, out=out, residual=out, gate=gate, rows_per_batch=21504)
                     else:
                         fn = lambda: ops.linear(x, w, b, epi, out=out)
                     times[v].append(_time(fn, iters=5, warmup=1))
-                    if epi != ops.EPI_RES_F32:
+                    if epi != ops.EPI_RES_F32 and int(vv) < 6:
                         o = out.float()
                         if ref is None:
                             ref = o.clone()
                         err = ((o - ref).norm() / ref.norm()).item()
                         assert err < 1e-2, (name, v, err)
-            fl = 2.0 * M * N * K
-            r = {"kernel": f"gemm_{name}", "M": M, "N": N, "K": K}
+            fl = 2.0 * Mx * N * K
+            r = {"kernel": f"gemm_{name}", "M": Mx, "N": N, "K": K}
+            ms_ref = _time(lambda: torch.nn.functional.linear(x, w), iters=5, warmup=1)
+            r["torch_tflops"] = round(fl / ms_ref / 1e9, 1)
             for v in gvars:
                 ms = sorted(times[v])[1]
                 r[f"v{v}_ms"] = round(ms, 4)
@@ -66,6 +75,7 @@ def main(which=("gemm", "attn")):
             print(json.dumps(r), flush=True)
             del x, w, out
         call("sa_gemm_set_variant", 4)
+        call("sa_gemm_set_group_m", 0)
     if "attnvar" in which:
         L, H, D = 21504, 12, 128
         qkv = torch.randn(3 * L, 3 * H * D, device=dev).bfloat16()

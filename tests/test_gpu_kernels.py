@@ -49,6 +49,37 @@ def test_gemm_epilogues(M, N, K):
     assert rel(out, res + ref * g_rows) < 2e-3
 
 
+@pytest.mark.parametrize("variant", [3, 4, 5, 9, 10, 11])
+@pytest.mark.parametrize("M,N,K", [(300, 520, 256), (257, 130, 128), (1000, 1536, 1536), (600, 300, 2304)])
+def test_gemm_variants(variant, M, N, K):
+    """Every GEMM schedule (sa_gemm_set_variant) on ragged M/N tiles, every epilogue, vs torch fp32."""
+    from stableavatar_amd import ops
+    from stableavatar_amd._lib import call
+    call("sa_gemm_set_variant", variant)
+    try:
+        x = torch.randn(M, K + 64, device=dev).bfloat16()[:, 32:32 + K]  # strided rows
+        w = (torch.randn(N, K, device=dev) / math.sqrt(K)).bfloat16()
+        b = torch.randn(N, device=dev)
+        ref = x.float() @ w.float().t() + b
+        assert rel(ops.linear(x, w, b, ops.EPI_BF16), ref) < 1e-2
+        assert rel(ops.linear(x, w, b, ops.EPI_F32), ref) < 2e-3
+        assert rel(ops.linear(x, w, b, ops.EPI_GELU_TANH_BF16), torch.nn.functional.gelu(ref, approximate="tanh")) < 1e-2
+        B = 3
+        rpb = (M + B - 1) // B
+        res = torch.randn(M, N, device=dev)
+        gate = torch.randn(B, N, device=dev)
+        out = res.clone()
+        ops.linear(x, w, b, ops.EPI_RES_F32, out=out, residual=out, gate=gate, rows_per_batch=rpb)
+        assert rel(out, res + ref * gate[torch.arange(M, device=dev) // rpb]) < 2e-3
+        a = torch.randn(2, 300, K, device=dev).bfloat16()
+        bb = torch.randn(2, 200, K, device=dev).bfloat16()
+        o = torch.empty(2, 300, 200, device=dev)
+        ops.bmm_nt(a, bb, o)
+        assert rel(o, a.float() @ bb.float().transpose(1, 2)) < 2e-3
+    finally:
+        call("sa_gemm_set_variant", 4)
+
+
 def test_gemm_strided_input_and_batched():
     from stableavatar_amd import ops
     big = torch.randn(200, 320, device=dev).bfloat16()
