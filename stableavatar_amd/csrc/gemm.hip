@@ -1155,7 +1155,7 @@ __device__ __forceinline__ void s6_store(char* lds_lane, const u32x4 (&stg)[16])
   *(u32x4*)(lds_lane + off) = stg[P];
 }
 
-template <int RS, int RK, int MODE, int DS>
+template <int RS, int RK, int MODE, int DS, int ABL = 0>
 __device__ __forceinline__ void s6_half(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&ac)[8], u32x4 (&bc)[8],
                                         u32x4 (&an)[8], u32x4 (&bn)[8], u32x4 (&stg)[16], char* lds_lane, int ks) {
   // MODE 0: reads of the next fragments in rows 0-3, global loads (tile ks) in rows 4-7
@@ -1164,38 +1164,39 @@ __device__ __forceinline__ void s6_half(const S5Ctx& c, f32x4 (&acc)[8][8], u32x
   {                                                                                           \
     s4_mma(acc[Q][0], bc[0], ac[Q]); s4_mma(acc[Q][1], bc[1], ac[Q]);                         \
     if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q>(c, an, bn); }                               \
-    else if constexpr (MODE == 0) { s6_load<DS, 4 * (Q - 4)>(c, stg, ks); }                   \
-    else { s6_store<DS, 4 * (Q - 4)>(lds_lane, stg); }                                        \
+    else if constexpr (MODE == 0) { if constexpr (!(ABL & 1)) s6_load<DS, 4 * (Q - 4)>(c, stg, ks); }                   \
+    else { if constexpr (!(ABL & 2)) s6_store<DS, 4 * (Q - 4)>(lds_lane, stg); else asm volatile("" :: "v"(stg[4 * (Q - 4)])); }                                        \
     s4_mma(acc[Q][2], bc[2], ac[Q]); s4_mma(acc[Q][3], bc[3], ac[Q]);                         \
     if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 1>(c, an, bn); }                           \
-    else if constexpr (MODE == 0) { s6_load<DS, 4 * (Q - 4) + 1>(c, stg, ks); }               \
-    else { s6_store<DS, 4 * (Q - 4) + 1>(lds_lane, stg); }                                    \
+    else if constexpr (MODE == 0) { if constexpr (!(ABL & 1)) s6_load<DS, 4 * (Q - 4) + 1>(c, stg, ks); }               \
+    else { if constexpr (!(ABL & 2)) s6_store<DS, 4 * (Q - 4) + 1>(lds_lane, stg); else asm volatile("" :: "v"(stg[4 * (Q - 4) + 1])); }                                    \
     s4_mma(acc[Q][4], bc[4], ac[Q]); s4_mma(acc[Q][5], bc[5], ac[Q]);                         \
     if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 2>(c, an, bn); }                           \
-    else if constexpr (MODE == 0) { s6_load<DS, 4 * (Q - 4) + 2>(c, stg, ks); }               \
-    else { s6_store<DS, 4 * (Q - 4) + 2>(lds_lane, stg); }                                    \
+    else if constexpr (MODE == 0) { if constexpr (!(ABL & 1)) s6_load<DS, 4 * (Q - 4) + 2>(c, stg, ks); }               \
+    else { if constexpr (!(ABL & 2)) s6_store<DS, 4 * (Q - 4) + 2>(lds_lane, stg); else asm volatile("" :: "v"(stg[4 * (Q - 4) + 2])); }                                    \
     s4_mma(acc[Q][6], bc[6], ac[Q]); s4_mma(acc[Q][7], bc[7], ac[Q]);                         \
     if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 3>(c, an, bn); }                           \
-    else if constexpr (MODE == 0) { s6_load<DS, 4 * (Q - 4) + 3>(c, stg, ks); }               \
-    else { s6_store<DS, 4 * (Q - 4) + 3>(lds_lane, stg); }                                    \
+    else if constexpr (MODE == 0) { if constexpr (!(ABL & 1)) s6_load<DS, 4 * (Q - 4) + 3>(c, stg, ks); }               \
+    else { if constexpr (!(ABL & 2)) s6_store<DS, 4 * (Q - 4) + 3>(lds_lane, stg); else asm volatile("" :: "v"(stg[4 * (Q - 4) + 3])); }                                    \
   }
   SA_S6_ROW(0) SA_S6_ROW(1) SA_S6_ROW(2) SA_S6_ROW(3) SA_S6_ROW(4) SA_S6_ROW(5) SA_S6_ROW(6) SA_S6_ROW(7)
 #undef SA_S6_ROW
 }
 
-template <int S>
+template <int S, int ABL = 0>
 __device__ __forceinline__ void s6_step(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8], u32x4 (&b0)[8],
                                         u32x4 (&a1)[8], u32x4 (&b1)[8], u32x4 (&stg)[16], char* lds_lane, int t,
                                         int nk) {
   s4_wait_frags(a0, b0);
-  s6_half<S, 1, 0, S>(c, acc, a0, b0, a1, b1, stg, lds_lane, min(t + 2, nk - 1) * 128);
+  s6_half<S, 1, 0, S, ABL>(c, acc, a0, b0, a1, b1, stg, lds_lane, min(t + 2, nk - 1) * 128);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of stage S and its ds_writes
   s4_wait_frags(a1, b1);
   __builtin_amdgcn_s_barrier();
-  s6_half<S ^ 1, 0, 1, S>(c, acc, a1, b1, a0, b0, stg, lds_lane, 0);
+  s6_half<S ^ 1, 0, 1, S, ABL>(c, acc, a1, b1, a0, b0, stg, lds_lane, 0);
 }
 
-template <int EPI>
+// ABL (measurement builds only): 1 = no staged global loads, 2 = no staged ds_writes
+template <int EPI, int ABL = 0>
 __global__ __launch_bounds__(256, 1) void gemm_s6_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1264,8 +1265,8 @@ __global__ __launch_bounds__(256, 1) void gemm_s6_kernel(GemmArgs g) {
   s5_read<0, 0, 12>(c, a0, b0); s5_read<0, 0, 13>(c, a0, b0); s5_read<0, 0, 14>(c, a0, b0); s5_read<0, 0, 15>(c, a0, b0);
 
   for (int t = 0; t < nk; t += 2) {
-    s6_step<0>(c, acc, a0, b0, a1, b1, stg, lds_lane, t, nk);
-    s6_step<1>(c, acc, a0, b0, a1, b1, stg, lds_lane, t + 1, nk);
+    s6_step<0, ABL>(c, acc, a0, b0, a1, b1, stg, lds_lane, t, nk);
+    s6_step<1, ABL>(c, acc, a0, b0, a1, b1, stg, lds_lane, t + 1, nk);
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -1507,6 +1508,17 @@ int launch(const GemmArgs& g, int batch, hipStream_t st) {
     }
     const int total = nm * nn * batch;
     hipLaunchKernelGGL(gemm_s7_kernel<EPI>, dim3(min(total, g_num_cus)), dim3(256), S7_LDS, st, g, batch);
+  } else if ((g_gemm_variant == 12 || g_gemm_variant == 13) && EPI == EPI_BF16 && g.K % 128 == 0) {
+    static int attr6 = 0;
+    if (!attr6) {
+      (void)hipFuncSetAttribute((const void*)gemm_s6_kernel<EPI, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S5_LDS);
+      (void)hipFuncSetAttribute((const void*)gemm_s6_kernel<EPI, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, S5_LDS);
+      attr6 = 1;
+    }
+    if (g_gemm_variant == 12)
+      hipLaunchKernelGGL((gemm_s6_kernel<EPI, 1>), dim3(nm * nn, 1, batch), dim3(256), S5_LDS, st, g);
+    else
+      hipLaunchKernelGGL((gemm_s6_kernel<EPI, 2>), dim3(nm * nn, 1, batch), dim3(256), S5_LDS, st, g);
   } else if (g_gemm_variant >= 6 && g_gemm_variant <= 8 && EPI == EPI_BF16 && g.K % 128 == 0) {
     static int attr_abl = 0;
     if (!attr_abl) {
@@ -1537,7 +1549,7 @@ extern "C" int sa_gemm_set_group_m(int gm) {
 }
 
 extern "C" int sa_gemm_set_variant(int variant) {
-  if (variant < 0 || variant > 11) return SA_ERR_ARG;
+  if (variant < 0 || variant > 13) return SA_ERR_ARG;
   g_gemm_variant = variant;
   return SA_OK;
 }
