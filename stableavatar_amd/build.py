@@ -22,12 +22,17 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-r
           f"-I{CSRC}", f"-I{PKG.parent / 'include'}"]
 
 
+# per-source extra flags (none at present: -fno-slp-vectorize on attention.hip was measured slower,
+# it pushes the 16x16x32 attention into scratch spills and costs the 32x32x16 one 4 %)
+EXTRA: dict[str, list[str]] = {}
+
+
 def _compile(src: Path) -> Path:
     obj = BUILD / (src.stem + ".o")
-    deps = [src, CSRC / "common.h"]
+    deps = [src, CSRC / "common.h", Path(__file__)]
     if obj.exists() and all(obj.stat().st_mtime >= d.stat().st_mtime for d in deps if d.exists()):
         return obj
-    cmd = [HIPCC, *CFLAGS, "-c", str(src), "-o", str(obj)]
+    cmd = [HIPCC, *CFLAGS, *EXTRA.get(src.stem, []), "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr}")

@@ -1191,14 +1191,301 @@ extern "C" int sa_attn_small(const void* q, const void* k, const void* v, void* 
   return SA_OK;
 }
 
+// ---- v6: v3's pipeline (2-deep K/V ring by LDS-DMA, asm LDS reads with counted waits, prescaled Q
+// and -m as the QK^T initial accumulator, deferred rescale) on mfma_f32_16x16x32_bf16 instead of
+// 32x32x16.  The two shapes take the same cycles per FLOP, but under load the chip holds a higher
+// clock on the 16x16x32 stream (MI355X_MICROARCH.md "DVFS give-back" item 7: ~1.12-1.15x FLOP/s on
+// random data).  Per wave: 32 queries as two 16-query tiles, 64-key blocks as four 16-key tiles.
+//   S^T tile (kt, qt) = K_kt · Q_qt^T: lane holds keys 4g+i (g = lane/16) of tile kt for query lane%16
+//   P^T as the PV B operand: the 32-key chunk c is taken in the permuted key order
+//     k = 8g + j -> key 32c + 4g + j (j < 4), 32c + 16 + 4g + j - 4 (j >= 4)
+//   so a lane's 8 P values are its own S^T registers of tiles 2c and 2c+1 (no lane exchange), and the
+//   V^T A operand uses the same order: two ds_read_b64_tr_b16 (rows 32c+4g.. and 32c+16+4g..)
+//   row max over 64 keys: 15 VALU max + permlane32 / permlane16 swaps; row sums stay per lane until
+//   the end.
+// LDS images: K rows chunk ^ (row & 15) (conflict-free 16-row b128 reads), V rows chunk ^ 2(row & 7)
+// (conflict-free transposed reads).
+__device__ __forceinline__ float max16x2(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ bf16x8 v6_as_bf8(u32x4 x) { return __builtin_bit_cast(bf16x8, x); }
+__device__ __forceinline__ bf16x8 v6_as_bf8(u32x2 lo, u32x2 hi) {
+  const u32x4 x = {lo[0], lo[1], hi[0], hi[1]};
+  return __builtin_bit_cast(bf16x8, x);
+}
+
+// K fragments of key tile KT (d chunks 0-3) of stage BUF
+template <int BUF, int KT>
+__device__ __forceinline__ void v6_read_k(u32x4* f, const uint32_t* ka) {
+  constexpr int base = BUF * STAGE_BYTES + KT * 4096;
+  ds_b128<base>(f[0], ka[0]);
+  ds_b128<base>(f[1], ka[1]);
+  ds_b128<base>(f[2], ka[2]);
+  ds_b128<base>(f[3], ka[3]);
+}
+// V^T fragments of key chunk C for d tiles DT0..DT0+3: f[2*t + h], h = rows +0 / +16
+template <int BUF, int C, int DT0>
+__device__ __forceinline__ void v6_read_v(u32x2* f, const uint32_t* va) {
+  constexpr int base = BUF * STAGE_BYTES + TILE_BYTES + C * 8192;
+  ds_tr64<base>(f[0], va[DT0 + 0]); ds_tr64<base + 4096>(f[1], va[DT0 + 0]);
+  ds_tr64<base>(f[2], va[DT0 + 1]); ds_tr64<base + 4096>(f[3], va[DT0 + 1]);
+  ds_tr64<base>(f[4], va[DT0 + 2]); ds_tr64<base + 4096>(f[5], va[DT0 + 2]);
+  ds_tr64<base>(f[6], va[DT0 + 3]); ds_tr64<base + 4096>(f[7], va[DT0 + 3]);
+}
+__device__ __forceinline__ void v6_mma_k(f32x4 (&S)[4][2], int kt, const u32x4* f, const bf16x8 (&qf)[2][4]) {
+#pragma unroll
+  for (int dc = 0; dc < 4; ++dc) {
+    S[kt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v6_as_bf8(f[dc]), qf[0][dc], S[kt][0], 0, 0, 0);
+    S[kt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v6_as_bf8(f[dc]), qf[1][dc], S[kt][1], 0, 0, 0);
+  }
+}
+__device__ __forceinline__ void v6_mma_v(f32x4 (&O)[8][2], int dt0, const u32x2* f, const bf16x8 (&pb)[2]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const bf16x8 a = v6_as_bf8(f[2 * t], f[2 * t + 1]);
+    O[dt0 + t][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb[0], O[dt0 + t][0], 0, 0, 0);
+    O[dt0 + t][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb[1], O[dt0 + t][1], 0, 0, 0);
+  }
+}
+template <int N>
+__device__ __forceinline__ void wait_k4(u32x4* f) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]) : "i"(N));
+}
+
+struct V6State {
+  f32x4 O[8][2];
+  f32x4 L[2];     // row sums of the bf16 P (every element equal), from a ones x P^T MFMA
+  float negm[2];  // -m per query tile (this lane's query)
+};
+
+template <int BUF>
+__device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2][4], const uint32_t* ka,
+                                              const uint32_t* va, int kb, int kv_len, int g) {
+  f32x4 S[4][2];
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) S[kt][qt] = (f32x4){st.negm[qt], st.negm[qt], st.negm[qt], st.negm[qt]};
+  // S'^T = c K Q^T - m, K fragments two key tiles ahead
+  u32x4 k0[4], k1[4];
+  v6_read_k<BUF, 0>(k0, ka);
+  v6_read_k<BUF, 1>(k1, ka);
+  wait_k4<4>(k0);
+  v6_mma_k(S, 0, k0, qf);
+  v6_read_k<BUF, 2>(k0, ka);
+  wait_k4<4>(k1);
+  v6_mma_k(S, 1, k1, qf);
+  v6_read_k<BUF, 3>(k1, ka);
+  wait_k4<4>(k0);
+  v6_mma_k(S, 2, k0, qf);
+  wait_k4<0>(k1);
+  v6_mma_k(S, 3, k1, qf);
+  // first V^T fragments under the softmax
+  u32x2 v0[8], v1[8];
+  v6_read_v<BUF, 0, 0>(v0, va);
+  v6_read_v<BUF, 0, 4>(v1, va);
+
+  if (kb * KVB + KVB > kv_len) {
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (kb * KVB + kt * 16 + 4 * g + i >= kv_len) { S[kt][0][i] = -INFINITY; S[kt][1][i] = -INFINITY; }
+  }
+  float mx[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    float m = S[0][qt][0];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) m = fmaxf(m, S[kt][qt][i]);
+    mx[qt] = max16x2(m);  // max of c S - m over the block's 64 keys
+  }
+  const bool first = kb == 0;
+  if (first || !__all(mx[0] <= RESCALE_THR && mx[1] <= RESCALE_THR)) {  // wave-uniform
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const float delta = first ? mx[qt] : fmaxf(mx[qt], 0.f);
+      const float alpha = __builtin_amdgcn_exp2f(-delta);
+      st.L[qt] *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st.O[dt][qt][i] *= alpha;
+      st.negm[qt] -= delta;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) S[kt][qt][i] -= delta;
+    }
+  }
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) S[kt][qt][i] = __builtin_amdgcn_exp2f(S[kt][qt][i]);
+  // O^T += V^T P^T, key chunk c = tiles (2c, 2c+1)
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    bf16x8 pb[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[qt][j] = f2bf(S[2 * c][qt][j]);
+        pb[qt][4 + j] = f2bf(S[2 * c + 1][qt][j]);
+      }
+    {
+      bf16x8 ones;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+      st.L[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[0], st.L[0], 0, 0, 0);
+      st.L[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[1], st.L[1], 0, 0, 0);
+    }
+    if (c == 0) {
+      wait_v<8>(v0);
+      v6_mma_v(st.O, 0, v0, pb);
+      v6_read_v<BUF, 1, 0>(v0, va);
+      wait_v<8>(v1);
+      v6_mma_v(st.O, 4, v1, pb);
+      v6_read_v<BUF, 1, 4>(v1, va);
+    } else {
+      wait_v<8>(v0);
+      v6_mma_v(st.O, 0, v0, pb);
+      wait_v<0>(v1);
+      v6_mma_v(st.O, 4, v1, pb);
+    }
+  }
+}
+
+__global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nx = gridDim.x, ny = gridDim.y;
+  const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
+  const int qb = flat % nx, h = (flat / nx) % ny, seg = flat / (nx * ny);
+  const int* sg = a.segs + seg * 4;
+  const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
+  if (qb * QB >= q_len || kv_len <= 0) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+
+  // Q as the B operand: query tile qt, d chunk dc: Q[query][dc*32 + 8g .. +7], prescaled by c
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qc = min(qb * QB + wave * 32 + qt * 16 + r16, q_len - 1);
+    const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * g;
+#pragma unroll
+    for (int dc = 0; dc < 4; ++dc) {
+      qf[qt][dc] = *(const bf16x8*)(qp + 32 * dc);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[qt][dc][j] = f2bf(bf2f(qf[qt][dc][j]) * a.c);
+    }
+  }
+
+  // staging: each wave moves 2 x 1-KB pieces (4 rows each) of K and of V per block; lane -> row
+  // (lane / 16), stored position lane % 16 holding source chunk (lane % 16) ^ swizzle(row)
+  const bf16* kbase = a.k + h * D;
+  const bf16* vbase = a.v + h * D;
+  int srow[2];
+  const bf16 *kp[2], *vp[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    srow[i] = (wave * 2 + i) * 4 + (lane >> 4);
+    const long key = kv_row0 + min(srow[i], kv_len - 1);
+    kp[i] = kbase + key * a.ks + ((r16 ^ (srow[i] & 15)) * 8);
+    vp[i] = vbase + key * a.vs + ((r16 ^ ((srow[i] & 7) << 1)) * 8);
+  }
+  auto stage = [&](int kb, int buf) {
+    char* base = smem + buf * STAGE_BYTES;
+    const bool full = kb * KVB + KVB <= kv_len;  // wave-uniform
+    const long ko = (long)kb * KVB * a.ks, vo = (long)kb * KVB * a.vs;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bf16 *ksrc = kp[i] + ko, *vsrc = vp[i] + vo;
+      if (!full) {
+        const long key = kv_row0 + min(kb * KVB + srow[i], kv_len - 1);
+        ksrc = kbase + key * a.ks + ((r16 ^ (srow[i] & 15)) * 8);
+        vsrc = vbase + key * a.vs + ((r16 ^ ((srow[i] & 7) << 1)) * 8);
+      }
+      __builtin_amdgcn_global_load_lds((const void*)ksrc, LDS_PTR(base + (wave * 2 + i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)vsrc, LDS_PTR(base + TILE_BYTES + (wave * 2 + i) * 1024), 16,
+                                       0, 0);
+    }
+  };
+
+  // per-lane LDS read bases (stage 0, key tile / chunk 0); the rest are +immediate
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
+  uint32_t ka[4], va[8];
+#pragma unroll
+  for (int dc = 0; dc < 4; ++dc) ka[dc] = lds0 + r16 * 256 + (((dc * 4 + g) ^ r16) << 4);
+  {
+    const int q = r16 >> 2, p = r16 & 3;
+    const int row = 4 * g + q;  // + 32 c (+16): same swizzle
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      const int ch = 2 * dt + (p >> 1);
+      va[dt] = lds0 + row * 256 + ((ch ^ ((row & 7) << 1)) << 4) + 8 * (p & 1);
+    }
+  }
+
+  V6State st;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) st.O[dt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  st.L[0] = st.L[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  st.negm[0] = st.negm[1] = 0.f;
+
+  const int nkb = (kv_len + KVB - 1) / KVB;
+  stage(0, 0);
+  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  for (int kb = 0; kb < nkb; kb += 2) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kb + 1 < nkb) stage(kb + 1, 1);
+    attn_v6_block<0>(st, qf, ka, va, kb, kv_len, g);
+    if (kb + 1 >= nkb) break;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kb + 2 < nkb) stage(kb + 2, 0);
+    attn_v6_block<1>(st, qf, ka, va, kb + 1, kv_len, g);
+  }
+
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const float inv = 1.0f / st.L[qt][0];
+    const int qi = qb * QB + wave * 32 + qt * 16 + r16;
+    if (qi < q_len) {
+      bf16* op = a.o + (long)(q_row0 + qi) * a.os + h * D + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        float v0 = st.O[dt][qt][0] * inv, v1 = st.O[dt][qt][1] * inv;
+        float v2 = st.O[dt][qt][2] * inv, v3 = st.O[dt][qt][3] * inv;
+        if (a.accumulate) {
+          const bf16x4 old = *(const bf16x4*)(op + dt * 16);
+          v0 += bf2f(old[0]); v1 += bf2f(old[1]); v2 += bf2f(old[2]); v3 += bf2f(old[3]);
+        }
+        *(bf16x4*)(op + dt * 16) = (bf16x4){f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
+      }
+    }
+  }
+}
+
 int g_attn_variant = -1;  // 0 = v1 (2-deep ring), 1 = v2 (3-deep ring, pipelined QK^T, deferred rescale),
                           // 2 = v1 + static priority, half-swap max, deferred rescale,
                           // 3 = v1 structure with asm LDS reads + counted waits (v3),
                           // 4 = v3 reads + two-group ping-pong (v4), 5 = v3 with prescaled Q and -m as
-                          // the QK^T initial accumulator
+                          // the QK^T initial accumulator, 6 = v5 on mfma_f32_16x16x32_bf16
 
 extern "C" int sa_attn_set_variant(int variant) {
-  if (variant < 0 || variant > 5) return SA_ERR_ARG;
+  if (variant < 0 || variant > 6) return SA_ERR_ARG;
   g_attn_variant = variant;
   return SA_OK;
 }
@@ -1226,6 +1513,8 @@ extern "C" int sa_attn_fwd(const void* q, const void* k, const void* v, void* o,
                               LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES_V2);
     attr = true;
@@ -1243,6 +1532,8 @@ extern "C" int sa_attn_fwd(const void* q, const void* k, const void* v, void* o,
     hipLaunchKernelGGL(attn_fwd_v3_kernel<true>, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
   else if (g_attn_variant == 4)
     hipLaunchKernelGGL(attn_fwd_v4_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+  else if (g_attn_variant == 6)
+    hipLaunchKernelGGL(attn_fwd_v6_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(attn_fwd_v2_kernel, grid, dim3(512), LDS_BYTES_V2, (hipStream_t)stream, a);
   SA_LAUNCH_CHECK();

@@ -77,12 +77,13 @@ def main(which=("gemm", "attn")):
         call("sa_gemm_set_variant", 4)
         call("sa_gemm_set_group_m", 0)
     if "attnvar" in which:
+        import os
         L, H, D = 21504, 12, 128
         qkv = torch.randn(3 * L, 3 * H * D, device=dev).bfloat16()
         segs = torch.tensor([[b * L, L, b * L, L] for b in range(3)], dtype=torch.int32, device=dev)
         q, k, v_ = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
         outs = {}
-        variants = (0, 3, 5)
+        variants = tuple(int(v) for v in os.environ.get("SA_KB_AVARS", "0,3,5").split(","))
         times = {v: [] for v in variants}
         for rnd in range(3):
             for v in variants:
@@ -94,12 +95,12 @@ def main(which=("gemm", "attn")):
         r = {"kernel": "attn_self"}
         for v in variants:
             ms = sorted(times[v])[1]
-            r[f"err_v{v}_v0"] = ((outs[v] - outs[0]).norm() / outs[0].norm()).item()
+            r[f"err_v{v}_v{variants[0]}"] = ((outs[v] - outs[variants[0]]).norm() / outs[variants[0]].norm()).item()
             r[f"v{v}_ms"] = round(ms, 3)
             r[f"v{v}_tflops"] = round(fl / ms / 1e9, 1)
         res.append(r)
         print(json.dumps(r), flush=True)
-        call("sa_attn_set_variant", 0)
+        call("sa_attn_set_variant", 5)
     if "gemm" in which:
         for (N, K, epi, name) in [(4608, 1536, ops.EPI_BF16, "qkv"), (1536, 1536, ops.EPI_RES_F32, "o_proj"),
                                   (8960, 1536, ops.EPI_GELU_TANH_BF16, "ffn_up"),
@@ -181,11 +182,17 @@ def main(which=("gemm", "attn")):
     if "dit" in which:
         res.append(bench_dit())
         print(json.dumps(res[-1]), flush=True)
+    if "ditvar" in which:  # in-situ A/B of attention variants inside full DiT forwards (interleaved)
+        import os
+        avars = tuple(int(v) for v in os.environ.get("SA_KB_AVARS", "5,6").split(","))
+        res.append(bench_dit(attn_variants=avars))
+        print(json.dumps(res[-1]), flush=True)
     return res
 
 
-def bench_dit(iters=3):
-    """One full 30-layer DiT forward at config 2 (B=3 CFG, 21 latent frames at 64x64, L=21504)."""
+def bench_dit(iters=3, attn_variants=None):
+    """One full 30-layer DiT forward at config 2 (B=3 CFG, 21 latent frames at 64x64, L=21504).
+    attn_variants: time the forward under each self-attention schedule, interleaved rounds."""
     from . import synthetic
     from .transformer import WanTransformer3DFantasyModel, param_shapes
     cfg = dict(model_type="i2v", dim=1536, ffn_dim=8960, freq_dim=256, text_dim=4096, in_dim=36, out_dim=16,
@@ -205,10 +212,23 @@ def bench_dit(iters=3):
     def fwd():
         return m.forward_window(lat, 0, True, 3, t, ctx, 21504, clip, y, voc, 81)
 
-    with torch.no_grad():
-        ms = _time(fwd, iters=iters, warmup=1)
     from .flops import dit_forward_flops
     fl = dit_forward_flops()
+    if attn_variants:
+        from ._lib import call
+        times = {v: [] for v in attn_variants}
+        with torch.no_grad():
+            for _ in range(3):
+                for v in attn_variants:
+                    call("sa_attn_set_variant", v)
+                    times[v].append(_time(fwd, iters=2, warmup=1))
+        call("sa_attn_set_variant", 5)
+        r = {"kernel": "dit_forward_attn_ab", "tflop": round(fl / 1e12, 1)}
+        for v in attn_variants:
+            r[f"attn_v{v}_ms"] = round(sorted(times[v])[1], 2)
+        return r
+    with torch.no_grad():
+        ms = _time(fwd, iters=iters, warmup=1)
     return {"kernel": "dit_forward", "ms": round(ms, 2), "tflop": round(fl / 1e12, 1),
             "tflops": round(fl / ms / 1e9, 1)}
 

@@ -99,8 +99,17 @@ def _ref_attn(q, k, v, scale):
     return torch.softmax(s, -1) @ v.float()
 
 
+@pytest.fixture(params=[5, 6], ids=["attn_v5", "attn_v6"])
+def attn_variant(request):
+    """run an attention test under each shipped schedule (5 = 32x32x16 MFMA, 6 = 16x16x32 MFMA)"""
+    from stableavatar_amd._lib import call
+    call("sa_attn_set_variant", request.param)
+    yield request.param
+    call("sa_attn_set_variant", 5)
+
+
 @pytest.mark.parametrize("Lq,Lk", [(300, 300), (512, 257), (1024, 17), (64, 512)])
-def test_attention_segments(Lq, Lk):
+def test_attention_segments(Lq, Lk, attn_variant):
     from stableavatar_amd import ops
     B, H, D = 2, 3, 128
     q = torch.randn(B * Lq, H * D + 64, device=dev).bfloat16()[:, :H * D]  # strided rows
@@ -120,7 +129,7 @@ def test_attention_segments(Lq, Lk):
     assert rel(o2, 2 * o.float()) < 1e-2
 
 
-def test_attention_vocal_grouping():
+def test_attention_vocal_grouping(attn_variant):
     """per-frame grouping of 1B:575-586: q rows of frame f attend to that frame's 17 keys"""
     from stableavatar_amd import ops
     B, F, G, Lv, H, D = 2, 3, 64, 17, 2, 128
@@ -137,7 +146,7 @@ def test_attention_vocal_grouping():
             assert rel(o[i * G:(i + 1) * G, sl], ref) < 1e-2
 
 
-def test_attention_spike_rescale():
+def test_attention_spike_rescale(attn_variant):
     """force the online-softmax rescale branch: a late key with a huge score"""
     from stableavatar_amd import ops
     L, D = 512, 128
