@@ -69,6 +69,9 @@ __device__ __forceinline__ void epi_row(const GemmArgs& g, float* v, long bz, in
   }
 #pragma unroll
   for (int j = 0; j < NC; ++j) {
+    // the reference's nn.Linear returns bf16 under autocast; GELU and the gated residual
+    // (1B:677-678,688-690) consume that rounded value
+    if (EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16 || EPI == EPI_RES_F32) v[j] = bf2f(f2bf(v[j]));
     if (EPI == EPI_GELU_BF16) v[j] = gelu_tanh(v[j]);
     if (EPI == EPI_GELU_ERF_BF16) v[j] = gelu_erf(v[j]);
     if (EPI == EPI_SILU_F32) v[j] = silu(v[j]);
@@ -505,6 +508,8 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             float t = acc[q][m][n][i] + bv[n][i];
+            if constexpr (EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16 || EPI == EPI_RES_F32)
+              t = bf2f(f2bf(t));  // bf16 Linear output, as epi_row
             if constexpr (EPI == EPI_SILU_F32) t = silu(t);
             if constexpr (EPI == EPI_GELU_BF16) t = gelu_tanh(t);
             if constexpr (EPI == EPI_GELU_ERF_BF16) t = gelu_erf(t);
