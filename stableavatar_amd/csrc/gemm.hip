@@ -1035,29 +1035,41 @@ __device__ __forceinline__ void s5_read(const S5Ctx& c, u32x4 (&a)[8], u32x4 (&b
 
 // one 64-MFMA half: MFMA row Q uses (ac[Q], bc[0..7]); the first 4 rows carry the reads of the
 // next fragments (stage RS, k half RK) and, when DMA, 4 DMA pieces each of tile ks into stage DS
-template <int RS, int RK, bool DMA, int DS>
+// DMA piece placement inside a half: packed (4 per MFMA row in rows 0-3) or SPREAD (2 per row, all 8)
+template <int DS, int Q, int POS, bool DMA, bool SPREAD>
+__device__ __forceinline__ void s5_dma_at(const S5Ctx& c, int ks) {
+  if constexpr (DMA) {
+    if constexpr (SPREAD) {
+      if constexpr (POS & 1) s5_dma<DS, 2 * Q + (POS >> 1)>(c, ks);
+    } else if constexpr (Q < 4) {
+      s5_dma<DS, 4 * Q + POS>(c, ks);
+    }
+  }
+}
+
+template <int RS, int RK, bool DMA, int DS, bool SPREAD = false>
 __device__ __forceinline__ void s5_half(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&ac)[8], u32x4 (&bc)[8],
                                         u32x4 (&an)[8], u32x4 (&bn)[8], int ks) {
 #define SA_S5_ROW(Q)                                                                        \
   {                                                                                         \
     s4_mma(acc[Q][0], bc[0], ac[Q]); s4_mma(acc[Q][1], bc[1], ac[Q]);                       \
     if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q>(c, an, bn); }                             \
-    if constexpr (DMA && Q < 4) { s5_dma<DS, 4 * Q>(c, ks); }                               \
+    s5_dma_at<DS, Q, 0, DMA, SPREAD>(c, ks);                               \
     s4_mma(acc[Q][2], bc[2], ac[Q]); s4_mma(acc[Q][3], bc[3], ac[Q]);                       \
     if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 1>(c, an, bn); }                         \
-    if constexpr (DMA && Q < 4) { s5_dma<DS, 4 * Q + 1>(c, ks); }                           \
+    s5_dma_at<DS, Q, 1, DMA, SPREAD>(c, ks);                           \
     s4_mma(acc[Q][4], bc[4], ac[Q]); s4_mma(acc[Q][5], bc[5], ac[Q]);                       \
     if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 2>(c, an, bn); }                         \
-    if constexpr (DMA && Q < 4) { s5_dma<DS, 4 * Q + 2>(c, ks); }                           \
+    s5_dma_at<DS, Q, 2, DMA, SPREAD>(c, ks);                           \
     s4_mma(acc[Q][6], bc[6], ac[Q]); s4_mma(acc[Q][7], bc[7], ac[Q]);                       \
     if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 3>(c, an, bn); }                         \
-    if constexpr (DMA && Q < 4) { s5_dma<DS, 4 * Q + 3>(c, ks); }                           \
+    s5_dma_at<DS, Q, 3, DMA, SPREAD>(c, ks);                           \
   }
   SA_S5_ROW(0) SA_S5_ROW(1) SA_S5_ROW(2) SA_S5_ROW(3) SA_S5_ROW(4) SA_S5_ROW(5) SA_S5_ROW(6) SA_S5_ROW(7)
 #undef SA_S5_ROW
 }
 
-template <int S>
+template <int S, bool SPREAD>
 __device__ __forceinline__ void s5_step(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8], u32x4 (&b0)[8],
                                         u32x4 (&a1)[8], u32x4 (&b1)[8], int t, int nk) {
   s4_wait_frags(a0, b0);
@@ -1065,10 +1077,10 @@ __device__ __forceinline__ void s5_step(const S5Ctx& c, f32x4 (&acc)[8][8], u32x
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   s4_wait_frags(a1, b1);
   __builtin_amdgcn_s_barrier();
-  s5_half<S ^ 1, 0, true, S>(c, acc, a1, b1, a0, b0, min(t + 2, nk - 1) * 128);
+  s5_half<S ^ 1, 0, true, S, SPREAD>(c, acc, a1, b1, a0, b0, min(t + 2, nk - 1) * 128);
 }
 
-template <int EPI>
+template <int EPI, bool SPREAD = false>
 __global__ __launch_bounds__(256, 1) void gemm_s5_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1131,8 +1143,8 @@ __global__ __launch_bounds__(256, 1) void gemm_s5_kernel(GemmArgs g) {
   s5_read<0, 0, 12>(c, a0, b0); s5_read<0, 0, 13>(c, a0, b0); s5_read<0, 0, 14>(c, a0, b0); s5_read<0, 0, 15>(c, a0, b0);
 
   for (int t = 0; t < nk; t += 2) {
-    s5_step<0>(c, acc, a0, b0, a1, b1, t, nk);
-    s5_step<1>(c, acc, a0, b0, a1, b1, t + 1, nk);
+    s5_step<0, SPREAD>(c, acc, a0, b0, a1, b1, t, nk);
+    s5_step<1, SPREAD>(c, acc, a0, b0, a1, b1, t + 1, nk);
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -1458,15 +1470,26 @@ int g_gemm_variant = -1;  // 0 = v1 (2-phase), 1 = phased (8 waves), 2 = w4 (4 w
                           // 3 = ping-pong 8-phase, 4 = ping-pong with direct (operand-swapped) epilogue,
                           // 5 = s4 (one wave per SIMD, buffer-DMA ring, scheduled interleave),
                           // 6-8 = s4 measurement ablations, 9 = s5 (s4 with 128-B rows, 2-stage ring),
-                          // 10 = s6 (s5 with register-staged loads), 11 = s7 (persistent s6)
+                          // 10 = s6 (s5 with register-staged loads), 11 = s7 (persistent s6),
+                          // 12-13 = s6 ablations, 14 = s5 with the DMA pieces spread over the half,
+                          // 15 = default: 14 for bf16 outputs, 4 for fp32 outputs
 
 template <int EPI>
-int launch(const GemmArgs& g, int batch, hipStream_t st) {
+int launch(const GemmArgs& g_in, int batch, hipStream_t st) {
   static int attr = 0;
   if (g_gemm_variant < 0) {
     const char* e = getenv("SA_GEMM_VARIANT");
-    g_gemm_variant = e ? atoi(e) : 4;
+    g_gemm_variant = e ? atoi(e) : 15;
   }
+  GemmArgs g = g_in;
+  // 15 = per-epilogue choice (measured, profiles/r01/gemm_ab_r4.md): bf16 outputs on the one-wave-per-
+  // SIMD LDS-DMA kernel with spread DMA (QKV +5 %, cross-Q +4 %, FFN-up +2 % over the ping-pong),
+  // fp32 / gated-residual outputs on the ping-pong kernel's direct epilogue
+  constexpr bool BF16_OUT = EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16;
+  const int variant = g_gemm_variant != 15 ? g_gemm_variant
+                      : (BF16_OUT && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
+                         (long)BN * g.ldw * 2 < 0x7fffffffL) ? 14 : 4;
+  if (g.group_m == 0) g.group_m = variant == 14 ? 4 : (g.N >= 4096 ? 8 : 1);
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_phased_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1474,6 +1497,8 @@ int launch(const GemmArgs& g, int batch, hipStream_t st) {
     (void)hipFuncSetAttribute((const void*)gemm_w4_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, W4_LDS);
     (void)hipFuncSetAttribute((const void*)gemm_s4_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S4_LDS);
     (void)hipFuncSetAttribute((const void*)gemm_s5_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S5_LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_s5_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              S5_LDS);
     (void)hipFuncSetAttribute((const void*)gemm_s6_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S5_LDS);
     (void)hipFuncSetAttribute((const void*)gemm_s7_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S7_LDS);
     (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1483,27 +1508,30 @@ int launch(const GemmArgs& g, int batch, hipStream_t st) {
     attr = 1;
   }
   const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
-  if (g_gemm_variant == 0)
+  if (variant == 0)
     hipLaunchKernelGGL(gemm_nt_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
-  else if (g_gemm_variant == 1)
+  else if (variant == 1)
     hipLaunchKernelGGL(gemm_phased_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
-  else if (g_gemm_variant == 2)
+  else if (variant == 2)
     hipLaunchKernelGGL(gemm_w4_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(256), W4_LDS, st, g);
-  else if (g_gemm_variant == 3) {
+  else if (variant == 3) {
     // fp32 outputs store straight from the (operand-swapped) accumulators; bf16 outputs go through
     // the LDS transpose for 16-B row stores
     constexpr bool F32_OUT = EPI == EPI_RES_F32 || EPI == EPI_F32 || EPI == EPI_SILU_F32;
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, F32_OUT>), dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
-  } else if (g_gemm_variant == 5 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
+  } else if (variant == 5 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
              (long)BN * g.ldw * 2 < 0x7fffffffL)
     hipLaunchKernelGGL(gemm_s4_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(256), S4_LDS, st, g);
-  else if (g_gemm_variant == 9 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
+  else if (variant == 9 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
            (long)BN * g.ldw * 2 < 0x7fffffffL)
     hipLaunchKernelGGL(gemm_s5_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(256), S5_LDS, st, g);
-  else if (g_gemm_variant == 10 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
+  else if (variant == 14 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
+           (long)BN * g.ldw * 2 < 0x7fffffffL)
+    hipLaunchKernelGGL((gemm_s5_kernel<EPI, true>), dim3(nm * nn, 1, batch), dim3(256), S5_LDS, st, g);
+  else if (variant == 10 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
            (long)BN * g.ldw * 2 < 0x7fffffffL)
     hipLaunchKernelGGL(gemm_s6_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(256), S5_LDS, st, g);
-  else if (g_gemm_variant == 11 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
+  else if (variant == 11 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
            (long)BN * g.ldw * 2 < 0x7fffffffL) {
     if (!g_num_cus) {
       int dev = 0;
@@ -1513,18 +1541,18 @@ int launch(const GemmArgs& g, int batch, hipStream_t st) {
     }
     const int total = nm * nn * batch;
     hipLaunchKernelGGL(gemm_s7_kernel<EPI>, dim3(min(total, g_num_cus)), dim3(256), S7_LDS, st, g, batch);
-  } else if ((g_gemm_variant == 12 || g_gemm_variant == 13) && EPI == EPI_BF16 && g.K % 128 == 0) {
+  } else if ((variant == 12 || variant == 13) && EPI == EPI_BF16 && g.K % 128 == 0) {
     static int attr6 = 0;
     if (!attr6) {
       (void)hipFuncSetAttribute((const void*)gemm_s6_kernel<EPI, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S5_LDS);
       (void)hipFuncSetAttribute((const void*)gemm_s6_kernel<EPI, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, S5_LDS);
       attr6 = 1;
     }
-    if (g_gemm_variant == 12)
+    if (variant == 12)
       hipLaunchKernelGGL((gemm_s6_kernel<EPI, 1>), dim3(nm * nn, 1, batch), dim3(256), S5_LDS, st, g);
     else
       hipLaunchKernelGGL((gemm_s6_kernel<EPI, 2>), dim3(nm * nn, 1, batch), dim3(256), S5_LDS, st, g);
-  } else if (g_gemm_variant >= 6 && g_gemm_variant <= 8 && EPI == EPI_BF16 && g.K % 128 == 0) {
+  } else if (variant >= 6 && variant <= 8 && EPI == EPI_BF16 && g.K % 128 == 0) {
     static int attr_abl = 0;
     if (!attr_abl) {
       (void)hipFuncSetAttribute((const void*)gemm_s4_kernel<EPI, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S4_LDS);
@@ -1532,9 +1560,9 @@ int launch(const GemmArgs& g, int batch, hipStream_t st) {
       (void)hipFuncSetAttribute((const void*)gemm_s4_kernel<EPI, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, S4_LDS);
       attr_abl = 1;
     }
-    if (g_gemm_variant == 6)
+    if (variant == 6)
       hipLaunchKernelGGL((gemm_s4_kernel<EPI, 1>), dim3(nm * nn, 1, batch), dim3(256), S4_LDS, st, g);
-    else if (g_gemm_variant == 7)
+    else if (variant == 7)
       hipLaunchKernelGGL((gemm_s4_kernel<EPI, 2>), dim3(nm * nn, 1, batch), dim3(256), S4_LDS, st, g);
     else
       hipLaunchKernelGGL((gemm_s4_kernel<EPI, 3>), dim3(nm * nn, 1, batch), dim3(256), S4_LDS, st, g);
@@ -1554,7 +1582,7 @@ extern "C" int sa_gemm_set_group_m(int gm) {
 }
 
 extern "C" int sa_gemm_set_variant(int variant) {
-  if (variant < 0 || variant > 13) return SA_ERR_ARG;
+  if (variant < 0 || variant > 15) return SA_ERR_ARG;
   g_gemm_variant = variant;
   return SA_OK;
 }
@@ -1573,9 +1601,9 @@ extern "C" int sa_gemm_bf16(const void* A, int64_t lda, int64_t strideA, const v
     group_m_env = e ? atoi(e) : 0;
     if (group_m_env < 0) group_m_env = 0;
   }
-  // measured (kbench gemmvar, 64512-row DiT GEMMs): runs of 8 tile rows help the wide-N GEMMs
-  // (QKV +2.3 %, FFN-up +2.8 %, 8192^3 +5 %) and cost the N = 1536 ones up to 2.7 %
-  const int group_m = group_m_env ? group_m_env : (N >= 4096 ? 8 : 1);
+  // 0 = chosen per kernel in launch(): ping-pong runs of 8 tile rows for N >= 4096 (QKV +2.3 %, FFN-up
+  // +2.8 %; the N = 1536 ones lose up to 2.7 %), LDS-DMA kernel runs of 4
+  const int group_m = group_m_env;
   GemmArgs g{(const bf16*)A, lda, strideA, (const bf16*)W, ldw, strideW, bias, C, ldc, strideC,
              residual, ldr, strideR, gate, gate_bstride, rows_per_batch > 0 ? rows_per_batch : 1, M, N, K,
              g_group_m_override > 0 ? g_group_m_override : group_m};

@@ -34,6 +34,7 @@ def main(which=("gemm", "attn")):
         # variant spec "V" or "V:G" (G = tile-raster group_m)
         gvars = tuple(os.environ.get("SA_KB_GVARS", "3,4").split(","))
         for (Mx, N, K, epi, name) in [(M, 4608, 1536, ops.EPI_BF16, "qkv"), (M, 1536, 1536, ops.EPI_RES_F32, "o_proj"),
+                                      (M, 1536, 1536, ops.EPI_BF16, "cross_q"),
                                       (M, 8960, 1536, ops.EPI_GELU_TANH_BF16, "ffn_up"),
                                       (M, 1536, 8960, ops.EPI_RES_F32, "ffn_down"),
                                       (8192, 8192, 8192, ops.EPI_BF16, "sq8192")]:
@@ -74,7 +75,7 @@ def main(which=("gemm", "attn")):
             res.append(r)
             print(json.dumps(r), flush=True)
             del x, w, out
-        call("sa_gemm_set_variant", 4)
+        call("sa_gemm_set_variant", 15)
         call("sa_gemm_set_group_m", 0)
     if "attnvar" in which:
         import os
