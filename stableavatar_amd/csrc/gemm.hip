@@ -1464,6 +1464,118 @@ __global__ __launch_bounds__(256, 1) void gemm_s7_kernel(GemmArgs g, int batch) 
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 
+// ------------------------------------------------------------------------------------------------
+// s8 kernel: s7's persistence (tile walk u = blockIdx.x + k*gridDim.x, K pipeline running across tile
+// seams, epilogue from a private strip above the ring) on the spread-DMA feed of variant 14: in the
+// last two K steps of a tile the DMA fetches K-tiles 0 and 1 of the next tile and the last step's
+// fragment reads take its first fragments, so a tile starts with no prologue.
+template <int S>
+__device__ __forceinline__ void s8_step(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8], u32x4 (&b0)[8],
+                                        u32x4 (&a1)[8], u32x4 (&b1)[8], int ks) {
+  s4_wait_frags(a0, b0);
+  s5_half<S, 1, false, 0>(c, acc, a0, b0, a1, b1, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  s4_wait_frags(a1, b1);
+  __builtin_amdgcn_s_barrier();
+  s5_half<S ^ 1, 0, true, S, true>(c, acc, a1, b1, a0, b0, ks);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
+  const int total = nm * nn * batch, G = gridDim.x;
+  int u = blockIdx.x;
+  S5Ctx c;
+  int m0, n0;
+  long bz;
+  s7_tile(g, u, total, G, nm, nn, m0, n0, bz, c.ra, c.rw);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = (i * 4 + wave) * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    c.aoff[i] = row * (int)g.lda * 2 + chunk * 16;
+    c.woff[i] = row * (int)g.ldw * 2 + chunk * 16;
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
+  c.lds_dma = __builtin_amdgcn_readfirstlane(lds0 + wave * 1024);
+  const int fr = lane & 15, fc = lane >> 4;
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      const int sw = ((4 * kh + fc) ^ ((fr >> 1) & 7)) << 4;
+      c.ard[st][kh] = lds0 + st * S5_STAGE + (wm * 128 + fr) * 128 + sw;
+      c.wrd[st][kh] = lds0 + st * S5_STAGE + 256 * 128 + (wn * 128 + fr) * 128 + sw;
+    }
+  const int nk = g.K / 64;  // even (launcher: K % 128 == 0)
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  u32x4 a0[8], b0[8], a1[8], b1[8];
+#define SA_S8_DMA_ALL(STAGE, T)                                                                       \
+  {                                                                                                   \
+    const int ks = (T) * 128;                                                                         \
+    s5_dma<STAGE, 0>(c, ks); s5_dma<STAGE, 1>(c, ks); s5_dma<STAGE, 2>(c, ks); s5_dma<STAGE, 3>(c, ks);     \
+    s5_dma<STAGE, 4>(c, ks); s5_dma<STAGE, 5>(c, ks); s5_dma<STAGE, 6>(c, ks); s5_dma<STAGE, 7>(c, ks);     \
+    s5_dma<STAGE, 8>(c, ks); s5_dma<STAGE, 9>(c, ks); s5_dma<STAGE, 10>(c, ks); s5_dma<STAGE, 11>(c, ks);   \
+    s5_dma<STAGE, 12>(c, ks); s5_dma<STAGE, 13>(c, ks); s5_dma<STAGE, 14>(c, ks); s5_dma<STAGE, 15>(c, ks); \
+  }
+  SA_S8_DMA_ALL(0, 0)
+  SA_S8_DMA_ALL(1, 1)
+#undef SA_S8_DMA_ALL
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  s5_read<0, 0, 0>(c, a0, b0); s5_read<0, 0, 1>(c, a0, b0); s5_read<0, 0, 2>(c, a0, b0); s5_read<0, 0, 3>(c, a0, b0);
+  s5_read<0, 0, 4>(c, a0, b0); s5_read<0, 0, 5>(c, a0, b0); s5_read<0, 0, 6>(c, a0, b0); s5_read<0, 0, 7>(c, a0, b0);
+  s5_read<0, 0, 8>(c, a0, b0); s5_read<0, 0, 9>(c, a0, b0); s5_read<0, 0, 10>(c, a0, b0); s5_read<0, 0, 11>(c, a0, b0);
+  s5_read<0, 0, 12>(c, a0, b0); s5_read<0, 0, 13>(c, a0, b0); s5_read<0, 0, 14>(c, a0, b0); s5_read<0, 0, 15>(c, a0, b0);
+
+  while (true) {
+    const int un = u + G;
+    const bool has_next = un < total;
+    __amdgpu_buffer_rsrc_t cra = c.ra, crw = c.rw, nra = c.ra, nrw = c.rw;
+    int nm0 = m0, nn0 = n0;
+    long nbz = bz;
+    if (has_next) s7_tile(g, un, total, G, nm, nn, nm0, nn0, nbz, nra, nrw);
+    for (int t = 0; t < nk; t += 2) {
+      {
+        const bool nx = t + 2 >= nk;  // DMA of the next tile's K-tile t+2-nk (or a re-read of the last)
+        c.ra = nx ? nra : cra;
+        c.rw = nx ? nrw : crw;
+        s8_step<0>(c, acc, a0, b0, a1, b1, (nx ? (has_next ? t + 2 - nk : nk - 1) : t + 2) * 128);
+      }
+      {
+        const bool nx = t + 3 >= nk;
+        c.ra = nx ? nra : cra;
+        c.rw = nx ? nrw : crw;
+        s8_step<1>(c, acc, a0, b0, a1, b1, (nx ? (has_next ? t + 3 - nk : nk - 1) : t + 3) * 128);
+      }
+    }
+    asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // MFMA -> v_accvgpr_read
+    s7_epilogue<EPI>(g, acc, smem, wave, lane, m0, n0, bz);
+    if (!has_next) break;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    u = un;
+    m0 = nm0;
+    n0 = nn0;
+    bz = nbz;
+    c.ra = nra;
+    c.rw = nrw;
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
 int g_num_cus = 0;
 
 int g_gemm_variant = -1;  // 0 = v1 (2-phase), 1 = phased (8 waves), 2 = w4 (4 waves, AGPR accumulators),
@@ -1472,7 +1584,7 @@ int g_gemm_variant = -1;  // 0 = v1 (2-phase), 1 = phased (8 waves), 2 = w4 (4 w
                           // 6-8 = s4 measurement ablations, 9 = s5 (s4 with 128-B rows, 2-stage ring),
                           // 10 = s6 (s5 with register-staged loads), 11 = s7 (persistent s6),
                           // 12-13 = s6 ablations, 14 = s5 with the DMA pieces spread over the half,
-                          // 15 = default: 14 for bf16 outputs, 4 for fp32 outputs
+                          // 15 = default: 16 for bf16 outputs, 4 for fp32 outputs, 16 = s8 (persistent 14)
 
 template <int EPI>
 int launch(const GemmArgs& g_in, int batch, hipStream_t st) {
@@ -1482,14 +1594,14 @@ int launch(const GemmArgs& g_in, int batch, hipStream_t st) {
     g_gemm_variant = e ? atoi(e) : 15;
   }
   GemmArgs g = g_in;
-  // 15 = per-epilogue choice (measured, profiles/r01/gemm_ab_r4.md): bf16 outputs on the one-wave-per-
-  // SIMD LDS-DMA kernel with spread DMA (QKV +5 %, cross-Q +4 %, FFN-up +2 % over the ping-pong),
+  // 15 = per-epilogue choice (measured, profiles/r01/gemm_ab_r4.md): bf16 outputs on the persistent
+  // one-wave-per-SIMD LDS-DMA kernel (QKV +8-15 %, cross-Q +7-10 %, FFN-up +3-4 % over the ping-pong),
   // fp32 / gated-residual outputs on the ping-pong kernel's direct epilogue
   constexpr bool BF16_OUT = EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16;
   const int variant = g_gemm_variant != 15 ? g_gemm_variant
                       : (BF16_OUT && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
-                         (long)BN * g.ldw * 2 < 0x7fffffffL) ? 14 : 4;
-  if (g.group_m == 0) g.group_m = variant == 14 ? 4 : (g.N >= 4096 ? 8 : 1);
+                         (long)BN * g.ldw * 2 < 0x7fffffffL) ? 16 : 4;
+  if (g.group_m == 0) g.group_m = variant == 14 ? 4 : variant == 16 ? 8 : (g.N >= 4096 ? 8 : 1);
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_phased_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1501,6 +1613,7 @@ int launch(const GemmArgs& g_in, int batch, hipStream_t st) {
                               S5_LDS);
     (void)hipFuncSetAttribute((const void*)gemm_s6_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S5_LDS);
     (void)hipFuncSetAttribute((const void*)gemm_s7_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S7_LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S7_LDS);
     (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1525,7 +1638,16 @@ int launch(const GemmArgs& g_in, int batch, hipStream_t st) {
   else if (variant == 9 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
            (long)BN * g.ldw * 2 < 0x7fffffffL)
     hipLaunchKernelGGL(gemm_s5_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(256), S5_LDS, st, g);
-  else if (variant == 14 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
+  else if (variant == 16 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
+           (long)BN * g.ldw * 2 < 0x7fffffffL) {
+    if (!g_num_cus) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_num_cus <= 0)
+        g_num_cus = 256;
+    }
+    hipLaunchKernelGGL(gemm_s8_kernel<EPI>, dim3(min(nm * nn * batch, g_num_cus)), dim3(256), S7_LDS, st, g, batch);
+  } else if (variant == 14 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
            (long)BN * g.ldw * 2 < 0x7fffffffL)
     hipLaunchKernelGGL((gemm_s5_kernel<EPI, true>), dim3(nm * nn, 1, batch), dim3(256), S5_LDS, st, g);
   else if (variant == 10 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
@@ -1582,7 +1704,7 @@ extern "C" int sa_gemm_set_group_m(int gm) {
 }
 
 extern "C" int sa_gemm_set_variant(int variant) {
-  if (variant < 0 || variant > 15) return SA_ERR_ARG;
+  if (variant < 0 || variant > 16) return SA_ERR_ARG;
   g_gemm_variant = variant;
   return SA_OK;
 }

@@ -50,7 +50,7 @@ def test_gemm_epilogues(M, N, K):
     assert rel(out, res + ref.bfloat16().float() * g_rows) < 2e-3
 
 
-@pytest.mark.parametrize("variant", [3, 4, 5, 9, 10, 11, 14, 15])
+@pytest.mark.parametrize("variant", [3, 4, 5, 9, 10, 11, 14, 15, 16])
 @pytest.mark.parametrize("M,N,K", [(300, 520, 256), (257, 130, 128), (1000, 1536, 1536), (600, 300, 2304)])
 def test_gemm_variants(variant, M, N, K):
     """Every GEMM schedule (sa_gemm_set_variant) on ragged M/N tiles, every epilogue, vs torch fp32."""
