@@ -40,12 +40,12 @@ int sa_gemm_bf16(const void* A, int64_t lda, int64_t strideA, const void* W, int
  * SA_ATTN_VARIANT).  gemm: 0 = 2-phase 8-wave, 1 = 4-phase 8-wave, 2 = 4-wave AGPR, 3 = 8-phase
  * ping-pong, 4 = ping-pong with operand-swapped direct epilogue, 5 = one wave per SIMD with a 32-deep
  * LDS-DMA ring, 9 = same with 64-deep K-tiles, 10 = register-staged, 11 = persistent register-staged,
- * 14 = 9 with spread DMA, 16 = persistent 14, 15 = 16 for bf16 outputs and 4 for fp32 outputs
- * (default); 6-8, 12-13 are
+ * 14 = 9 with spread DMA, 16 = persistent 14, 15 = 16 where K % 128 == 0 else 4 (default);
+ * 6-8, 12-13 are
  * measurement ablations (wrong results by construction).  attention: 0 = 2-deep ring, 1 = 3-deep ring
  * with pipelined QK^T, 2 = 0 + deferred rescale, 3 = asm LDS reads with counted waits + XCD order,
- * 4 = 3 + two-group ping-pong, 5 = 3 with prescaled Q and -m as the QK^T accumulator (default),
- * 6 = 5 on mfma_f32_16x16x32_bf16. */
+ * 4 = 3 + two-group ping-pong, 5 = 3 with prescaled Q and -m as the QK^T accumulator,
+ * 6 = 5 on mfma_f32_16x16x32_bf16 (default). */
 int sa_gemm_set_variant(int variant);
 int sa_attn_set_variant(int variant);
 /* GEMM tile raster: runs of group_m tile rows walked column-major (0 = env SA_GEMM_GROUP_M / default). */

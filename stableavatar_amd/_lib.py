@@ -55,6 +55,10 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    # torch first: its wheel bundles libamdhip64.so.7; if this library were dlopened before torch, the
+    # soname would bind to /opt/rocm's copy and torch would then map a second HIP runtime, whose
+    # streams and allocations ours cannot use (launches fail with hipErrorNoDevice)
+    import torch  # noqa: F401
     if not LIB_PATH.exists():
         raise RuntimeError(f"libstableavatar_hip.so not built ({LIB_PATH}); run __graft_entry__.build()")
     L = ctypes.CDLL(str(LIB_PATH))

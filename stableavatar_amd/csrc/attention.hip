@@ -699,21 +699,30 @@ __global__ __launch_bounds__(512) void attn_fwd_v3_kernel(AttnArgs a) {
 
   const float lt = st.l_run + __shfl_xor(st.l_run, 32, 64);
   const float inv = 1.0f / lt;
-  if (qi < q_len) {
-    bf16* op = a.o + (long)(q_row0 + qi) * a.os + h * D;
+  // lanes q and q+32 hold alternating 4-column groups k (columns 8k..8k+3 / 8k+4..8k+7) of one query
+  // row; one permlane32 swap per dword pairs groups (k, k+1) so every lane stores 16 contiguous bytes
+  // (cdna_hip_programming.md T21: 8 dwordx4 stores instead of 16 dwordx2)
+  bf16* op = a.o + (long)(q_row0 + min(qi, q_len - 1)) * a.os + h * D + 8 * hi;
 #pragma unroll
-    for (int db = 0; db < 4; ++db)
+  for (int k = 0; k < 16; k += 2) {
+    const f32x16& Oa = st.O[k >> 2];
+    const f32x16& Ob = st.O[(k + 1) >> 2];
+    const int ia = 4 * (k & 3), ib = 4 * ((k + 1) & 3);
+    const bf16x4 pa = {f2bf(Oa[ia] * inv), f2bf(Oa[ia + 1] * inv), f2bf(Oa[ia + 2] * inv), f2bf(Oa[ia + 3] * inv)};
+    const bf16x4 pb = {f2bf(Ob[ib] * inv), f2bf(Ob[ib + 1] * inv), f2bf(Ob[ib + 2] * inv), f2bf(Ob[ib + 3] * inv)};
+    const u32x2 ga = __builtin_bit_cast(u32x2, pa), gb = __builtin_bit_cast(u32x2, pb);
+    const auto rx = __builtin_amdgcn_permlane32_swap(ga[0], gb[0], false, false);
+    const auto ry = __builtin_amdgcn_permlane32_swap(ga[1], gb[1], false, false);
+    u32x4 out = {rx[0], ry[0], rx[1], ry[1]};
+    bf16* p = op + 8 * k;
+    if (a.accumulate) {  // bf16 + bf16 as the reference's sum of attention outputs (1B:602)
+      const bf16x8 ov = *(const bf16x8*)p;
+      bf16x8 nv = __builtin_bit_cast(bf16x8, out);
 #pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {
-        const int d0 = db * 32 + 8 * r4 + 4 * hi;
-        float v0 = st.O[db][4 * r4 + 0] * inv, v1 = st.O[db][4 * r4 + 1] * inv;
-        float v2 = st.O[db][4 * r4 + 2] * inv, v3 = st.O[db][4 * r4 + 3] * inv;
-        if (a.accumulate) {
-          const bf16x4 old = *(const bf16x4*)(op + d0);
-          v0 += bf2f(old[0]); v1 += bf2f(old[1]); v2 += bf2f(old[2]); v3 += bf2f(old[3]);
-        }
-        *(bf16x4*)(op + d0) = (bf16x4){f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
-      }
+      for (int j = 0; j < 8; ++j) nv[j] = f2bf(bf2f(ov[j]) + bf2f(nv[j]));
+      out = __builtin_bit_cast(u32x4, nv);
+    }
+    if (qi < q_len) *(u32x4*)p = out;
   }
 }
 
@@ -1113,16 +1122,15 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
     }
   }
 
-  if (qi < a.q_len) {
-    bf16* op = a.o + (long)(q_row0 + qi) * a.os + h * D;
+  // 16-byte stores from permlane32-swapped column-group pairs, as the self-attention epilogue (T21)
+  bf16* op = a.o + (long)(q_row0 + min(qi, a.q_len - 1)) * a.os + h * D + 8 * hi;
 #pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {
-        const int d0 = db * 32 + 8 * r4 + 4 * hi;
-        const bf16x2 lo = acc[db * 8 + 2 * r4], hv = acc[db * 8 + 2 * r4 + 1];
-        *(bf16x4*)(op + d0) = (bf16x4){lo[0], lo[1], hv[0], hv[1]};
-      }
+  for (int k = 0; k < 16; k += 2) {
+    const uint32_t a0 = __builtin_bit_cast(uint32_t, acc[2 * k]), a1 = __builtin_bit_cast(uint32_t, acc[2 * k + 1]);
+    const uint32_t b0 = __builtin_bit_cast(uint32_t, acc[2 * k + 2]), b1 = __builtin_bit_cast(uint32_t, acc[2 * k + 3]);
+    const auto rx = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+    const auto ry = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+    if (qi < a.q_len) *(u32x4*)(op + 8 * k) = (u32x4){rx[0], ry[0], rx[1], ry[1]};
   }
 }
 
@@ -1458,22 +1466,32 @@ __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) {
     attn_v6_block<1>(st, qf, ka, va, kb + 1, kv_len, g);
   }
 
+  // lane rows g and g^1 (lanes l, l^16) hold adjacent 4-column groups of one query row: one
+  // permlane16 swap per dword pairs d tiles (dt, dt+1) so each lane stores 16 contiguous bytes (T21)
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const float inv = 1.0f / st.L[qt][0];
     const int qi = qb * QB + wave * 32 + qt * 16 + r16;
-    if (qi < q_len) {
-      bf16* op = a.o + (long)(q_row0 + qi) * a.os + h * D + 4 * g;
+    bf16* op = a.o + (long)(q_row0 + min(qi, q_len - 1)) * a.os + h * D + 4 * (g & ~1) + 16 * (g & 1);
 #pragma unroll
-      for (int dt = 0; dt < 8; ++dt) {
-        float v0 = st.O[dt][qt][0] * inv, v1 = st.O[dt][qt][1] * inv;
-        float v2 = st.O[dt][qt][2] * inv, v3 = st.O[dt][qt][3] * inv;
-        if (a.accumulate) {
-          const bf16x4 old = *(const bf16x4*)(op + dt * 16);
-          v0 += bf2f(old[0]); v1 += bf2f(old[1]); v2 += bf2f(old[2]); v3 += bf2f(old[3]);
-        }
-        *(bf16x4*)(op + dt * 16) = (bf16x4){f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
+    for (int dt = 0; dt < 8; dt += 2) {
+      const f32x4& A = st.O[dt][qt];
+      const f32x4& B = st.O[dt + 1][qt];
+      const bf16x4 pa = {f2bf(A[0] * inv), f2bf(A[1] * inv), f2bf(A[2] * inv), f2bf(A[3] * inv)};
+      const bf16x4 pb = {f2bf(B[0] * inv), f2bf(B[1] * inv), f2bf(B[2] * inv), f2bf(B[3] * inv)};
+      const u32x2 ga = __builtin_bit_cast(u32x2, pa), gb = __builtin_bit_cast(u32x2, pb);
+      const auto rx = __builtin_amdgcn_permlane16_swap(ga[0], gb[0], false, false);
+      const auto ry = __builtin_amdgcn_permlane16_swap(ga[1], gb[1], false, false);
+      u32x4 out = {rx[0], ry[0], rx[1], ry[1]};
+      bf16* p = op + dt * 16;
+      if (a.accumulate) {  // bf16 + bf16 as the reference's sum of attention outputs (1B:602)
+        const bf16x8 ov = *(const bf16x8*)p;
+        bf16x8 nv = __builtin_bit_cast(bf16x8, out);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) nv[j] = f2bf(bf2f(ov[j]) + bf2f(nv[j]));
+        out = __builtin_bit_cast(u32x4, nv);
       }
+      if (qi < q_len) *(u32x4*)p = out;
     }
   }
 }
@@ -1500,7 +1518,7 @@ extern "C" int sa_attn_fwd(const void* q, const void* k, const void* v, void* o,
   static bool attr = false;
   if (g_attn_variant < 0) {
     const char* e = getenv("SA_ATTN_VARIANT");
-    g_attn_variant = e ? atoi(e) : 5;
+    g_attn_variant = e ? atoi(e) : 6;
   }
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -1312,12 +1312,76 @@ __device__ __forceinline__ void s7_step(const S5Ctx& c, f32x4 (&acc)[8][8], u32x
 constexpr int S7_STRIP = 16 * 68 * 4;             // [16 rows][64 (+4) cols] fp32 per wave
 constexpr int S7_LDS = S5_LDS + 4 * S7_STRIP;     // 145 KB
 
+// gated-residual epilogue of an interior tile: the residual / gate rows of the 16 (row block, column
+// half) steps are loaded S7_RES_AHEAD steps ahead (the fragment registers are dead here), bias once per
+// column half, so the residual's HBM latency is paid about once per tile instead of once per step
+constexpr int S7_RES_AHEAD = 2;
+__device__ __forceinline__ void s7_res_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8], float* strip, int wm, int wn,
+                                                int fr, int fc, int er, int ec, int m0, int n0, long bz) {
+  f32x4 bias_h[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      bias_h[h][q] = g.bias ? *(const f32x4*)(g.bias + n0 + wn * 128 + h * 64 + ec + 4 * q) : (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 rb[S7_RES_AHEAD][4], gb[S7_RES_AHEAD][4];
+  auto fetch = [&](int k, int slot) {
+    const int i = k >> 1, h = k & 1;
+    const int row = m0 + wm * 128 + i * 16 + er;
+    const int col = n0 + wn * 128 + h * 64 + ec;
+    const float* R = g.R + bz * g.sR + (long)row * g.ldr + col;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rb[slot][q] = *(const f32x4*)(R + 4 * q);
+    if (g.gate) {
+      const float* G = g.gate + (long)(row / g.rows_per_batch) * g.gate_bstride + col;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) gb[slot][q] = *(const f32x4*)(G + 4 * q);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) gb[slot][q] = (f32x4){1.f, 1.f, 1.f, 1.f};
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < S7_RES_AHEAD; ++k) fetch(k, k);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int i = k >> 1, h = k & 1, slot = k % S7_RES_AHEAD;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *(f32x4*)(strip + fr * 68 + j * 16 + fc * 4) = acc[i][4 * h + j];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    f32x4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = *(const f32x4*)(strip + er * 68 + ec + q * 4);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    float* C = (float*)g.C + bz * g.sC + (long)(m0 + wm * 128 + i * 16 + er) * g.ldc + n0 + wn * 128 + h * 64 + ec;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float t = bf2f(f2bf(v[q][e] + bias_h[h][q][e]));  // bf16 Linear output (reference autocast)
+        o[e] = rb[slot][q][e] + t * gb[slot][q][e];
+      }
+      *(f32x4*)(C + 4 * q) = o;
+    }
+    if (k + S7_RES_AHEAD < 16) fetch(k + S7_RES_AHEAD, slot);
+  }
+}
+
 template <int EPI>
 __device__ __forceinline__ void s7_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8], char* smem, int wave, int lane,
                                             int m0, int n0, long bz) {
   const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fc = lane >> 4;
   float* strip = (float*)(smem + S5_LDS + wave * S7_STRIP);
   const int er = lane >> 2, ec = (lane & 3) * 16;
+  if constexpr (EPI == EPI_RES_F32) {
+    if (m0 + BM <= g.M && n0 + BN <= g.N) {  // wave-uniform
+      s7_res_epilogue(g, acc, strip, wm, wn, fr, fc, er, ec, m0, n0, bz);
+      return;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int grow = m0 + wm * 128 + i * 16 + er;
@@ -1584,7 +1648,7 @@ int g_gemm_variant = -1;  // 0 = v1 (2-phase), 1 = phased (8 waves), 2 = w4 (4 w
                           // 6-8 = s4 measurement ablations, 9 = s5 (s4 with 128-B rows, 2-stage ring),
                           // 10 = s6 (s5 with register-staged loads), 11 = s7 (persistent s6),
                           // 12-13 = s6 ablations, 14 = s5 with the DMA pieces spread over the half,
-                          // 15 = default: 16 for bf16 outputs, 4 for fp32 outputs, 16 = s8 (persistent 14)
+                          // 15 = default: 16 where K % 128 == 0, else 4; 16 = s8 (persistent 14)
 
 template <int EPI>
 int launch(const GemmArgs& g_in, int batch, hipStream_t st) {
@@ -1594,14 +1658,16 @@ int launch(const GemmArgs& g_in, int batch, hipStream_t st) {
     g_gemm_variant = e ? atoi(e) : 15;
   }
   GemmArgs g = g_in;
-  // 15 = per-epilogue choice (measured, profiles/r01/gemm_ab_r4.md): bf16 outputs on the persistent
-  // one-wave-per-SIMD LDS-DMA kernel (QKV +8-15 %, cross-Q +7-10 %, FFN-up +3-4 % over the ping-pong),
-  // fp32 / gated-residual outputs on the ping-pong kernel's direct epilogue
+  // 15 = default (measured, profiles/r01/gemm_ab_r4.md): the persistent one-wave-per-SIMD LDS-DMA
+  // kernel wherever its K % 128 tiling applies (over the ping-pong: QKV +8-15 %, cross-Q +7-10 %,
+  // FFN-up +3-4 %, FFN-down with the prefetched residual epilogue +4 %, O-proj +-1 %), else the
+  // ping-pong kernel (e.g. the K = 192 patch embedding)
   constexpr bool BF16_OUT = EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16;
   const int variant = g_gemm_variant != 15 ? g_gemm_variant
-                      : (BF16_OUT && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
+                      : (g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
                          (long)BN * g.ldw * 2 < 0x7fffffffL) ? 16 : 4;
-  if (g.group_m == 0) g.group_m = variant == 14 ? 4 : variant == 16 ? 8 : (g.N >= 4096 ? 8 : 1);
+  if (g.group_m == 0)
+    g.group_m = variant == 14 ? 4 : variant == 16 ? (BF16_OUT ? 8 : 4) : (g.N >= 4096 ? 8 : 1);
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_phased_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -101,7 +101,7 @@ def main(which=("gemm", "attn")):
             r[f"v{v}_tflops"] = round(fl / ms / 1e9, 1)
         res.append(r)
         print(json.dumps(r), flush=True)
-        call("sa_attn_set_variant", 5)
+        call("sa_attn_set_variant", 6)
     if "gemm" in which:
         for (N, K, epi, name) in [(4608, 1536, ops.EPI_BF16, "qkv"), (1536, 1536, ops.EPI_RES_F32, "o_proj"),
                                   (8960, 1536, ops.EPI_GELU_TANH_BF16, "ffn_up"),
@@ -223,7 +223,7 @@ def bench_dit(iters=3, attn_variants=None):
                 for v in attn_variants:
                     call("sa_attn_set_variant", v)
                     times[v].append(_time(fwd, iters=2, warmup=1))
-        call("sa_attn_set_variant", 5)
+        call("sa_attn_set_variant", 6)
         r = {"kernel": "dit_forward_attn_ab", "tflop": round(fl / 1e12, 1)}
         for v in attn_variants:
             r[f"attn_v{v}_ms"] = round(sorted(times[v])[1], 2)

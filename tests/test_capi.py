@@ -1,6 +1,5 @@
 """C-ABI checks that need no GPU: the library builds/loads, exports every symbol declared in
 include/stableavatar_hip.h, and the ctypes signatures match the header's parameter lists."""
-import ctypes
 import re
 import subprocess
 
@@ -46,7 +45,7 @@ def test_library_exports_every_symbol():
     exported = set(re.findall(r"\bT (sa_\w+)", nm))
     missing = set(_lib.header_symbols()) - exported
     assert not missing, missing
-    L = ctypes.CDLL(str(_lib.LIB_PATH))
+    L = _lib.lib()  # torch's HIP runtime first, then the library (see _lib.lib)
     for name in _lib.header_symbols():
         assert getattr(L, name) is not None
 

@@ -106,7 +106,7 @@ def attn_variant(request):
     from stableavatar_amd._lib import call
     call("sa_attn_set_variant", request.param)
     yield request.param
-    call("sa_attn_set_variant", 5)
+    call("sa_attn_set_variant", 6)
 
 
 @pytest.mark.parametrize("Lq,Lk", [(300, 300), (512, 257), (1024, 17), (64, 512)])
