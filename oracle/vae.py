@@ -1,6 +1,6 @@
 """ORACLE — test infrastructure only (tests/, smoke(), bench.py cpu_baseline).
 
-CPU fp32 restatement of the Wan-2.1 3-D causal VAE *decoder* (wan/models/wan_vae.py).
+CPU fp32 restatement of the Wan-2.1 3-D causal VAE decoder and encoder (wan/models/wan_vae.py).
 The reference decodes one latent frame at a time with a 2-frame causal feature cache
 (wan_vae.py:549-574, CausalConv3d :20-39, Resample :104-163).  That schedule is equivalent to
 running every layer over the whole clip at once with:
@@ -8,8 +8,15 @@ running every layer over the whole clip at once with:
   * Resample 'upsample3d': frame 0 bypasses time_conv ('Rep', :108-111); frames 1.. go through a
     causal time_conv over the sub-sequence that EXCLUDES frame 0 (the first cached chunk is
     zero-filled, :123-131), then each output frame splits into two (:137-140).
-This module implements the whole-clip form; tests/test_oracle_golden.py pins it against the
-reference's own frame-by-frame decode output.
+The encoder (wan_vae.py:519-547) runs chunks of 1, 4, 4, ... frames with the same cache; in
+whole-clip form:
+  * CausalConv3d as above;
+  * Resample 'downsample2d' / 'downsample3d': ZeroPad2d((0,1,0,1)) + 3x3 stride-2 conv per frame;
+    'downsample3d' then keeps frame 0 (its first chunk is only cached, :145-148) and maps frames
+    1.. through time_conv (3,1,1) stride 2 WITHOUT padding over [last frame of the previous chunk,
+    chunk] (:150-157), i.e. output j >= 1 = time_conv(frames 2j-2, 2j-1, 2j) of the whole clip.
+This module implements the whole-clip forms; tests/test_oracle_golden.py pins them against the
+reference's own chunked decode / encode outputs.
 """
 from __future__ import annotations
 
@@ -180,4 +187,124 @@ def flops_decode(T, h, w, dim=96, z_dim=16):
             fl += 2 * t * hh * ww * 9 * cin * cout
         elif kind == "head":
             fl += 2 * n * 27 * cin * cout
+    return fl
+
+
+def encoder_layout(dim=96, dim_mult=(1, 2, 4, 4), num_res_blocks=2, temperal_downsample=(False, True, True)):
+    """Module list of Encoder3d (wan_vae.py:268-319): list of (kind, name, in, out)."""
+    dims = [dim * u for u in [1] + list(dim_mult)]
+    L = [("conv", "conv1", 3, dims[0])]
+    k = 0
+    for i, (din, dout) in enumerate(zip(dims[:-1], dims[1:])):
+        for _ in range(num_res_blocks):
+            L.append(("res", f"downsamples.{k}", din, dout))
+            k += 1
+            din = dout
+        if i != len(dim_mult) - 1:
+            L.append(("down3d" if temperal_downsample[i] else "down2d", f"downsamples.{k}", dout, dout))
+            k += 1
+    L += [("res", "middle.0", dims[-1], dims[-1]), ("attn", "middle.1", dims[-1], dims[-1]),
+          ("res", "middle.2", dims[-1], dims[-1]), ("head", "head", dims[-1], None)]
+    return L
+
+
+def encoder_param_shapes(dim=96, z_dim=16):
+    """{name: shape} of the encoder half of AutoencoderKLWan (prefix 'model.'); head -> 2*z_dim."""
+    S = {"model.conv1.weight": (2 * z_dim, 2 * z_dim, 1, 1, 1), "model.conv1.bias": (2 * z_dim,)}
+    p = "model.encoder."
+    for kind, name, cin, cout in encoder_layout(dim):
+        q = p + name
+        if kind == "conv":
+            S[q + ".weight"] = (cout, cin, 3, 3, 3)
+            S[q + ".bias"] = (cout,)
+        elif kind == "res":
+            S[q + ".residual.0.gamma"] = (cin, 1, 1, 1)
+            S[q + ".residual.2.weight"] = (cout, cin, 3, 3, 3)
+            S[q + ".residual.2.bias"] = (cout,)
+            S[q + ".residual.3.gamma"] = (cout, 1, 1, 1)
+            S[q + ".residual.6.weight"] = (cout, cout, 3, 3, 3)
+            S[q + ".residual.6.bias"] = (cout,)
+            if cin != cout:
+                S[q + ".shortcut.weight"] = (cout, cin, 1, 1, 1)
+                S[q + ".shortcut.bias"] = (cout,)
+        elif kind == "attn":
+            S[q + ".norm.gamma"] = (cin, 1, 1)
+            S[q + ".to_qkv.weight"] = (cin * 3, cin, 1, 1)
+            S[q + ".to_qkv.bias"] = (cin * 3,)
+            S[q + ".proj.weight"] = (cin, cin, 1, 1)
+            S[q + ".proj.bias"] = (cin,)
+        elif kind in ("down2d", "down3d"):
+            S[q + ".resample.1.weight"] = (cout, cin, 3, 3)
+            S[q + ".resample.1.bias"] = (cout,)
+            if kind == "down3d":
+                S[q + ".time_conv.weight"] = (cout, cout, 3, 1, 1)
+                S[q + ".time_conv.bias"] = (cout,)
+        elif kind == "head":
+            S[q + ".0.gamma"] = (cin, 1, 1, 1)
+            S[q + ".2.weight"] = (2 * z_dim, cin, 3, 3, 3)
+            S[q + ".2.bias"] = (2 * z_dim,)
+    return S
+
+
+def resample_down(P, q, x, temporal):
+    """Resample downsample2d/downsample3d (wan_vae.py:91-100, :142-157) in whole-clip form."""
+    b, c, t, h, w = x.shape
+    y = x.permute(0, 2, 1, 3, 4).reshape(b * t, c, h, w)
+    y = F.conv2d(F.pad(y, (0, 1, 0, 1)), P[q + ".resample.1.weight"], P[q + ".resample.1.bias"], stride=2)
+    x = y.reshape(b, t, c, y.shape[2], y.shape[3]).permute(0, 2, 1, 3, 4)
+    if temporal and t > 1:
+        rest = F.conv3d(x, P[q + ".time_conv.weight"], P[q + ".time_conv.bias"], stride=(2, 1, 1))
+        x = torch.cat([x[:, :, :1], rest], 2)
+    return x
+
+
+def encode(P, x, dim=96, z_dim=16):
+    """AutoencoderKLWan._encode(x) (wan_vae.py:519-547, :643-648): video [B,3,1+4k,H,W] in [-1,1] ->
+    [B, 2*z_dim, 1+k, H/8, W/8] = cat(normalised mu, log_var) (the posterior's parameters; .mode() is
+    the first z_dim channels)."""
+    x = x.float()
+    if (x.shape[2] - 1) % 4:
+        raise ValueError("the chunked encoder consumes 1 + 4k frames")
+    p = "model.encoder."
+    for kind, name, cin, cout in encoder_layout(dim):
+        q = p + name
+        if kind == "conv":
+            x = causal_conv3d(x, P[q + ".weight"], P[q + ".bias"])
+        elif kind == "res":
+            x = residual_block(P, q, x)
+        elif kind == "attn":
+            x = attention_block(P, q, x)
+        elif kind in ("down2d", "down3d"):
+            x = resample_down(P, q, x, kind == "down3d")
+        elif kind == "head":
+            x = F.silu(rms_norm(x, P[q + ".0.gamma"]))
+            x = causal_conv3d(x, P[q + ".2.weight"], P[q + ".2.bias"])
+    x = causal_conv3d(x, P["model.conv1.weight"], P["model.conv1.bias"])
+    mu, log_var = x.chunk(2, dim=1)
+    mean = torch.tensor(MEAN, dtype=torch.float32).view(1, z_dim, 1, 1, 1)
+    std = torch.tensor(STD, dtype=torch.float32).view(1, z_dim, 1, 1, 1)
+    return torch.cat([(mu - mean) * (1.0 / std), log_var], 1)
+
+
+def flops_encode(T, H, W, dim=96, z_dim=16):
+    """Analytic conv/attention FLOPs (2/MAC) of a whole-clip encode of T = 1+4k frames at H x W."""
+    fl = 0
+    t, hh, ww = T, H, W
+    for kind, name, cin, cout in encoder_layout(dim):
+        n = t * hh * ww
+        if kind == "conv":
+            fl += 2 * n * 27 * cin * cout
+        elif kind == "res":
+            fl += 2 * n * 27 * (cin * cout + cout * cout) + (2 * n * cin * cout if cin != cout else 0)
+        elif kind == "attn":
+            fl += 2 * n * cin * cin * 4 + 4 * t * (hh * ww) ** 2 * cin
+        elif kind in ("down2d", "down3d"):
+            hh, ww = hh // 2, ww // 2
+            fl += 2 * t * hh * ww * 9 * cin * cout
+            if kind == "down3d":
+                t = 1 + (t - 1) // 2
+                fl += 2 * (t - 1) * hh * ww * 3 * cout * cout
+        elif kind == "head":
+            fl += 2 * n * 27 * cin * 2 * z_dim
+    fl += 2 * t * hh * ww * (2 * z_dim) ** 2
     return fl

@@ -80,8 +80,39 @@ def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group) -> 
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
 
 
+class Pending:
+    """An issued all-to-all and the unpack that runs once it has landed.
+
+    On RCCL the collective runs on ProcessGroupNCCL's own stream; ``wait()`` makes the caller's
+    current stream wait for it (no host sync) and then enqueues the unpack copies there, so compute
+    queued on the current stream between issue and ``wait()`` overlaps the transfer."""
+
+    def __init__(self, work, finish):
+        self.work, self.finish = work, finish
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+        if self.finish is not None:
+            self.finish()
+            self.finish = None
+
+
+def _a2a_async(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group):
+    if inp.is_cuda and dist.get_backend(group) == "gloo":
+        _a2a(out, inp, out_splits, in_splits, group)  # host-staged: completes here
+        return None
+    return dist.all_to_all_single(out, inp, out_splits, in_splits, group=group, async_op=True)
+
+
 class UlyssesExchange:
-    """The two all-to-alls around one sequence-parallel self-attention."""
+    """The two all-to-alls around one sequence-parallel self-attention.
+
+    ``to_heads`` / ``to_tokens`` move all CFG rows in one collective each.  ``to_heads_row`` /
+    ``to_tokens_row`` move one CFG row and return a ``Pending``: the transformer issues the three
+    rows' Q/K/V exchanges up front and runs row b's attention while rows b+1.. are in flight and row
+    b-1's output travels back (comm/compute overlap on separate HIP streams)."""
 
     def __init__(self, plan: SPPlan, group=None):
         self.plan = plan
@@ -151,6 +182,70 @@ class UlyssesExchange:
         parts = recv.view(G, B, Lc, hg * D)
         out.view(B, Lc, G, hg * D).copy_(parts.permute(1, 2, 0, 3))
         return out
+
+    # one CFG row at a time, asynchronous ----------------------------------------------------------
+    def to_heads_row(self, qkv: torch.Tensor, b: int, B: int, Lc: int, D: int,
+                     q_dst: torch.Tensor, kv_dst: torch.Tensor) -> Pending:
+        """Row b of ``to_heads``: q_dst [B*G*Lc, hg*D] and kv_dst [B*Lp, 2*hg*D] (the layouts
+        ``to_heads`` returns) receive row b once the returned Pending is waited on."""
+        p = self.plan
+        N, G, hg = p.world, p.G, p.hg
+        x = qkv.view(B, Lc, 3, G, hg * D)[b]
+        q_el = Lc * hg * D
+        kv_el = 2 * q_el
+        my_part = p.part_of_chunk(p.rank)
+        sends, in_splits = [], []
+        for j in range(N):
+            gj, pj = j % G, j // G
+            n = 0
+            if pj == my_part:
+                sends.append(x[:, 0, gj].reshape(-1))
+                n += q_el
+            sends.append(x[:, 1:3, gj].reshape(-1))  # [Lc, 2, hg*D]
+            in_splits.append(n + kv_el)
+        send = torch.cat(sends)
+        src_q = [p.part_of_chunk(r) == p.part for r in range(N)]
+        out_splits = [(q_el if src_q[r] else 0) + kv_el for r in range(N)]
+        recv = torch.empty(sum(out_splits), dtype=qkv.dtype, device=qkv.device)
+        work = _a2a_async(recv, send, out_splits, in_splits, self.group)
+        Lq = G * Lc
+
+        def finish():
+            qv = q_dst.view(B, Lq, hg * D)[b]
+            kvv = kv_dst.view(B, N * Lc, 2 * hg * D)[b]
+            off, qi = 0, 0
+            for r in range(N):
+                if src_q[r]:
+                    qv[qi * Lc:(qi + 1) * Lc].copy_(recv[off:off + q_el].view(Lc, hg * D))
+                    qi += 1
+                    off += q_el
+                kvv[r * Lc:(r + 1) * Lc].copy_(recv[off:off + kv_el].view(Lc, 2 * hg * D))
+                off += kv_el
+
+        return Pending(work, finish)
+
+    def to_tokens_row(self, o: torch.Tensor, b: int, B: int, Lc: int, D: int, out: torch.Tensor) -> Pending:
+        """Row b of ``to_tokens``: o [B*G*Lc, hg*D]; out [B*Lc, H*D] receives row b on wait()."""
+        p = self.plan
+        N, G, hg = p.world, p.G, p.hg
+        el = Lc * hg * D
+        ov = o.view(B, G, Lc, hg * D)[b]
+        sends, in_splits = [], []
+        for r in range(N):
+            if p.part_of_chunk(r) == p.part:
+                sends.append(ov[r - p.part * G].reshape(-1))
+                in_splits.append(el)
+            else:
+                in_splits.append(0)
+        send = torch.cat(sends)
+        out_splits = [el if (j // G) == p.part_of_chunk(p.rank) else 0 for j in range(N)]
+        recv = torch.empty(sum(out_splits), dtype=o.dtype, device=o.device)
+        work = _a2a_async(recv, send, out_splits, in_splits, self.group)
+
+        def finish():
+            out.view(B, Lc, G, hg * D)[b].copy_(recv.view(G, Lc, hg * D).permute(1, 0, 2))
+
+        return Pending(work, finish)
 
 
 def gather_tokens(local: torch.Tensor, B: int, Lc: int, world: int, group=None) -> torch.Tensor:

@@ -549,7 +549,20 @@ class WanTransformer3DFantasyModel(nn.Module):
             Lq, hg = plan.G * Lc, plan.hg
             segs_self = self._segs.get(("self_sp", B, Lp, Lq), [[b * Lq, Lq, b * Lp, Lp] for b in range(B)], dev)
             o_sp = torch.empty(B * Lq, hg * self.d, device=dev, dtype=torch.bfloat16)
+            # per-row pipelining only when it adds no attention waves: a row's launch has
+            # ceil(Lq / 256) x hg workgroups; B serial launches must not need more rounds over the CUs
+            # than the batched one (N = 8: 63 workgroups per row would leave most CUs idle)
+            n_cu = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 256
+            wg_row = -(-Lq // 256) * hg
+            ov = os.environ.get("SA_SP_OVERLAP", "1")  # 0 off, 1 when it adds no waves, 2 always
+            sp_rows = ov == "2" or (ov == "1" and B * -(-wg_row // n_cu) <= -(-(B * wg_row) // n_cu))
+            if sp_rows:
+                q_sp = torch.empty(B * Lq, hg * self.d, device=dev, dtype=torch.bfloat16)
+                kv_sp = torch.empty(B * Lp, 2 * hg * self.d, device=dev, dtype=torch.bfloat16)
+                segs_rows = [self._segs.get(("self_sp_row", b, Lp, Lq), [[b * Lq, Lq, b * Lp, Lp]], dev)
+                             for b in range(B)]
         else:
+            sp_rows = False
             segs_self = self._segs.get(("self", B, Lp), [[b * Lp, Lp, b * Lp, Lp] for b in range(B)], dev)
         segs_txt = self._segs.get(("txt", B, Lc, ctx.text_len), sp.local_segments(B, Lc, ctx.text_len), dev)
         segs_img = self._segs.get(("img", B, Lc, ctx.img_len), sp.local_segments(B, Lc, ctx.img_len), dev)
@@ -569,21 +582,32 @@ class WanTransformer3DFantasyModel(nn.Module):
             ops.qk_rmsnorm_rope(ws.qkv, 0, dim, L.nq, L.nk, dim, self.eps, rope=pk.rope, rows_per_batch=Lc,
                                 tok_offset=rank * Lc, grid=grid, head_dim=self.d,
                                 n_frame_pairs=self.d // 2 - 2 * (self.d // 6), n_height_pairs=self.d // 6)
-            if NS > 1:  # Ulysses: tokens -> heads, full-sequence attention, heads -> tokens
+            if NS > 1 and sp_rows:  # Ulysses, one CFG row per exchange, overlapped with attention
+                pend = [exch.to_heads_row(ws.qkv, b, B, Lc, self.d, q_sp, kv_sp) for b in range(B)]
+                back = []
+                for b in range(B):
+                    pend[b].wait()
+                    ops.attention(q_sp, kv_sp[:, :hg * self.d], kv_sp[:, hg * self.d:], o_sp, segs_rows[b], 1, Lq,
+                                  hg)
+                    back.append(exch.to_tokens_row(o_sp, b, B, Lc, self.d, ws.att))
+                for pb in back:
+                    pb.wait()
+            elif NS > 1:  # Ulysses: tokens -> heads, full-sequence attention, heads -> tokens
                 q_sp, kv_sp = exch.to_heads(ws.qkv, B, Lc, self.d)
                 args_ = (q_sp, kv_sp[:, :hg * self.d], kv_sp[:, hg * self.d:], o_sp, segs_self, B, Lq, hg)
             else:
                 args_ = (ws.qkv[:, :dim], ws.qkv[:, dim:2 * dim], ws.qkv[:, 2 * dim:], ws.att, segs_self, B, Lp, H_)
-            if self._events is not None:  # bench.py: HIP events around the self-attention kernel
-                ev0 = torch.cuda.Event(enable_timing=True)
-                ev0.record()
-            ops.attention(*args_)
-            if self._events is not None:
-                ev1 = torch.cuda.Event(enable_timing=True)
-                ev1.record()
-                self._events.append((ev0, ev1))
-            if NS > 1:
-                exch.to_tokens(o_sp, B, Lc, self.d, ws.att)
+            if not (NS > 1 and sp_rows):
+                if self._events is not None:  # bench.py: HIP events around the self-attention kernel
+                    ev0 = torch.cuda.Event(enable_timing=True)
+                    ev0.record()
+                ops.attention(*args_)
+                if self._events is not None:
+                    ev1 = torch.cuda.Event(enable_timing=True)
+                    ev1.record()
+                    self._events.append((ev0, ev1))
+                if NS > 1:
+                    exch.to_tokens(o_sp, B, Lc, self.d, ws.att)
             ops.linear(ws.att, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2], rows_per_batch=Lc)
             # cross-attention: text + image + per-frame vocal (1B:534-605, 684)
             ops.layernorm_mod(x, ws.mod, self.eps, weight=L.n3w, bias=L.n3b)

@@ -24,7 +24,8 @@ import _refstub  # noqa: E402
 _refstub.install()
 
 from stableavatar_amd import synthetic  # noqa: E402
-from golden_cases import DIT_SMALL, dit_inputs, VAE_SMALL, vae_latent, PIPE, pipe_fixed_inputs  # noqa: E402
+from golden_cases import (DIT_SMALL, dit_inputs, VAE_SMALL, vae_latent, VAE_ENC_SMALL, vae_video, PIPE,  # noqa: E402
+                          pipe_fixed_inputs)
 
 torch.set_grad_enabled(False)
 
@@ -78,6 +79,21 @@ def gen_vae():
         out[name] = y.numpy()
         print("vae", name, tuple(y.shape), float(y.abs().mean()))
     np.savez_compressed(os.path.join(HERE, "vae_small.npz"), **out)
+
+
+def gen_vae_enc():
+    """AutoencoderKLWan._encode (wan_vae.py:643-648): chunked 1, 4, 4.. encode with the feature cache;
+    stored: cat(normalised mu, log_var) [1, 32, 1+(T-1)/4, H/8, W/8]."""
+    out = {}
+    for name, cfg in VAE_ENC_SMALL.items():
+        v = build_ref_vae(cfg)
+        x = vae_video(cfg)
+        h = v._encode(x)
+        mode = v.encode(x)[0].mode()
+        assert torch.equal(mode, h[:, :16])
+        out[name] = h.numpy()
+        print("vae_enc", name, tuple(h.shape), float(h.abs().mean()))
+    np.savez_compressed(os.path.join(HERE, "vae_enc_small.npz"), **out)
 
 
 class _Obj(types.SimpleNamespace):
@@ -189,6 +205,6 @@ def gen_tables():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["tables", "dit", "vae", "pipeline"]
+    which = sys.argv[1:] or ["tables", "dit", "vae", "vae_enc", "pipeline"]
     for w in which:
         globals()["gen_" + w]()

@@ -35,6 +35,15 @@ VAE_SMALL = {"dim32_T3_8x8": dict(dim=32, seed=21, T=3, h=8, w=8),
              "dim96_T2_4x4": dict(dim=96, seed=22, T=2, h=4, w=4)}
 
 
+VAE_ENC_SMALL = {"dim32_T9_32x32": dict(dim=32, seed=21, T=9, H=32, W=32),
+                 "dim96_T5_16x16": dict(dim=96, seed=22, T=5, H=16, W=16)}
+
+
+def vae_video(cfg):
+    """Encoder input: [1, 3, T, H, W] video, N(0, 0.5^2) clamped to [-1, 1] like pixel values."""
+    return (0.5 * synthetic.seeded_normal((1, 3, cfg["T"], cfg["H"], cfg["W"]), 300 + cfg["seed"])).clamp(-1, 1)
+
+
 def vae_latent(cfg):
     return synthetic.seeded_normal((1, 16, cfg["T"], cfg["h"], cfg["w"]), 200 + cfg["seed"])
 

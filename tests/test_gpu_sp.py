@@ -23,7 +23,8 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, case, qret):
+def _worker(rank, world, port, case, overlap, qret):
+    os.environ["SA_SP_OVERLAP"] = overlap
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -43,13 +44,13 @@ def _worker(rank, world, port, case, qret):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case", ["full", "short"])
-def test_sp2_matches_single_gpu(case):
+@pytest.mark.parametrize("case,overlap", [("full", "0"), ("short", "0"), ("full", "2")])
+def test_sp2_matches_single_gpu(case, overlap):
     world = 2
     ctx = mp.get_context("spawn")
     qret = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, case, qret)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, overlap, qret)) for r in range(world)]
     for p in procs:
         p.start()
     res = [qret.get(timeout=300) for _ in range(world)]

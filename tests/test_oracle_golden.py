@@ -10,7 +10,8 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "golden"))
 
-from golden_cases import DIT_SMALL, PIPE, VAE_SMALL, dit_inputs, pipe_fixed_inputs, vae_latent  # noqa: E402
+from golden_cases import (DIT_SMALL, PIPE, VAE_ENC_SMALL, VAE_SMALL, dit_inputs, pipe_fixed_inputs,  # noqa: E402
+                          vae_latent, vae_video)
 
 from oracle import dit as odit  # noqa: E402
 from oracle import pipeline as opipe  # noqa: E402
@@ -77,6 +78,23 @@ def test_vae_decode_vs_reference(name):
     g = G("vae_small.npz")[name]
     assert y.shape == g.shape
     assert rel(y, g) < 1e-5
+
+
+@pytest.mark.parametrize("name", list(VAE_ENC_SMALL))
+def test_vae_encode_vs_reference(name):
+    """Whole-clip encoder restatement == the reference's chunked (1, 4, 4, ..) cached encode."""
+    cfg = VAE_ENC_SMALL[name]
+    P = synthetic.fill_state_dict(ovae.encoder_param_shapes(dim=cfg["dim"]), cfg["seed"])
+    with torch.no_grad():
+        h = ovae.encode(P, vae_video(cfg), dim=cfg["dim"])
+    g = G("vae_enc_small.npz")[name]
+    assert h.shape == g.shape
+    assert rel(h, g) < 1e-5
+
+
+def test_vae_encode_flops():
+    """107.2 TFLOP for the reference frame + 80 zero frames at 512x512."""
+    assert abs(ovae.flops_encode(81, 512, 512) / 1e12 - 107.2) < 0.1
 
 
 def test_pipeline_vs_reference():

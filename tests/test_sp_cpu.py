@@ -51,6 +51,17 @@ def _worker(rank, world, port, B, Lp, H, D, q_ret):
         out = torch.empty(B * Lc, H * D)
         ex.to_tokens(o, B, Lc, D, out)
         err = (out.view(B, Lc, H, D) - ref[:, rank * Lc:(rank + 1) * Lc]).abs().max().item()
+        # per-row asynchronous exchange (the overlapped path): identical buffers, bit-exact
+        q2, kv2 = torch.empty_like(q), torch.empty_like(kv)
+        pend = [ex.to_heads_row(mine, b, B, Lc, D, q2, kv2) for b in range(B)]
+        out2 = torch.empty_like(out)
+        back = []
+        for b in range(B):
+            pend[b].wait()
+            back.append(ex.to_tokens_row(o, b, B, Lc, D, out2))
+        for pb in back:
+            pb.wait()
+        assert torch.equal(q2, q) and torch.equal(kv2, kv) and torch.equal(out2, out)
         full = sp.gather_tokens(out, B, Lc, world)
         gerr = (full.view(B, Lp, H, D) - ref).abs().max().item()
         q_ret.put((rank, err, gerr, plan.G, plan.R))
