@@ -36,6 +36,7 @@ def parse():
     p.add_argument("--sample-steps", type=int, default=50)
     p.add_argument("--overlap", type=int, default=15)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-encode", action="store_true", help="skip the (untimed) VAE encode measurement")
     p.add_argument("--sp", action="store_true",
                    help="N>1: one clip sequence-parallel over all ranks (Ulysses, strong scaling) instead of "
                         "one clip per rank (replicas, weak scaling)")
@@ -46,13 +47,14 @@ def build(dev, seed=0):
     from stableavatar_amd import synthetic
     from stableavatar_amd.transformer import WanTransformer3DFantasyModel, param_shapes
     from stableavatar_amd.vae import AutoencoderKLWan
-    from stableavatar_amd.vae import param_shapes as vae_shapes
+    from stableavatar_amd.vae import encoder_param_shapes, param_shapes as vae_shapes
     cfg = dict(model_type="i2v", dim=1536, ffn_dim=8960, freq_dim=256, text_dim=4096, in_dim=36, out_dim=16,
                num_heads=12, num_layers=30, text_len=512)
     dit = WanTransformer3DFantasyModel(**cfg).to(dev)
     dit.load_state_dict(synthetic.fill_state_dict(param_shapes(cfg), seed, backend="torch", device=dev))
     vae = AutoencoderKLWan().to(dev)
-    vae.load_state_dict(synthetic.fill_state_dict(vae_shapes(), seed + 1, backend="torch", device=dev))
+    vae.load_state_dict(synthetic.fill_state_dict(dict(vae_shapes(), **encoder_param_shapes()), seed + 1,
+                                                  backend="torch", device=dev))
     return dit, vae
 
 
@@ -162,6 +164,22 @@ def main():
         events = dit._events
         dit._events = None
     assert video.shape[1] == args.frames and torch.isfinite(video).all()
+    enc = None
+    if not args.no_encode:  # once-per-call VAE encode of reference frame + zeros (pipeline:679-692), untimed
+        ref = torch.zeros(1, 3, args.frames, args.size, args.size, device=dev)
+        ref[:, :, 0].uniform_(-1, 1)
+        with torch.no_grad():
+            vae.encode(ref)
+            torch.cuda.synchronize()
+            te = time.perf_counter()
+            lat_y = vae.encode(ref)[0].mode()
+            torch.cuda.synchronize()
+            te = time.perf_counter() - te
+        assert tuple(lat_y.shape) == (1, 16, (args.frames - 1) // 4 + 1, args.size // 8, args.size // 8)
+        ef = flops.vae_encode_flops(args.frames, args.size, args.size)
+        enc = {"ms": round(te * 1e3, 1), "tflop": round(ef / 1e12, 2), "tflops_per_s": round(ef / te / 1e12, 1),
+               "note": "AutoencoderKLWan.encode of the reference frame + zeros, once per call; outside the timed "
+                       "region and the metric (SURVEY.md §8(d))"}
     if world > 1:
         import torch.distributed as dist
         tt = torch.tensor([dt], device=dev, dtype=torch.float64)
@@ -206,7 +224,7 @@ def main():
                             "algorithmic_bytes": 4 * 3 * seq_len * 1536 * 2,
                             "launch_ms": round(attn_ms, 3), "flop_per_launch": attn_flop},
                "path_mfma_frac": round(path_flop * args.steps / dt / PEAK_BF16 / (world if sp_mode else 1), 4),
-               "cpu_baseline": cpu}
+               "cpu_baseline": cpu, "vae_encode": enc}
         print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist

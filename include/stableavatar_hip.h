@@ -137,6 +137,14 @@ int sa_conv3d_cl(const void* x, int T, int H, int W, int Cin, int upsample, cons
                  int Cout_pad, int kt, int kh, int kw, const void* residual, void* y, int out_f32,
                  int interleave_half, void* stream);
 
+/* Encoder downsampling convs on channels-last bf16, fp32 accumulate, bf16 out [T_out][H][W][Cout]:
+ * mode 1 = Resample 'downsample2d/3d' spatial part (wan_vae.py:91-100): ZeroPad2d((0,1,0,1)) + 3x3
+ *   stride-2 conv per frame, x [T_out][H_in][W_in][Cin] -> H_in/2 x W_in/2, w [Cout_pad][1][3][3][Cin];
+ * mode 2 = 'downsample3d' time_conv (3,1,1) stride (2,1,1) without padding (:99, :150-157):
+ *   output frame t reads input frames 2t..2t+2 (the caller passes frame 0 separately), w [Cout_pad][3][1][1][Cin]. */
+int sa_conv3d_cl_down(const void* x, int T_out, int H_in, int W_in, int Cin, int mode, const void* w,
+                      const float* bias, int Cout, int Cout_pad, void* y, void* stream);
+
 /* RMS_norm (wan_vae.py:42-57): x / max(||x||_2, 1e-12) * sqrt(C) * gamma over channels (+SiLU :198-200). */
 int sa_vae_rmsnorm_silu(const void* x, void* y, const float* gamma, int64_t rows, int C, int do_silu, void* stream);
 
@@ -147,6 +155,11 @@ int sa_vae_input(const float* z, int Cz, int64_t THW, const float* mean, const f
 /* channels-last fp32 [THW][C_stride] -> [C][THW] clamped to [-1,1] (:668); post != 0 also applies
  * decode_latents' /2 + 0.5 and clamp(0,1) (wan_inference_long_pipeline.py:427). */
 int sa_vae_output(const float* in, int C_stride, int C, int64_t THW, float* out, int post, void* stream);
+
+/* Encoder output (wan_vae.py:538-545): channels-last fp32 [THW][C_stride] holding mu | log_var ->
+ * [2 Cz][THW] fp32 with mu normalised (mu - mean) * (1/std); log_var unchanged. */
+int sa_vae_latent_out(const float* in, int C_stride, int Cz, int64_t THW, const float* mean, const float* stdv,
+                      float* out, void* stream);
 
 /* row softmax of fp32 scores (scaled) -> bf16 probabilities (AttentionBlock SDPA, wan_vae.py:255-259). */
 int sa_softmax_rows(const float* s, int64_t ld_s, void* p, int64_t ld_p, int64_t rows, int n, float scale,

@@ -14,5 +14,5 @@ scripts/pmc_attn.sh > gpurun_out/pmcattn_$tag.log 2>&1; rc=$?; echo "pmc attn rc
 scripts/gpustep.sh 300 gpurun_out/bench_$tag.log python bench.py; rc=$?; echo "bench rc=$rc"
 [ $rc -ne 0 ] && exit $rc
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$tag -o run -- python bench.py > gpurun_out/prof_$tag.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o run -- python bench.py > gpurun_out/prof_$tag.log 2>&1
 echo "prof rc=$?"

@@ -37,6 +37,8 @@ SIGNATURES = {
     "sa_vae_rmsnorm_silu": "pppliip",
     "sa_vae_input": "pilpppip",
     "sa_vae_output": "piilpip",
+    "sa_conv3d_cl_down": "piiiiippiipp",
+    "sa_vae_latent_out": "piilpppp",
     "sa_softmax_rows": "plpllifp",
     "sa_transpose_bf16": "pllplliiip",
 }

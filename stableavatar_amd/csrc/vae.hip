@@ -29,6 +29,9 @@ struct ConvArgs {
   int out_f32;
   int ichalf;        // >0: time_conv interleave, out[2t + n/ichalf][h][w][n%ichalf]
   long M;
+  int down;          // 0: stride 1; 1: ZeroPad2d((0,1,0,1)) + 3x3 stride 2 (Resample 'downsample*',
+                     // :91-100), input [T][Hin][Win]; 2: (3,1,1) time_conv, stride 2, no padding
+                     // (:99, :150-157): output frame t reads input frames 2t .. 2t+2
 };
 
 constexpr int BM = 128, BK = 32;
@@ -74,10 +77,24 @@ __global__ __launch_bounds__(256) void conv3d_cl_kernel(ConvArgs a) {
     const int dt = tap / (a.kh * a.kw), dh = (tap / a.kw) % a.kh, dw = tap % a.kw;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int ti = at[j] + dt - (a.kt - 1);
-      const int hi = ah[j] + dh - (a.kh - 1) / 2;
-      const int wi = aw[j] + dw - (a.kw - 1) / 2;
-      const bool ok = arow_ok[j] && ti >= 0 && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
+      int ti, hi, wi;
+      bool ok;
+      if (a.down == 1) {  // wave-uniform
+        ti = at[j];
+        hi = 2 * ah[j] + dh;
+        wi = 2 * aw[j] + dw;
+        ok = arow_ok[j] && hi < a.Hin && wi < a.Win;
+      } else if (a.down == 2) {
+        ti = 2 * at[j] + dt;
+        hi = ah[j];
+        wi = aw[j];
+        ok = arow_ok[j];
+      } else {
+        ti = at[j] + dt - (a.kt - 1);
+        hi = ah[j] + dh - (a.kh - 1) / 2;
+        wi = aw[j] + dw - (a.kw - 1) / 2;
+        ok = arow_ok[j] && ti >= 0 && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
+      }
       if (ok) {
         const int hp = a.upsample ? (hi >> 1) : hi, wp = a.upsample ? (wi >> 1) : wi;
         const bf16* src = a.x + (((long)ti * a.Hin + hp) * a.Win + wp) * a.Cin + ci0 + ac[j] * 8;
@@ -287,6 +304,18 @@ __global__ void transpose_kernel(const bf16* in, long ldi, long si, bf16* out, l
   }
 }
 
+// encoder output: channels-last fp32 [THW][C_stride] (mu | log_var) -> [2 Cz][THW] with
+// mu normalised as (mu - mean) * (1 / std) (wan_vae.py:538-544); log_var passes through
+__global__ void vae_latent_out_kernel(const float* in, int C_stride, int Cz, long THW, const float* mean,
+                                      const float* stdv, float* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= THW * 2 * Cz) return;
+  const int c = (int)(i / THW);
+  const long p = i % THW;
+  const float v = in[p * C_stride + c];
+  out[i] = c < Cz ? (v - mean[c]) * (1.0f / stdv[c]) : v;
+}
+
 inline unsigned nblk(long n, int t) { return (unsigned)((n + t - 1) / t); }
 
 }  // namespace
@@ -299,12 +328,27 @@ extern "C" int sa_conv3d_cl(const void* x, int T, int H, int W, int Cin, int ups
   if (upsample && (H % 2 || W % 2)) return SA_ERR_ARG;
   if (interleave_half > 0 && (Cout != 2 * interleave_half || residual)) return SA_ERR_ARG;
   ConvArgs a{(const bf16*)x, T, H, W, Cin, upsample ? H / 2 : H, upsample ? W / 2 : W, upsample, (const bf16*)w,
-             bias, Cout, kt, kh, kw, (const bf16*)residual, y, out_f32, interleave_half, (long)T * H * W};
+             bias, Cout, kt, kh, kw, (const bf16*)residual, y, out_f32, interleave_half, (long)T * H * W, 0};
   hipStream_t st = (hipStream_t)stream;
   // N tile chosen so the packed weight rows (Cout_pad) cover whole tiles
   if (Cout_pad % 192 == 0 && Cout > 96) return launch_conv<12>(a, st);
   if (Cout_pad % 96 == 0 && Cout > 16) return launch_conv<6>(a, st);
   if (Cout_pad % 16 == 0 && Cout <= 16) return launch_conv<1>(a, st);
+  return SA_ERR_ARG;
+}
+
+extern "C" int sa_conv3d_cl_down(const void* x, int T_out, int H_in, int W_in, int Cin, int mode, const void* w,
+                                 const float* bias, int Cout, int Cout_pad, void* y, void* stream) {
+  if (!x || !w || !bias || !y || T_out <= 0 || H_in <= 0 || W_in <= 0) return SA_ERR_ARG;
+  if (Cin % BK || Cout % 4 || (mode != 1 && mode != 2)) return SA_ERR_ARG;
+  if (mode == 1 && (H_in % 2 || W_in % 2)) return SA_ERR_ARG;
+  const int H = mode == 1 ? H_in / 2 : H_in, W = mode == 1 ? W_in / 2 : W_in;
+  const int kt = mode == 1 ? 1 : 3, kh = mode == 1 ? 3 : 1;
+  ConvArgs a{(const bf16*)x, T_out, H, W, Cin, H_in, W_in, 0, (const bf16*)w, bias, Cout, kt, kh, kh,
+             nullptr, y, 0, 0, (long)T_out * H * W, mode};
+  hipStream_t st = (hipStream_t)stream;
+  if (Cout_pad % 192 == 0 && Cout > 96) return launch_conv<12>(a, st);
+  if (Cout_pad % 96 == 0 && Cout > 16) return launch_conv<6>(a, st);
   return SA_ERR_ARG;
 }
 
@@ -340,6 +384,15 @@ extern "C" int sa_vae_output(const float* in, int C_stride, int C, int64_t THW, 
   if (!in || !out || C > C_stride) return SA_ERR_ARG;
   hipLaunchKernelGGL(vae_output_kernel, dim3(nblk(THW * C, 256)), dim3(256), 0, (hipStream_t)stream, in, C_stride, C,
                      THW, out, post);
+  SA_LAUNCH_CHECK();
+  return SA_OK;
+}
+
+extern "C" int sa_vae_latent_out(const float* in, int C_stride, int Cz, int64_t THW, const float* mean,
+                                 const float* stdv, float* out, void* stream) {
+  if (!in || !out || !mean || !stdv || 2 * Cz > C_stride) return SA_ERR_ARG;
+  hipLaunchKernelGGL(vae_latent_out_kernel, dim3(nblk(THW * 2 * Cz, 256)), dim3(256), 0, (hipStream_t)stream, in,
+                     C_stride, Cz, THW, mean, stdv, out);
   SA_LAUNCH_CHECK();
   return SA_OK;
 }

@@ -45,3 +45,28 @@ def vae_decode_flops(T=21, h=64, w=64, dim=96, z_dim=16):
         cin = dout
     fl += 2 * t * hh * ww * 27 * cin * 3                                   # head
     return fl
+
+
+def vae_encode_flops(T=81, H=512, W=512, dim=96, z_dim=16):
+    """Conv/attention FLOPs (2/MAC) of a whole-clip VAE encode of T = 1+4k frames (107.2 TFLOP at
+    81 x 512 x 512); walks stableavatar_amd.vae.encoder_layout."""
+    from .vae import encoder_layout
+    fl = 0
+    t, hh, ww = T, H, W
+    for kind, _name, cin, cout in encoder_layout(dim):
+        n = t * hh * ww
+        if kind == "conv":
+            fl += 2 * n * 27 * cin * cout
+        elif kind == "res":
+            fl += 2 * n * 27 * (cin * cout + cout * cout) + (2 * n * cin * cout if cin != cout else 0)
+        elif kind == "attn":
+            fl += 2 * n * cin * cin * 4 + 4 * t * (hh * ww) ** 2 * cin
+        elif kind in ("down2d", "down3d"):
+            hh, ww = hh // 2, ww // 2
+            fl += 2 * t * hh * ww * 9 * cin * cout
+            if kind == "down3d":
+                t = 1 + (t - 1) // 2
+                fl += 2 * (t - 1) * hh * ww * 3 * cout * cout
+        elif kind == "head":
+            fl += 2 * n * 27 * cin * 2 * z_dim
+    return fl + 2 * t * hh * ww * (2 * z_dim) ** 2

@@ -1,11 +1,12 @@
-"""Drop-in AutoencoderKLWan decode for MI355X (reference: wan/models/wan_vae.py).
+"""Drop-in AutoencoderKLWan for MI355X (reference: wan/models/wan_vae.py).
 
-Same state_dict keys ('model.conv2.*', 'model.decoder.*'), `from_pretrained(path, additional_kwargs)`
-and `decode(z, return_dict=True) -> DecoderOutput(sample=...)` as the reference.  The decoder runs
-over the whole clip at once (equivalent to the reference's frame-by-frame causal cache, see
-oracle/vae.py) with channels-last bf16 activations and every conv as an MFMA implicit GEMM.
-Encoding (reference-frame conditioning, once per call) is SURVEY.md §8(f) "next" and not part of
-this hot path.
+Same state_dict keys ('model.conv1/conv2.*', 'model.encoder.*', 'model.decoder.*'),
+`from_pretrained(path, additional_kwargs)`, `decode(z, return_dict=True) -> DecoderOutput(sample=...)`
+and `encode(x, return_dict=True) -> AutoencoderKLOutput(latent_dist=...)` (`encode(x)[0].mode()` as the
+pipeline calls it, wan_inference_long_pipeline.py:414-415) as the reference.  Decoder and encoder run
+over the whole clip at once (equivalent to the reference's chunked causal feature cache, see
+oracle/vae.py) with channels-last bf16 activations and every conv as an MFMA implicit GEMM.  The
+encoder (reference frame + zeros, once per call) is SURVEY.md §8(f) row 1.
 """
 from __future__ import annotations
 
@@ -82,6 +83,61 @@ def param_shapes(dim=96, z_dim=16):
     return S
 
 
+def encoder_layout(dim=96, dim_mult=(1, 2, 4, 4), num_res_blocks=2, temperal_downsample=(False, True, True)):
+    """Module list of Encoder3d (wan_vae.py:268-319): (kind, name, in, out)."""
+    dims = [dim * u for u in [1] + list(dim_mult)]
+    L = [("conv", "conv1", 3, dims[0])]
+    k = 0
+    for i, (din, dout) in enumerate(zip(dims[:-1], dims[1:])):
+        for _ in range(num_res_blocks):
+            L.append(("res", f"downsamples.{k}", din, dout))
+            k += 1
+            din = dout
+        if i != len(dim_mult) - 1:
+            L.append(("down3d" if temperal_downsample[i] else "down2d", f"downsamples.{k}", dout, dout))
+            k += 1
+    L += [("res", "middle.0", dims[-1], dims[-1]), ("attn", "middle.1", dims[-1], dims[-1]),
+          ("res", "middle.2", dims[-1], dims[-1]), ("head", "head", dims[-1], None)]
+    return L
+
+
+def encoder_param_shapes(dim=96, z_dim=16):
+    """{key: shape} of the encode half of AutoencoderKLWan ('model.conv1', 'model.encoder.*')."""
+    S = {"model.conv1.weight": (2 * z_dim, 2 * z_dim, 1, 1, 1), "model.conv1.bias": (2 * z_dim,)}
+    for kind, name, cin, cout in encoder_layout(dim):
+        q = "model.encoder." + name
+        if kind == "conv":
+            S[q + ".weight"] = (cout, cin, 3, 3, 3)
+            S[q + ".bias"] = (cout,)
+        elif kind == "res":
+            S[q + ".residual.0.gamma"] = (cin, 1, 1, 1)
+            S[q + ".residual.2.weight"] = (cout, cin, 3, 3, 3)
+            S[q + ".residual.2.bias"] = (cout,)
+            S[q + ".residual.3.gamma"] = (cout, 1, 1, 1)
+            S[q + ".residual.6.weight"] = (cout, cout, 3, 3, 3)
+            S[q + ".residual.6.bias"] = (cout,)
+            if cin != cout:
+                S[q + ".shortcut.weight"] = (cout, cin, 1, 1, 1)
+                S[q + ".shortcut.bias"] = (cout,)
+        elif kind == "attn":
+            S[q + ".norm.gamma"] = (cin, 1, 1)
+            S[q + ".to_qkv.weight"] = (cin * 3, cin, 1, 1)
+            S[q + ".to_qkv.bias"] = (cin * 3,)
+            S[q + ".proj.weight"] = (cin, cin, 1, 1)
+            S[q + ".proj.bias"] = (cin,)
+        elif kind in ("down2d", "down3d"):
+            S[q + ".resample.1.weight"] = (cout, cin, 3, 3)
+            S[q + ".resample.1.bias"] = (cout,)
+            if kind == "down3d":
+                S[q + ".time_conv.weight"] = (cout, cout, 3, 1, 1)
+                S[q + ".time_conv.bias"] = (cout,)
+        elif kind == "head":
+            S[q + ".0.gamma"] = (cin, 1, 1, 1)
+            S[q + ".2.weight"] = (2 * z_dim, cin, 3, 3, 3)
+            S[q + ".2.bias"] = (2 * z_dim,)
+    return S
+
+
 def _cout_pad(cout):
     if cout > 96:
         return ((cout + 191) // 192) * 192
@@ -112,6 +168,32 @@ class DecoderOutput:
         self.sample = sample
 
 
+class DiagonalGaussianDistribution:
+    """diffusers' posterior over h = cat(mean, logvar) (wan_vae.py:656); the pipeline uses .mode()."""
+
+    def __init__(self, parameters):
+        self.parameters = parameters
+        self.mean, self.logvar = torch.chunk(parameters, 2, dim=1)
+        self.logvar = torch.clamp(self.logvar, -30.0, 20.0)
+        self.std = torch.exp(0.5 * self.logvar)
+        self.var = torch.exp(self.logvar)
+
+    def mode(self):
+        return self.mean
+
+    def sample(self, generator=None):
+        noise = torch.randn(self.mean.shape, generator=generator, dtype=self.mean.dtype).to(self.mean.device)
+        return self.mean + self.std * noise
+
+
+class AutoencoderKLOutput:
+    def __init__(self, latent_dist):
+        self.latent_dist = latent_dist
+
+    def __getitem__(self, i):
+        return (self.latent_dist,)[i]
+
+
 class AutoencoderKLWan(nn.Module):
     """wan_vae.py:619-704, decode path on HIP kernels."""
 
@@ -123,7 +205,8 @@ class AutoencoderKLWan(nn.Module):
         self.z_dim, self.dim = latent_channels, dim
         self.mean = torch.tensor(MEAN, dtype=torch.float32)
         self.std = torch.tensor(STD, dtype=torch.float32)
-        for name, shp in param_shapes(dim, latent_channels).items():
+        shapes = dict(param_shapes(dim, latent_channels), **encoder_param_shapes(dim, latent_channels))
+        for name, shp in shapes.items():
             *path, leaf = name.split(".")
             mod = self
             for p in path:
@@ -132,6 +215,7 @@ class AutoencoderKLWan(nn.Module):
                 mod = getattr(mod, p)
             mod.register_parameter(leaf, nn.Parameter(torch.empty(shp), requires_grad=False))
         self._packed = None
+        self._packed_enc = None
 
     @property
     def dtype(self):
@@ -152,16 +236,12 @@ class AutoencoderKLWan(nn.Module):
         return model
 
     def load_state_dict(self, state_dict, strict=True, assign=False):
-        self._packed = None
+        self._packed = self._packed_enc = None
         return super().load_state_dict(state_dict, strict=strict, assign=assign)
 
     def _apply(self, fn, recurse=True):
-        self._packed = None
+        self._packed = self._packed_enc = None
         return super()._apply(fn, recurse)
-
-    def encode(self, x, return_dict=True):
-        raise NotImplementedError("VAE encode (reference-frame conditioning, once per call) is SURVEY.md §8(f) "
-                                  "'next'; pass the conditioning latents `y` directly")
 
     # ------------------------------------------------------------------ packing
 
@@ -201,6 +281,45 @@ class AutoencoderKLWan(nn.Module):
                 e.conv = _pack_conv(P[q + ".2.weight"], P[q + ".2.bias"], cout_store=4)
             pk.layers.append(e)
         self._packed = pk
+        return pk
+
+    def _pack_enc(self):
+        if self._packed_enc is not None:
+            return self._packed_enc
+        dev = self.model.conv1.weight.device
+        if dev.type != "cuda":
+            raise RuntimeError("AutoencoderKLWan.encode runs on the MI355X HIP kernels: move it to 'cuda'")
+        P = dict(self.named_parameters())
+        g = lambda n: P[n].detach().float().reshape(-1).contiguous()  # noqa: E731
+        z2 = 2 * self.z_dim
+        pk = SimpleNamespace(layers=[], mean=self.mean.to(dev), std=self.std.to(dev),
+                             zero3=torch.zeros(3, device=dev), one3=torch.ones(3, device=dev))
+        pk.conv1 = _pack_conv(P["model.conv1.weight"], P["model.conv1.bias"])
+        for kind, name, cin, cout in encoder_layout(self.dim):
+            q = "model.encoder." + name
+            e = SimpleNamespace(kind=kind, cin=cin, cout=cout)
+            if kind == "conv":  # 3 input channels, zero-padded to the 32-deep K step
+                e.conv = _pack_conv(P[q + ".weight"], P[q + ".bias"], cin_pad=32)
+            elif kind == "res":
+                e.g0, e.g3 = g(q + ".residual.0.gamma"), g(q + ".residual.3.gamma")
+                e.c1 = _pack_conv(P[q + ".residual.2.weight"], P[q + ".residual.2.bias"])
+                e.c2 = _pack_conv(P[q + ".residual.6.weight"], P[q + ".residual.6.bias"])
+                e.sc = (_pack_conv(P[q + ".shortcut.weight"], P[q + ".shortcut.bias"])
+                        if q + ".shortcut.weight" in P else None)
+            elif kind == "attn":
+                e.g = g(q + ".norm.gamma")
+                e.qkv = _pack_conv(P[q + ".to_qkv.weight"], P[q + ".to_qkv.bias"])
+                e.proj = _pack_conv(P[q + ".proj.weight"], P[q + ".proj.bias"])
+            elif kind in ("down2d", "down3d"):
+                e.rs = _pack_conv(P[q + ".resample.1.weight"], P[q + ".resample.1.bias"])
+                if kind == "down3d":
+                    e.tc = _pack_conv(P[q + ".time_conv.weight"], P[q + ".time_conv.bias"])
+            elif kind == "head":
+                e.g = g(q + ".0.gamma")
+                e.conv = _pack_conv(P[q + ".2.weight"], P[q + ".2.bias"])
+                assert e.conv.cout == z2
+            pk.layers.append(e)
+        self._packed_enc = pk
         return pk
 
     # ------------------------------------------------------------------ kernels
@@ -264,6 +383,64 @@ class AutoencoderKLWan(nn.Module):
             self._conv(x[1:], T - 1, H, W, e.tc, out=u[1:], interleave=C)
             x, T = u, 1 + 2 * (T - 1)
         return self._conv(x, T, 2 * H, 2 * W, e.rs, upsample=True), T, 2 * H, 2 * W
+
+    @staticmethod
+    def _down(e, x, T, H, W):
+        """Resample downsample2d/3d (wan_vae.py:91-100, :142-157) in whole-clip form: stride-2 3x3
+        conv with right/bottom zero padding per frame; 3d: frame 0 kept, frames 1.. = stride-2
+        time_conv over frames (2j-2, 2j-1, 2j)."""
+        C = x.shape[-1]
+        y = torch.empty(T, H // 2, W // 2, e.rs.cout, device=x.device, dtype=torch.bfloat16)
+        call("sa_conv3d_cl_down", x.data_ptr(), T, H, W, C, 1, e.rs.w.data_ptr(), e.rs.b.data_ptr(), e.rs.cout,
+             e.rs.cout_pad, y.data_ptr(), ops._stream())
+        H, W = H // 2, W // 2
+        if e.kind == "down3d" and T > 1:
+            To = 1 + (T - 1) // 2
+            z = torch.empty(To, H, W, e.tc.cout, device=x.device, dtype=torch.bfloat16)
+            z[0].copy_(y[0])
+            call("sa_conv3d_cl_down", y.data_ptr(), To - 1, H, W, e.rs.cout, 2, e.tc.w.data_ptr(), e.tc.b.data_ptr(),
+                 e.tc.cout, e.tc.cout_pad, z[1:].data_ptr(), ops._stream())
+            y, T = z, To
+        return y, T, H, W
+
+    def encode_clip(self, v):
+        """v [3, T, H, W] (T = 1 + 4k, H, W multiples of 8) -> [32, 1 + k, H/8, W/8] fp32 =
+        cat((mu - mean) / std, log_var) (AutoencoderKLWan_.encode, wan_vae.py:519-547)."""
+        pk = self._pack_enc()
+        dev = pk.mean.device
+        C3, T, H, W = v.shape
+        if C3 != 3 or (T - 1) % 4 or H % 8 or W % 8:
+            raise ValueError(f"encode expects [3, 1+4k, 8h, 8w] frames, got {tuple(v.shape)}")
+        vc = v.to(device=dev, dtype=torch.float32).contiguous()
+        x = torch.empty(T, H, W, 32, device=dev, dtype=torch.bfloat16)
+        call("sa_vae_input", vc.data_ptr(), 3, T * H * W, pk.zero3.data_ptr(), pk.one3.data_ptr(), x.data_ptr(), 32,
+             ops._stream())
+        for e in pk.layers:
+            if e.kind == "conv":
+                x = self._conv(x, T, H, W, e.conv)
+            elif e.kind == "res":
+                x = self._res(e, x, T, H, W)
+            elif e.kind == "attn":
+                x = self._attn(e, x, T, H, W)
+            elif e.kind in ("down2d", "down3d"):
+                x, T, H, W = self._down(e, x, T, H, W)
+            elif e.kind == "head":
+                y = self._rms(x, e.g, True)
+                x = self._conv(y, T, H, W, e.conv)
+        h = self._conv(x, T, H, W, pk.conv1, out_f32=True)
+        out = torch.empty(2 * self.z_dim, T, H, W, device=dev, dtype=torch.float32)
+        call("sa_vae_latent_out", h.data_ptr(), h.shape[-1], self.z_dim, T * H * W, pk.mean.data_ptr(),
+             pk.std.data_ptr(), out.data_ptr(), ops._stream())
+        return out
+
+    def encode(self, x, return_dict=True):
+        """wan_vae.py:650-660: [B, 3, 1+4k, H, W] -> AutoencoderKLOutput(latent_dist=posterior over
+        cat(mu, log_var) [B, 32, 1+k, H/8, W/8]); the pipeline takes encode(x)[0].mode()."""
+        h = torch.stack([self.encode_clip(u) for u in x])
+        post = DiagonalGaussianDistribution(h)
+        if not return_dict:
+            return (post,)
+        return AutoencoderKLOutput(latent_dist=post)
 
     def decode_clip(self, z, post=False):
         """z [16, T, h, w] fp32 (one batch item) -> [3, 1+4(T-1), 8h, 8w] fp32 in [-1,1]

@@ -11,7 +11,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "golden"))
 
-from golden_cases import PIPE, VAE_SMALL, pipe_fixed_inputs, vae_latent  # noqa: E402
+from golden_cases import PIPE, VAE_ENC_SMALL, VAE_SMALL, pipe_fixed_inputs, vae_latent, vae_video  # noqa: E402
 
 from stableavatar_amd import synthetic  # noqa: E402
 
@@ -31,9 +31,10 @@ def psnr(a, b, peak):
 
 
 def make_vae(dim, seed):
-    from stableavatar_amd.vae import AutoencoderKLWan, param_shapes
+    from stableavatar_amd.vae import AutoencoderKLWan, encoder_param_shapes, param_shapes
     v = AutoencoderKLWan(dim=dim)
-    v.load_state_dict(synthetic.fill_state_dict(param_shapes(dim=dim), seed), strict=True)
+    shapes = dict(param_shapes(dim=dim), **encoder_param_shapes(dim=dim))
+    v.load_state_dict(synthetic.fill_state_dict(shapes, seed), strict=True)
     return v.cuda()
 
 
@@ -48,6 +49,37 @@ def test_vae_decode_vs_reference(name):
     assert tuple(out.shape) == g.shape
     # outputs live in [-1, 1]: PSNR over a peak-to-peak range of 2
     assert psnr(out, g, 2.0) > 40.0 and rel(out, g) < 3e-2, (psnr(out, g, 2.0), rel(out, g))
+
+
+@pytest.mark.parametrize("name", list(VAE_ENC_SMALL))
+def test_vae_encode_vs_reference(name):
+    """HIP encoder (whole clip, bf16 activations) vs the reference's chunked fp32 encode: the
+    posterior parameters cat(mu, log_var) within rel-L2 3e-2 and .mode() == mu."""
+    cfg = VAE_ENC_SMALL[name]
+    v = make_vae(cfg["dim"], cfg["seed"])
+    with torch.no_grad():
+        post = v.encode(vae_video(cfg).cuda())[0]
+        h = post.parameters
+        mode = post.mode()
+    torch.cuda.synchronize()
+    g = G("vae_enc_small.npz")[name]
+    assert tuple(h.shape) == g.shape
+    assert torch.equal(mode, h[:, :16])
+    assert rel(h, g) < 3e-2, rel(h, g)
+
+
+def test_vae_encode_full_frame_shape_and_causality():
+    """512x512-class property at a GPU-sized clip (dim 96, 33 frames at 128x128): output shape, and
+    causality - frames after t change no latent frame before their chunk (encode of a prefix == the
+    same prefix of the full encode, up to bf16 reordering noise)."""
+    v = make_vae(96, 23)
+    x = (0.5 * synthetic.seeded_normal((1, 3, 33, 128, 128), 333)).clamp(-1, 1).cuda()
+    with torch.no_grad():
+        full = v.encode(x)[0].parameters
+        pre = v.encode(x[:, :, :17])[0].parameters
+    torch.cuda.synchronize()
+    assert tuple(full.shape) == (1, 32, 9, 16, 16) and torch.isfinite(full).all()
+    assert rel(pre, full[:, :, :5]) < 1e-6, rel(pre, full[:, :, :5])
 
 
 def test_pipeline_vs_reference():
