@@ -7,6 +7,7 @@
 //    then the 3-D complex RoPE (1B:295-323) with fp64-derived fp32 (cos,sin) tables; tokens past
 //    f*h*w (padding) are left unrotated (1B:319).  In place on the fused QKV GEMM output.
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -180,6 +181,80 @@ __global__ __launch_bounds__(256) void qk_rmsnorm_rope_kernel(QkArgs a) {
   if (a.k_col >= 0) rms_rope_one(base + a.k_col, a.wk, a, lane, fi, hi_, wi, rot);
 }
 
+// Self-attention case (C = 1536 = 3 x 512, head_dim 128, q and k, 3-D RoPE): one wave per token row
+// loads q and k together (six 16-byte loads in flight), reduces both sums of squares in one
+// butterfly, and applies RoPE with this lane's 4 (cos, sin) pairs, which are the same for every
+// head chunk of the row ((i*512 + lane*8) % 128 does not depend on i) and for q and k.
+__device__ __forceinline__ float2 wave_sum2(float2 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    v.x += __shfl_xor(v.x, o, 64);
+    v.y += __shfl_xor(v.y, o, 64);
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(256) void qk_rmsnorm_rope_pair_kernel(QkArgs a) {
+  constexpr int NCH = 3, HD = 128;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= a.M) return;
+  bf16* qp = a.x + (long)row * a.ldx + a.q_col + lane * 8;
+  bf16* kp = a.x + (long)row * a.ldx + a.k_col + lane * 8;
+  float q[NCH][8], k[NCH][8];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    load8<bf16>(qp + i * 512, q[i]);
+    load8<bf16>(kp + i * 512, k[i]);
+  }
+  float cs[4], sn[4];
+  const int t = a.tok_offset + row % a.rows_per_batch;
+  const bool rot = t < a.F * a.H * a.W;
+  {
+    const int fi = t / (a.H * a.W), hi_ = (t / a.W) % a.H, wi = t % a.W;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pi = ((lane * 8) % HD) / 2 + j;
+      const int pos = pi < a.nf ? fi : (pi < a.nf + a.nh ? hi_ : wi);
+      const float2 c = rot ? *(const float2*)(a.rope + (pos * (HD / 2) + pi) * 2) : make_float2(1.f, 0.f);
+      cs[j] = c.x;
+      sn[j] = c.y;
+    }
+  }
+  float2 ss = make_float2(0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ss.x += q[i][j] * q[i][j];
+      ss.y += k[i][j] * k[i][j];
+    }
+  ss = wave_sum2(ss);
+  const float rq = rsqrtf(ss.x / (NCH * 512) + a.eps), rk = rsqrtf(ss.y / (NCH * 512) + a.eps);
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c0 = i * 512 + lane * 8;
+    float wq[8], wk[8], yq[8], yk[8];
+    load8<float>(a.wq + c0, wq);
+    load8<float>(a.wk + c0, wk);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      yq[j] = q[i][j] * rq * wq[j];
+      yk[j] = k[i][j] * rk * wk[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float qr = yq[2 * j], qi = yq[2 * j + 1], kr = yk[2 * j], ki = yk[2 * j + 1];
+      yq[2 * j] = qr * cs[j] - qi * sn[j];
+      yq[2 * j + 1] = qr * sn[j] + qi * cs[j];
+      yk[2 * j] = kr * cs[j] - ki * sn[j];
+      yk[2 * j + 1] = kr * sn[j] + ki * cs[j];
+    }
+    store8<bf16>(qp + i * 512, yq);
+    store8<bf16>(kp + i * 512, yk);
+  }
+}
+
 template <typename TI, typename TO>
 int launch_ln(const LnArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((layernorm_mod_kernel<TI, TO>), dim3((a.M + 3) / 4), dim3(256), 0, st, a);
@@ -217,7 +292,10 @@ extern "C" int sa_qk_rmsnorm_rope(void* x, int64_t ldx, int q_col, int k_col, co
   if (rope && (rows_per_batch <= 0 || head_dim % 8 || F <= 0 || H <= 0 || W <= 0)) return SA_ERR_ARG;
   QkArgs a{(bf16*)x, ldx, q_col, k_col, wq, wk, M, C, head_dim, eps, rope, rows_per_batch > 0 ? rows_per_batch : 1,
            tok_offset, F, H, W, n_frame_pairs, n_height_pairs};
-  hipLaunchKernelGGL(qk_rmsnorm_rope_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
+  if (rope && k_col >= 0 && C == 1536 && head_dim == 128 && getenv("SA_QK_GENERIC") == nullptr)
+    hipLaunchKernelGGL(qk_rmsnorm_rope_pair_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(qk_rmsnorm_rope_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
   SA_LAUNCH_CHECK();
   return SA_OK;
 }

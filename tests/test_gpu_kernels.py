@@ -260,6 +260,33 @@ def test_qk_rmsnorm_rope():
     assert torch.equal(x[:, 2 * C:], qkv[:, 2 * C:])
 
 
+@pytest.mark.parametrize("tok_offset", [0, 37])
+def test_qk_rmsnorm_rope_pair_matches_generic(tok_offset, monkeypatch):
+    """The fused q+k kernel (C=1536, D=128) agrees with the generic per-tensor kernel to one bf16 ulp,
+    incl. an SP token offset and padded (unrotated) rows."""
+    from stableavatar_amd import ops
+    from stableavatar_amd.transformer import rope_table
+    F, H, W, C = 3, 4, 6, 1536
+    L = F * H * W + 8
+    qkv = torch.randn(2 * L, 3 * C, device=dev).bfloat16()
+    wq, wk = torch.randn(C, device=dev), torch.randn(C, device=dev)
+    rope = rope_table(128).to(dev)
+    outs = []
+    for generic in (False, True):
+        if generic:
+            monkeypatch.setenv("SA_QK_GENERIC", "1")
+        x = qkv.clone()
+        ops.qk_rmsnorm_rope(x, 0, C, wq, wk, C, 1e-6, rope=rope, rows_per_batch=L, tok_offset=tok_offset,
+                            grid=(F, H, W), n_frame_pairs=22, n_height_pairs=21)
+        torch.cuda.synchronize()
+        outs.append(x)
+    # same math; FMA contraction may differ, so an element may round to the neighbouring bf16 value
+    diff = (outs[0].float() - outs[1].float()).abs()
+    assert rel(outs[0].float(), outs[1].float()) < 1e-3
+    assert (diff > 0).float().mean().item() < 0.05
+    assert (diff <= outs[1].float().abs() * 2 ** -7 + 1e-6).all()
+
+
 def test_patchify_roundtrip():
     from stableavatar_amd import ops
     B, F, H, W = 3, 2, 8, 12
