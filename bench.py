@@ -40,6 +40,12 @@ def parse():
     p.add_argument("--sp", action="store_true",
                    help="N>1: one clip sequence-parallel over all ranks (Ulysses, strong scaling) instead of "
                         "one clip per rank (replicas, weak scaling)")
+    p.add_argument("--window-dp", action="store_true",
+                   help="N>1: one long clip with its sliding windows spread over the ranks (window parallelism, "
+                        "strong scaling; use with --video-frames)")
+    p.add_argument("--video-frames", type=int, default=None,
+                   help="length of the generated video (default: --frames, i.e. one window); e.g. 165 = the "
+                        "examples/case-1 shape (42 latent frames, 5 windows per step at overlap 15)")
     return p.parse_args()
 
 
@@ -58,13 +64,14 @@ def build(dev, seed=0):
     return dit, vae
 
 
-def make_inputs(dev, frames, size, seed):
-    T = (frames - 1) // 4 + 1
+def make_inputs(dev, frames, size, seed, video_frames=None):
+    T = ((video_frames or frames) - 1) // 4 + 1
+    fpb = (frames - 1) // 4 + 1
     h = size // 8
     g = torch.Generator().manual_seed(seed)
     latents = torch.randn(1, 16, T, h, h, generator=g).to(dev).bfloat16()  # CPU noise, injected (App. A.13)
     gd = torch.Generator(device=dev).manual_seed(seed + 1)
-    y = torch.randn(3, 20, T, h, h, device=dev, generator=gd).bfloat16()
+    y = torch.randn(3, 20, fpb, h, h, device=dev, generator=gd).bfloat16()
     ctx = [torch.randn(n, 4096, device=dev, generator=gd) for n in (126, 126, 48)]
     ctx[1] = ctx[0]
     clip = torch.randn(1, 257, 1280, device=dev, generator=gd).expand(3, -1, -1).contiguous()
@@ -73,7 +80,7 @@ def make_inputs(dev, frames, size, seed):
     return latents, y, ctx, clip, a
 
 
-def cpu_baseline(size, frames, sample_steps):
+def cpu_baseline(size, frames, sample_steps, n_fwd=None, out_frames=None):
     """Time the CPU oracle (fp32 restatement, oracle/) on a bounded sample of the same workload:
     one of the 30 DiT blocks at the full config-2 shape and the VAE decoder on one latent frame,
     then extrapolate to the clip (50 steps x 30 blocks + 81-frame decode)."""
@@ -102,11 +109,13 @@ def cpu_baseline(size, frames, sample_steps):
         t0 = time.time()
         ovae.decode(Pv, z)
         t_vae_frame = time.time() - t0
-    t_clip = sample_steps * 30 * t_block + frames * t_vae_frame
-    return {"value": round(frames / t_clip, 6), "unit": "frames/s", "cores": threads, "kind": "port",
+    n_fwd = n_fwd or sample_steps
+    out_frames = out_frames or frames
+    t_clip = n_fwd * 30 * t_block + out_frames * t_vae_frame
+    return {"value": round(out_frames / t_clip, 6), "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": f"oracle fp32: 1 of 30 DiT blocks at B=3,L={L} ({t_block:.1f}s) + VAE decode of 1 latent "
-                      f"frame at {size}x{size} ({t_vae_frame:.1f}s), extrapolated to {sample_steps} steps x 30 "
-                      f"blocks + {frames} frames = {t_clip:.0f}s per clip"}
+                      f"frame at {size}x{size} ({t_vae_frame:.1f}s), extrapolated to {n_fwd} forwards x 30 "
+                      f"blocks + {out_frames} frames = {t_clip:.0f}s per clip"}
 
 
 def main():
@@ -126,13 +135,19 @@ def main():
     from stableavatar_amd.scheduler import FlowMatchEulerDiscreteScheduler
 
     sp_mode = args.sp and world > 1
+    wdp = args.window_dp and world > 1
+    if sp_mode and wdp:
+        raise SystemExit("--sp and --window-dp are exclusive")
     dit, vae = build(dev, seed=0)
     if sp_mode:
         dit.enable_multi_gpus_inference()
-    latents, y, ctx, clip, a = make_inputs(dev, args.frames, args.size, seed=42 + (0 if sp_mode else rank))
+    latents, y, ctx, clip, a = make_inputs(dev, args.frames, args.size, seed=42 + (0 if sp_mode or wdp else rank),
+                                           video_frames=args.video_frames)
     sched = FlowMatchEulerDiscreteScheduler(1000, shift=5.0)
     sched.set_timesteps(args.sample_steps, device=dev)
     pipe = WanI2VTalkingInferenceLongPipeline(vae=vae, transformer=dit, scheduler=sched)
+    if wdp:
+        pipe.enable_window_parallel()
     T = latents.shape[2]
     fpb = (args.frames - 1) // 4 + 1
     feats = {(s, e): torch.cat([torch.zeros_like(a), a, a]) for (s, e, _) in window_schedule(T, fpb, args.overlap)}
@@ -163,7 +178,8 @@ def main():
         dt = time.perf_counter() - t0
         events = dit._events
         dit._events = None
-    assert video.shape[1] == args.frames and torch.isfinite(video).all()
+    out_frames = 1 + 4 * (T - 1)
+    assert video.shape[1] == out_frames and torch.isfinite(video).all()
     enc = None
     if not args.no_encode:  # once-per-call VAE encode of reference frame + zeros (pipeline:679-692), untimed
         ref = torch.zeros(1, 3, args.frames, args.size, args.size, device=dev)
@@ -195,6 +211,8 @@ def main():
         traffic = tj["hbm_bytes_per_launch"]
         traffic_src = f"profiles/pmc_attn_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, {tj['kernel'][:60]})"
     parallelism = f"replicas{world}" if world > 1 else "single"
+    if wdp:
+        parallelism = f"windows{world}"
     if sp_mode:
         from stableavatar_amd import sp
         plan = sp.make_plan(world, rank, 12)
@@ -203,27 +221,29 @@ def main():
     achieved = attn_flop / (attn_ms * 1e-3)
     n_fwd = args.sample_steps * len(window_schedule(T, fpb, args.overlap))
     path_flop = n_fwd * flops.dit_forward_flops(B=3, L=seq_len, n_frames=fpb) + flops.vae_decode_flops(T, h, h)
-    frames_total = (1 if sp_mode else world) * args.frames * args.steps
+    frames_total = (1 if sp_mode or wdp else world) * out_frames * args.steps
     value = frames_total / dt
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.size, args.frames, args.sample_steps)
+            cpu = cpu_baseline(args.size, args.frames, args.sample_steps, n_fwd, out_frames)
         out = {"metric": METRIC, "value": round(value, 4), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 1), "higher_is_better": True,
-               "scaling": "strong" if sp_mode else "weak", "vs_baseline": None, "dtype": "bf16",
+               "scaling": "strong" if sp_mode or wdp else "weak", "vs_baseline": None, "dtype": "bf16",
                "data": "synthetic (random-init weights by name-keyed seed; synthetic text/CLIP/wav2vec features "
                        "and conditioning latents; CPU-generated initial noise)",
-               "config": {"workload": f"Wan-1.3B StableAvatar {args.size}x{args.size}x{args.frames}f, "
-                                      f"{args.sample_steps} steps, CFG x3, single audio clip, VAE decode",
-                          "global_batch": 3 * (1 if sp_mode else world), "seq_len": seq_len,
+               "config": {"workload": f"Wan-1.3B StableAvatar {args.size}x{args.size}x{out_frames}f"
+                                      + (f" ({len(window_schedule(T, fpb, args.overlap))} windows of {args.frames}f,"
+                                         f" overlap {args.overlap})" if out_frames != args.frames else "")
+                                      + f", {args.sample_steps} steps, CFG x3, single audio clip, VAE decode",
+                          "global_batch": 3 * (1 if sp_mode or wdp else world), "seq_len": seq_len,
                           "dit_forwards_per_clip": n_fwd, "parallelism": parallelism},
                "roofline": {"bound": "mfma", "kernel": "attn_fwd (self-attention, flash, D=128)",
                             "achieved": round(achieved / 1e12, 1), "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
                             "frac": round(achieved / PEAK_BF16, 4), "traffic": traffic, "traffic_source": traffic_src,
                             "algorithmic_bytes": 4 * 3 * seq_len * 1536 * 2,
                             "launch_ms": round(attn_ms, 3), "flop_per_launch": attn_flop},
-               "path_mfma_frac": round(path_flop * args.steps / dt / PEAK_BF16 / (world if sp_mode else 1), 4),
+               "path_mfma_frac": round(path_flop * args.steps / dt / PEAK_BF16 / (world if sp_mode or wdp else 1), 4),
                "cpu_baseline": cpu, "vae_encode": enc}
         print(json.dumps(out), flush=True)
     if world > 1:

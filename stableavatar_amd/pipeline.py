@@ -77,7 +77,19 @@ class WanI2VTalkingInferenceLongPipeline:
         self.clip_image_encoder, self.scheduler = clip_image_encoder, scheduler
         self.wav2vec_processor, self.wav2vec = wav2vec_processor, wav2vec
         self.vae_encoder = None  # optional module with .encode() for the reference frame (§8(f))
+        self.window_group = None  # set by enable_window_parallel()
         self.device = torch.device("cuda")
+
+    def enable_window_parallel(self, group=None):
+        """Split the sliding windows of every step over the ranks of ``group`` (default: the
+        torch.distributed world, RCCL).  All windows of a step read only latents_all (:726), so
+        each rank runs the DiT on windows k = rank, rank + N, ..; the noise predictions are
+        all-gathered (one async collective per round of N windows, overlapping the next round's
+        forward) and every rank applies the CFG / Euler / blend steps of all windows in the
+        reference order -- bit-identical latents on every rank and to the single-GPU loop."""
+        import torch.distributed as dist
+        self.window_group = group if group is not None else dist.group.WORLD
+        return self
 
     def to(self, device=None, **_):
         if device is not None:
@@ -145,6 +157,10 @@ class WanI2VTalkingInferenceLongPipeline:
         pred = torch.empty_like(lat)
         yb = y.to(device=dev, dtype=torch.bfloat16).contiguous()
         sig = [float(s) for s in sigmas]
+        if self.window_group is not None:
+            return self._denoise_window_parallel(lat, pred, yb, context, clip_context, window_features, timesteps,
+                                                 sig, wins, wts, cfg, fpb, clip_length, seq_len, overlap,
+                                                 text_guide_scale, audio_guide_scale, callback)
         for i, t in enumerate(timesteps):
             pred.zero_()
             tt = torch.as_tensor(t, dtype=torch.float32, device=dev).reshape(1)
@@ -155,6 +171,47 @@ class WanI2VTalkingInferenceLongPipeline:
                                                         clip_length)
                 blend = s != 0 and i != 0
                 ops.flow_step(lat, pred, noise, s, sig[i + 1] - sig[i], audio_guide_scale or 0.0,
+                              text_guide_scale or 0.0, overlap if blend else 0, pe, wts if blend else None, blend)
+            lat, pred = pred, lat
+            if callback is not None:
+                callback(i, t, lat)
+        return lat
+
+    def _denoise_window_parallel(self, lat, pred, yb, context, clip_context, window_features, timesteps, sig, wins,
+                                 wts, cfg, fpb, clip_length, seq_len, overlap, text_guide_scale, audio_guide_scale,
+                                 callback):
+        import torch.distributed as dist
+
+        from . import sp
+        grp = self.window_group
+        N, r = dist.get_world_size(grp), dist.get_rank(grp)
+        dev = lat.device
+        R = 3 if cfg else 1
+        C, H, W = lat.shape[1], lat.shape[3], lat.shape[4]
+        rounds = -(-len(wins) // N)
+        slots = torch.empty(rounds * N, R * C * fpb * H * W, device=dev, dtype=torch.bfloat16)
+
+        def view(k):
+            Fw = wins[k][1] - wins[k][0]
+            return slots[k, :R * C * Fw * H * W].view(R, C, Fw, H, W)
+
+        for i, t in enumerate(timesteps):
+            pred.zero_()
+            tt = torch.as_tensor(t, dtype=torch.float32, device=dev).reshape(1)
+            pend = []
+            for j in range(rounds):
+                k = j * N + r
+                if k < len(wins):
+                    s, e, _ = wins[k]
+                    self.transformer.forward_window(lat, s, True, R, tt, context, seq_len, clip_context,
+                                                    yb[:, :, :e - s], window_features[(s, e)], clip_length,
+                                                    out=view(k))
+                pend.append(sp.all_gather_slots(slots[j * N:(j + 1) * N], r, grp))
+            for p_ in pend:
+                p_.wait()
+            for k, (s, e, pe) in enumerate(wins):
+                blend = s != 0 and i != 0
+                ops.flow_step(lat, pred, view(k), s, sig[i + 1] - sig[i], audio_guide_scale or 0.0,
                               text_guide_scale or 0.0, overlap if blend else 0, pe, wts if blend else None, blend)
             lat, pred = pred, lat
             if callback is not None:

@@ -248,6 +248,21 @@ class UlyssesExchange:
         return Pending(work, finish)
 
 
+def all_gather_slots(buf: torch.Tensor, rank: int, group=None) -> Pending:
+    """Window parallelism: buf [world, S]; row ``rank`` holds this rank's noise
+    prediction of one window, every row is filled on every rank once the Pending is waited on."""
+    mine = buf[rank:rank + 1]  # [1, S]: the output is gathered as [world, S]
+    if dist.get_backend(group) == "gloo":
+        if buf.is_cuda:  # host-staged (several ranks sharing one GPU in tests)
+            o = torch.empty(buf.shape, dtype=buf.dtype)
+            dist.all_gather_into_tensor(o, mine.cpu().contiguous(), group=group)
+            buf.copy_(o)
+        else:
+            dist.all_gather_into_tensor(buf, mine.clone(), group=group)
+        return Pending(None, None)
+    return Pending(dist.all_gather_into_tensor(buf, mine, group=group, async_op=True), None)
+
+
 def gather_tokens(local: torch.Tensor, B: int, Lc: int, world: int, group=None) -> torch.Tensor:
     """[B*Lc, C] chunk of every rank -> [B*Lp, C] (batch-major), on every rank (1B:1150-1152)."""
     C = local.shape[1]

@@ -111,3 +111,41 @@ def test_vocal_segments_use_global_frames(world):
     assert len(seen) == B * Lp
     for (b, gt), (k0, kl) in seen.items():
         assert k0 == (b * n_fr + gt // G) * nper and kl == nper
+
+
+def _slots_worker(rank, world, port, q_ret):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n_win, S = 5, 33
+        rounds = -(-n_win // world)
+        buf = torch.full((rounds * world, S), -1.0)
+        pend = []
+        for j in range(rounds):  # the window-parallel schedule of pipeline._denoise_window_parallel
+            k = j * world + rank
+            if k < n_win:
+                buf[k] = torch.arange(S, dtype=torch.float32) + 100 * k
+            pend.append(sp.all_gather_slots(buf[j * world:(j + 1) * world], rank))
+        for p in pend:
+            p.wait()
+        ok = all(torch.equal(buf[k], torch.arange(S, dtype=torch.float32) + 100 * k) for k in range(n_win))
+        q_ret.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_window_parallel_slot_gather(world):
+    """Every rank ends with every window's slot (5 windows: uneven rounds for both world sizes)."""
+    ctx = mp.get_context("spawn")
+    qret = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_slots_worker, args=(r, world, port, qret)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [qret.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok in res), res
