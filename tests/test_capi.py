@@ -60,3 +60,17 @@ def test_bad_arguments_are_rejected_without_gpu_work():
     assert L.sa_attn_fwd(None, None, None, None, None, 1, 1, 1, 128, 128, 128, 128, 128, 1.0, 0, None) == 1
     with pytest.raises(_lib.KernelError):
         _lib.call("sa_fill_f32", None, 10, 0.0, None)
+
+
+def test_encoder_entry_points_reject_bad_arguments():
+    """VAE-encode entry points (sa_conv3d_cl_down, sa_vae_latent_out) validate before launching."""
+    if not _lib.LIB_PATH.exists():
+        pytest.skip("library not built")
+    L = _lib.lib()
+    one = 16  # any non-null host address: rejected before it is dereferenced
+    assert L.sa_conv3d_cl_down(None, 1, 8, 8, 32, 1, one, one, 32, 96, one, None) == 1      # null input
+    assert L.sa_conv3d_cl_down(one, 1, 8, 8, 32, 3, one, one, 32, 96, one, None) == 1       # unknown mode
+    assert L.sa_conv3d_cl_down(one, 1, 7, 8, 32, 1, one, one, 32, 96, one, None) == 1       # odd H for stride 2
+    assert L.sa_conv3d_cl_down(one, 1, 8, 8, 3, 1, one, one, 32, 96, one, None) == 1        # Cin % 32
+    assert L.sa_vae_latent_out(None, 32, 16, 64, one, one, one, None) == 1
+    assert L.sa_vae_latent_out(one, 16, 16, 64, one, one, one, None) == 1                   # 2*Cz > C_stride
