@@ -52,18 +52,20 @@ struct LnArgs {
 
 constexpr int MAXV = 8;  // up to 8 chunks of 8 per lane -> C <= 4096
 
-template <typename TI, typename TO>
+// FIXED > 0: C == FIXED * 512 known at compile time (the DiT's C = 1536), so every chunk's loads are
+// unconditional and issue together; FIXED == 0: any C % 8 == 0 up to 4096.
+template <typename TI, typename TO, int FIXED = 0>
 __global__ __launch_bounds__(256) void layernorm_mod_kernel(LnArgs a) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= a.M) return;
   const TI* x = (const TI*)a.x + (long)row * a.ldx;
-  const int nch = (a.C + 511) / 512;
+  const int nch = FIXED ? FIXED : (a.C + 511) / 512;
   float v[MAXV][8];
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i)
-    if (i < nch && i * 512 + lane * 8 < a.C) {
+    if (i < nch && (FIXED || i * 512 + lane * 8 < a.C)) {
       load8<TI>(x + i * 512 + lane * 8, v[i]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += v[i][j];
@@ -72,7 +74,7 @@ __global__ __launch_bounds__(256) void layernorm_mod_kernel(LnArgs a) {
   float q = 0.f;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i)
-    if (i < nch && i * 512 + lane * 8 < a.C) {
+    if (i < nch && (FIXED || i * 512 + lane * 8 < a.C)) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) { const float d = v[i][j] - mean; q += d * d; }
     }
@@ -81,7 +83,7 @@ __global__ __launch_bounds__(256) void layernorm_mod_kernel(LnArgs a) {
   TO* out = (TO*)a.out + (long)row * a.ldo;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i)
-    if (i < nch && i * 512 + lane * 8 < a.C) {
+    if (i < nch && (FIXED || i * 512 + lane * 8 < a.C)) {
       const int c0 = i * 512 + lane * 8;
       float y[8], w8[8], b8[8], sc8[8], sh8[8], g8[8];
 #pragma unroll
@@ -118,14 +120,15 @@ struct QkArgs {
   int nf, nh;         // pairs assigned to frame / height axes (rest: width)
 };
 
+template <int FIXED>
 __device__ __forceinline__ void rms_rope_one(bf16* p, const float* w, const QkArgs& a, int lane, int fi, int hi_,
                                              int wi, bool rot) {
-  const int nch = (a.C + 511) / 512;
+  const int nch = FIXED ? FIXED : (a.C + 511) / 512;
   float v[MAXV][8];
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i)
-    if (i < nch && i * 512 + lane * 8 < a.C) {
+    if (i < nch && (FIXED || i * 512 + lane * 8 < a.C)) {
       load8<bf16>(p + i * 512 + lane * 8, v[i]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += v[i][j] * v[i][j];
@@ -133,7 +136,7 @@ __device__ __forceinline__ void rms_rope_one(bf16* p, const float* w, const QkAr
   const float r = rsqrtf(wave_sum(s) / a.C + a.eps);
 #pragma unroll
   for (int i = 0; i < MAXV; ++i)
-    if (i < nch && i * 512 + lane * 8 < a.C) {
+    if (i < nch && (FIXED || i * 512 + lane * 8 < a.C)) {
       const int c0 = i * 512 + lane * 8;
       float y[8];
 #pragma unroll
@@ -161,6 +164,7 @@ __device__ __forceinline__ void rms_rope_one(bf16* p, const float* w, const QkAr
     }
 }
 
+template <int FIXED = 0>
 __global__ __launch_bounds__(256) void qk_rmsnorm_rope_kernel(QkArgs a) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -177,8 +181,8 @@ __global__ __launch_bounds__(256) void qk_rmsnorm_rope_kernel(QkArgs a) {
     }
   }
   bf16* base = a.x + (long)row * a.ldx;
-  rms_rope_one(base + a.q_col, a.wq, a, lane, fi, hi_, wi, rot);
-  if (a.k_col >= 0) rms_rope_one(base + a.k_col, a.wk, a, lane, fi, hi_, wi, rot);
+  rms_rope_one<FIXED>(base + a.q_col, a.wq, a, lane, fi, hi_, wi, rot);
+  if (a.k_col >= 0) rms_rope_one<FIXED>(base + a.k_col, a.wk, a, lane, fi, hi_, wi, rot);
 }
 
 // Self-attention case (C = 1536 = 3 x 512, head_dim 128, q and k, 3-D RoPE): one wave per token row
@@ -257,7 +261,10 @@ __global__ __launch_bounds__(256) void qk_rmsnorm_rope_pair_kernel(QkArgs a) {
 
 template <typename TI, typename TO>
 int launch_ln(const LnArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((layernorm_mod_kernel<TI, TO>), dim3((a.M + 3) / 4), dim3(256), 0, st, a);
+  if (a.C == 1536)
+    hipLaunchKernelGGL((layernorm_mod_kernel<TI, TO, 3>), dim3((a.M + 3) / 4), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((layernorm_mod_kernel<TI, TO>), dim3((a.M + 3) / 4), dim3(256), 0, st, a);
   SA_LAUNCH_CHECK();
   return SA_OK;
 }
@@ -294,8 +301,10 @@ extern "C" int sa_qk_rmsnorm_rope(void* x, int64_t ldx, int q_col, int k_col, co
            tok_offset, F, H, W, n_frame_pairs, n_height_pairs};
   if (rope && k_col >= 0 && C == 1536 && head_dim == 128 && getenv("SA_QK_GENERIC") == nullptr)
     hipLaunchKernelGGL(qk_rmsnorm_rope_pair_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
+  else if (C == 1536)
+    hipLaunchKernelGGL(qk_rmsnorm_rope_kernel<3>, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
   else
-    hipLaunchKernelGGL(qk_rmsnorm_rope_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(qk_rmsnorm_rope_kernel<0>, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
   SA_LAUNCH_CHECK();
   return SA_OK;
 }
