@@ -132,10 +132,12 @@ int sa_cast_f32_bf16(const float* in, void* out, int64_t n, void* stream);
  * kt in {1,3} (causal: kt-1 zero frames in front), kh = kw in {1,3} (zero pad (k-1)/2).
  * upsample != 0 reads the input through nearest-exact 2x upsampling (Upsample, :60-66).
  * interleave_half = C > 0 writes time_conv output channel block j of frame t to frame 2t+j
- * (Resample 'upsample3d', :137-140).  w = bf16 [Cout_pad][kt][kh][kw][Cin], Cin % 32 == 0. */
+ * (Resample 'upsample3d', :137-140).  w = bf16 [Cout_pad][kt][kh][kw][Cin], Cin % 32 == 0.
+ * x_prev (kt > 1, may be null) = the causal cache (CausalConv3d cache_x, :27-36): the kt-1 input
+ * frames before frame 0, [kt-1][H'][W'][Cin]; null = zero padding (first chunk / whole clip). */
 int sa_conv3d_cl(const void* x, int T, int H, int W, int Cin, int upsample, const void* w, const float* bias, int Cout,
                  int Cout_pad, int kt, int kh, int kw, const void* residual, void* y, int out_f32,
-                 int interleave_half, void* stream);
+                 int interleave_half, const void* x_prev, void* stream);
 
 /* Encoder downsampling convs on channels-last bf16, fp32 accumulate, bf16 out [T_out][H][W][Cout]:
  * mode 1 = Resample 'downsample2d/3d' spatial part (wan_vae.py:91-100): ZeroPad2d((0,1,0,1)) + 3x3

@@ -33,7 +33,7 @@ SIGNATURES = {
     "sa_gather_rows": "plpipllp",
     "sa_fill_f32": "plfp",
     "sa_cast_f32_bf16": "pplp",
-    "sa_conv3d_cl": "piiiiippiiiiippiip",
+    "sa_conv3d_cl": "piiiiippiiiiippiipp",
     "sa_vae_rmsnorm_silu": "pppliip",
     "sa_vae_input": "pilpppip",
     "sa_vae_output": "piilpip",

@@ -32,6 +32,7 @@ struct ConvArgs {
   int down;          // 0: stride 1; 1: ZeroPad2d((0,1,0,1)) + 3x3 stride 2 (Resample 'downsample*',
                      // :91-100), input [T][Hin][Win]; 2: (3,1,1) time_conv, stride 2, no padding
                      // (:99, :150-157): output frame t reads input frames 2t .. 2t+2
+  const bf16* xprev; // causal cache [kt-1][Hin][Win][Cin]: input frames -(kt-1)..-1 (null: zeros)
 };
 
 constexpr int BM = 128, BK = 32;
@@ -93,11 +94,16 @@ __global__ __launch_bounds__(256) void conv3d_cl_kernel(ConvArgs a) {
         ti = at[j] + dt - (a.kt - 1);
         hi = ah[j] + dh - (a.kh - 1) / 2;
         wi = aw[j] + dw - (a.kw - 1) / 2;
-        ok = arow_ok[j] && ti >= 0 && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
+        ok = arow_ok[j] && (ti >= 0 || a.xprev) && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
       }
       if (ok) {
         const int hp = a.upsample ? (hi >> 1) : hi, wp = a.upsample ? (wi >> 1) : wi;
-        const bf16* src = a.x + (((long)ti * a.Hin + hp) * a.Win + wp) * a.Cin + ci0 + ac[j] * 8;
+        const bf16* xb = a.x;
+        if (ti < 0) {  // only with a cache (chunked decode): frame kt-1+ti of the previous chunk's tail
+          xb = a.xprev;
+          ti += a.kt - 1;
+        }
+        const bf16* src = xb + (((long)ti * a.Hin + hp) * a.Win + wp) * a.Cin + ci0 + ac[j] * 8;
         ra[j] = *(const u32x4*)src;
       } else {
         ra[j] = (u32x4){0u, 0u, 0u, 0u};
@@ -322,13 +328,14 @@ inline unsigned nblk(long n, int t) { return (unsigned)((n + t - 1) / t); }
 
 extern "C" int sa_conv3d_cl(const void* x, int T, int H, int W, int Cin, int upsample, const void* w,
                             const float* bias, int Cout, int Cout_pad, int kt, int kh, int kw, const void* residual,
-                            void* y, int out_f32, int interleave_half, void* stream) {
+                            void* y, int out_f32, int interleave_half, const void* x_prev, void* stream) {
   if (!x || !w || !bias || !y || T <= 0 || H <= 0 || W <= 0) return SA_ERR_ARG;
   if (Cin % BK || Cout % 4 || (kt != 1 && kt != 3) || (kh != 1 && kh != 3) || (kw != 1 && kw != 3)) return SA_ERR_ARG;
   if (upsample && (H % 2 || W % 2)) return SA_ERR_ARG;
   if (interleave_half > 0 && (Cout != 2 * interleave_half || residual)) return SA_ERR_ARG;
   ConvArgs a{(const bf16*)x, T, H, W, Cin, upsample ? H / 2 : H, upsample ? W / 2 : W, upsample, (const bf16*)w,
-             bias, Cout, kt, kh, kw, (const bf16*)residual, y, out_f32, interleave_half, (long)T * H * W, 0};
+             bias, Cout, kt, kh, kw, (const bf16*)residual, y, out_f32, interleave_half, (long)T * H * W, 0,
+             kt > 1 ? (const bf16*)x_prev : nullptr};
   hipStream_t st = (hipStream_t)stream;
   // N tile chosen so the packed weight rows (Cout_pad) cover whole tiles
   if (Cout_pad % 192 == 0 && Cout > 96) return launch_conv<12>(a, st);
@@ -345,7 +352,7 @@ extern "C" int sa_conv3d_cl_down(const void* x, int T_out, int H_in, int W_in, i
   const int H = mode == 1 ? H_in / 2 : H_in, W = mode == 1 ? W_in / 2 : W_in;
   const int kt = mode == 1 ? 1 : 3, kh = mode == 1 ? 3 : 1;
   ConvArgs a{(const bf16*)x, T_out, H, W, Cin, H_in, W_in, 0, (const bf16*)w, bias, Cout, kt, kh, kh,
-             nullptr, y, 0, 0, (long)T_out * H * W, mode};
+             nullptr, y, 0, 0, (long)T_out * H * W, mode, nullptr};
   hipStream_t st = (hipStream_t)stream;
   if (Cout_pad % 192 == 0 && Cout > 96) return launch_conv<12>(a, st);
   if (Cout_pad % 96 == 0 && Cout > 16) return launch_conv<6>(a, st);

@@ -325,7 +325,7 @@ class AutoencoderKLWan(nn.Module):
     # ------------------------------------------------------------------ kernels
 
     @staticmethod
-    def _conv(x, T, H, W, c, residual=None, upsample=False, out=None, out_f32=False, interleave=0):
+    def _conv(x, T, H, W, c, residual=None, upsample=False, out=None, out_f32=False, interleave=0, prev=None):
         if out is None:
             if interleave:
                 out = torch.empty(2 * T, H, W, interleave, device=x.device, dtype=torch.bfloat16)
@@ -334,8 +334,20 @@ class AutoencoderKLWan(nn.Module):
                                   dtype=torch.float32 if out_f32 else torch.bfloat16)
         call("sa_conv3d_cl", x.data_ptr(), T, H, W, c.cin, int(upsample), c.w.data_ptr(), c.b.data_ptr(), c.cout,
              c.cout_pad, c.kt, c.kh, c.kw, 0 if residual is None else residual.data_ptr(), out.data_ptr(),
-             int(out_f32), interleave, ops._stream())
+             int(out_f32), interleave, 0 if prev is None else prev.data_ptr(), ops._stream())
         return out
+
+    @staticmethod
+    def _cache(state, key, x):
+        """Chunked decode: (the causal cache for this chunk's conv input, update) -- CausalConv3d's
+        cache_x (wan_vae.py:27-36): the last 2 input frames seen so far, zeros before the clip."""
+        if state is None:
+            return None
+        prev = state.get(key)
+        if prev is None:
+            prev = torch.zeros((2,) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
+        state[key] = torch.cat([prev, x])[-2:].clone() if x.shape[0] < 2 else x[-2:].clone()
+        return prev
 
     @staticmethod
     def _rms(x, gamma, silu):
@@ -345,12 +357,12 @@ class AutoencoderKLWan(nn.Module):
              ops._stream())
         return y
 
-    def _res(self, e, x, T, H, W):
+    def _res(self, e, x, T, H, W, state=None):
         h = self._conv(x, T, H, W, e.sc) if e.sc is not None else x
         y = self._rms(x, e.g0, True)
-        y = self._conv(y, T, H, W, e.c1)
+        y = self._conv(y, T, H, W, e.c1, prev=self._cache(state, (id(e), 1), y))
         y = self._rms(y, e.g3, True)
-        return self._conv(y, T, H, W, e.c2, residual=h)
+        return self._conv(y, T, H, W, e.c2, residual=h, prev=self._cache(state, (id(e), 2), y))
 
     def _attn(self, e, x, T, H, W):
         """AttentionBlock (wan_vae.py:243-265): per-frame single-head attention over H*W tokens."""
@@ -375,12 +387,16 @@ class AutoencoderKLWan(nn.Module):
             ops.bmm_nt(p[:n], vt[t0:t0 + n], o[t0:t0 + n], epilogue=ops.EPI_BF16)
         return self._conv(o.view(T, H, W, C), T, H, W, e.proj, residual=x)
 
-    def _up(self, e, x, T, H, W):
+    def _up(self, e, x, T, H, W, state=None, first=True):
         C = x.shape[-1]
-        if e.kind == "up3d" and T > 1:
+        if e.kind == "up3d" and not first:  # a later chunk: every frame goes through time_conv
+            u = torch.empty(2 * T, H, W, C, device=x.device, dtype=torch.bfloat16)
+            self._conv(x, T, H, W, e.tc, out=u, interleave=C, prev=self._cache(state, id(e), x))
+            x, T = u, 2 * T
+        elif e.kind == "up3d" and T > 1:
             u = torch.empty(1 + 2 * (T - 1), H, W, C, device=x.device, dtype=torch.bfloat16)
             u[0].copy_(x[0])
-            self._conv(x[1:], T - 1, H, W, e.tc, out=u[1:], interleave=C)
+            self._conv(x[1:], T - 1, H, W, e.tc, out=u[1:], interleave=C, prev=self._cache(state, id(e), x[1:]))
             x, T = u, 1 + 2 * (T - 1)
         return self._conv(x, T, 2 * H, 2 * W, e.rs, upsample=True), T, 2 * H, 2 * W
 
@@ -442,10 +458,31 @@ class AutoencoderKLWan(nn.Module):
             return (post,)
         return AutoencoderKLOutput(latent_dist=post)
 
-    def decode_clip(self, z, post=False):
+    decode_chunk = 24  # latent frames per chunk of a long clip (bounds the activations to ~100 frames)
+
+    def decode_clip(self, z, post=False, chunk=None):
         """z [16, T, h, w] fp32 (one batch item) -> [3, 1+4(T-1), 8h, 8w] fp32 in [-1,1]
-        (post=True: decode_latents' [0,1] mapping, pipeline:425-430)."""
+        (post=True: decode_latents' [0,1] mapping, pipeline:425-430).  Clips longer than `chunk`
+        latent frames are decoded chunk by chunk with the reference's causal cache carried between
+        chunks (every kt=3 conv gets the last 2 input frames of the previous chunk), so memory stays
+        bounded for arbitrarily long (config 5, 1000+ frame) clips and the result equals the
+        whole-clip decode."""
         pk = self._pack()
+        dev = pk.mean.device
+        Cz, T, H, W = z.shape
+        chunk = chunk or self.decode_chunk
+        if T <= chunk:
+            return self._decode_chunk(pk, z, True, None, post)
+        out = torch.empty(3, 1 + 4 * (T - 1), 8 * H, 8 * W, device=dev, dtype=torch.float32)
+        state = {}
+        for c0 in range(0, T, chunk):
+            c1 = min(c0 + chunk, T)
+            y = self._decode_chunk(pk, z[:, c0:c1], c0 == 0, state, post)
+            o0 = 0 if c0 == 0 else 1 + 4 * (c0 - 1)
+            out[:, o0:o0 + y.shape[1]].copy_(y)
+        return out
+
+    def _decode_chunk(self, pk, z, first, state, post):
         dev = pk.mean.device
         Cz, T, H, W = z.shape
         zc = z.to(device=dev, dtype=torch.float32).contiguous()
@@ -455,16 +492,16 @@ class AutoencoderKLWan(nn.Module):
         x = self._conv(x, T, H, W, pk.conv2)
         for e in pk.layers:
             if e.kind == "conv":
-                x = self._conv(x, T, H, W, e.conv)
+                x = self._conv(x, T, H, W, e.conv, prev=self._cache(state, id(e), x))
             elif e.kind == "res":
-                x = self._res(e, x, T, H, W)
+                x = self._res(e, x, T, H, W, state)
             elif e.kind == "attn":
                 x = self._attn(e, x, T, H, W)
             elif e.kind in ("up3d", "up2d"):
-                x, T, H, W = self._up(e, x, T, H, W)
+                x, T, H, W = self._up(e, x, T, H, W, state, first)
             elif e.kind == "head":
                 y = self._rms(x, e.g, True)
-                x = self._conv(y, T, H, W, e.conv, out_f32=True)
+                x = self._conv(y, T, H, W, e.conv, out_f32=True, prev=self._cache(state, id(e), y))
         out = torch.empty(3, T, H, W, device=dev, dtype=torch.float32)
         call("sa_vae_output", x.data_ptr(), 4, 3, T * H * W, out.data_ptr(), int(post), ops._stream())
         return out

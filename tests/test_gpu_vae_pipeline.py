@@ -51,6 +51,21 @@ def test_vae_decode_vs_reference(name):
     assert psnr(out, g, 2.0) > 40.0 and rel(out, g) < 3e-2, (psnr(out, g, 2.0), rel(out, g))
 
 
+@pytest.mark.parametrize("chunk", [1, 2, 3])
+def test_vae_chunked_decode_equals_whole_clip(chunk):
+    """Long-clip decode (config 5) in chunks of latent frames with the causal cache carried between
+    chunks == the whole-clip decode, bit for bit (chunk 1 is the reference's own frame-by-frame
+    schedule, wan_vae.py:549-574)."""
+    v = make_vae(32, 24)
+    z = synthetic.seeded_normal((16, 7, 8, 8), 424).cuda()
+    with torch.no_grad():
+        whole = v.decode_clip(z, chunk=7)
+        part = v.decode_clip(z, chunk=chunk)
+    torch.cuda.synchronize()
+    assert tuple(part.shape) == (3, 25, 64, 64)
+    assert torch.equal(whole, part), (whole - part).abs().max().item()
+
+
 @pytest.mark.parametrize("name", list(VAE_ENC_SMALL))
 def test_vae_encode_vs_reference(name):
     """HIP encoder (whole clip, bf16 activations) vs the reference's chunked fp32 encode: the
