@@ -578,26 +578,39 @@ class WanTransformer3DFantasyModel(nn.Module):
             em = emod[li]  # [B, 6, dim]
             # self-attention (1B:675-679)
             ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 0], scale=em[:, 1], rows_per_batch=Lc)
-            ops.linear(ws.mod, L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv)
-            ops.qk_rmsnorm_rope(ws.qkv, 0, dim, L.nq, L.nk, dim, self.eps, rope=pk.rope, rows_per_batch=Lc,
-                                tok_offset=rank * Lc, grid=grid, head_dim=self.d,
-                                n_frame_pairs=self.d // 2 - 2 * (self.d // 6), n_height_pairs=self.d // 6)
-            if NS > 1 and sp_rows:  # Ulysses, one CFG row per exchange, overlapped with attention
-                pend = [exch.to_heads_row(ws.qkv, b, B, Lc, self.d, q_sp, kv_sp) for b in range(B)]
+            rope_kw = dict(rope=pk.rope, rows_per_batch=Lc, tok_offset=rank * Lc, grid=grid, head_dim=self.d,
+                           n_frame_pairs=self.d // 2 - 2 * (self.d // 6), n_height_pairs=self.d // 6)
+            if NS > 1 and sp_rows:
+                # Ulysses pipelined over the CFG rows: row b's Q/K/V exchange is issued right after its
+                # QKV GEMM + norm/RoPE (so it travels under rows b+1..'s GEMMs), row b's attention waits
+                # only on it, and row b's output exchange travels under the next rows' attention and
+                # the earlier rows' O-projections
+                pend = []
+                for b in range(B):
+                    rs = slice(b * Lc, (b + 1) * Lc)
+                    ops.linear(ws.mod[rs], L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv[rs])
+                    ops.qk_rmsnorm_rope(ws.qkv[rs], 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
+                    pend.append(exch.to_heads_row(ws.qkv, b, B, Lc, self.d, q_sp, kv_sp))
                 back = []
                 for b in range(B):
                     pend[b].wait()
                     ops.attention(q_sp, kv_sp[:, :hg * self.d], kv_sp[:, hg * self.d:], o_sp, segs_rows[b], 1, Lq,
                                   hg)
                     back.append(exch.to_tokens_row(o_sp, b, B, Lc, self.d, ws.att))
-                for pb in back:
-                    pb.wait()
-            elif NS > 1:  # Ulysses: tokens -> heads, full-sequence attention, heads -> tokens
-                q_sp, kv_sp = exch.to_heads(ws.qkv, B, Lc, self.d)
-                args_ = (q_sp, kv_sp[:, :hg * self.d], kv_sp[:, hg * self.d:], o_sp, segs_self, B, Lq, hg)
+                for b in range(B):
+                    rs = slice(b * Lc, (b + 1) * Lc)
+                    back[b].wait()
+                    ops.linear(ws.att[rs], L.w_o, L.b_o, ops.EPI_RES_F32, out=x[rs], residual=x[rs],
+                               gate=em[b:b + 1, 2], rows_per_batch=Lc)
             else:
-                args_ = (ws.qkv[:, :dim], ws.qkv[:, dim:2 * dim], ws.qkv[:, 2 * dim:], ws.att, segs_self, B, Lp, H_)
-            if not (NS > 1 and sp_rows):
+                ops.linear(ws.mod, L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv)
+                ops.qk_rmsnorm_rope(ws.qkv, 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
+                if NS > 1:  # Ulysses: tokens -> heads, full-sequence attention, heads -> tokens
+                    q_sp, kv_sp = exch.to_heads(ws.qkv, B, Lc, self.d)
+                    args_ = (q_sp, kv_sp[:, :hg * self.d], kv_sp[:, hg * self.d:], o_sp, segs_self, B, Lq, hg)
+                else:
+                    args_ = (ws.qkv[:, :dim], ws.qkv[:, dim:2 * dim], ws.qkv[:, 2 * dim:], ws.att, segs_self, B, Lp,
+                             H_)
                 if self._events is not None:  # bench.py: HIP events around the self-attention kernel
                     ev0 = torch.cuda.Event(enable_timing=True)
                     ev0.record()
@@ -608,7 +621,8 @@ class WanTransformer3DFantasyModel(nn.Module):
                     self._events.append((ev0, ev1))
                 if NS > 1:
                     exch.to_tokens(o_sp, B, Lc, self.d, ws.att)
-            ops.linear(ws.att, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2], rows_per_batch=Lc)
+                ops.linear(ws.att, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2],
+                           rows_per_batch=Lc)
             # cross-attention: text + image + per-frame vocal (1B:534-605, 684)
             ops.layernorm_mod(x, ws.mod, self.eps, weight=L.n3w, bias=L.n3b)
             qc = ws.qkv[:, :dim]

@@ -44,7 +44,7 @@ def _worker(rank, world, port, case, overlap, qret):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case,overlap", [("full", "0"), ("short", "0"), ("full", "2")])
+@pytest.mark.parametrize("case,overlap", [("full", "0"), ("short", "0"), ("full", "2"), ("short", "2")])
 def test_sp2_matches_single_gpu(case, overlap):
     world = 2
     ctx = mp.get_context("spawn")
