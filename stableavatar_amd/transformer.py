@@ -188,6 +188,7 @@ class WanTransformer3DFantasyModel(nn.Module):
                          text_len=text_len)
         _register_tree(self, param_shapes(self._cfg), torch.float32)
         self.sp_world_size, self.sp_world_rank, self.sp_group = 1, 0, None
+        self.teacache = None  # enable_teacache() (1B:867)
         self.teacache = None
         self._packed = None
         self._ws = {}
@@ -256,6 +257,16 @@ class WanTransformer3DFantasyModel(nn.Module):
 
     def enable_teacache(self, *a, **k):
         raise NotImplementedError("TeaCache changes the numerics and is out of scope (SURVEY.md §2 #11)")
+
+    def disable_teacache(self):
+        self.teacache = None
+
+    def enable_teacache(self, coefficients, num_steps: int, rel_l1_thresh: float, num_skip_start_steps: int = 0,
+                        offload: bool = True):
+        """1B:874-885 (inference.py:526-535)."""
+        from .teacache import TeaCache
+        self.teacache = TeaCache(coefficients, num_steps, rel_l1_thresh=rel_l1_thresh,
+                                 num_skip_start_steps=num_skip_start_steps, offload=offload)
 
     def disable_teacache(self):
         self.teacache = None
@@ -462,10 +473,10 @@ class WanTransformer3DFantasyModel(nn.Module):
         if isinstance(y, (list, tuple)):
             y = torch.stack(list(y))
         return self.forward_window(x, 0, False, x.shape[0], t, context, seq_len, clip_fea, y, vocal_embeddings,
-                                   video_sample_n_frames, is_clip_level_modeling)
+                                   video_sample_n_frames, is_clip_level_modeling, cond_flag=cond_flag)
 
     def forward_window(self, lat, frame_offset, broadcast, B, t, context, seq_len, clip_fea, y, vocal_embeddings,
-                       video_sample_n_frames=81, is_clip_level_modeling=False, out=None):
+                       video_sample_n_frames=81, is_clip_level_modeling=False, out=None, cond_flag=True):
         """Forward on frames [frame_offset, frame_offset + Fw) of `lat` ([B|1, C, T, H, W]); with
         broadcast=True one latent row feeds all B CFG rows (the pipeline's torch.cat([latents]*3))."""
         if is_clip_level_modeling:
@@ -518,132 +529,143 @@ class WanTransformer3DFantasyModel(nn.Module):
 
         ctx = self._context(pk, context, clip_fea, B, dev)
 
-        # vocal context (1B:1004-1009): projector on the last (full-condition) row only
-        n_fr = (video_sample_n_frames - 1) // 4 + 1
-        if Lp % n_fr:
-            raise ValueError("seq_len must split evenly into latent frames for the per-frame audio attention")
-        lat_row = torch.empty(Lp, dim, device=dev, dtype=torch.bfloat16)
-        if vocal_embeddings.shape[0] == 1 and B != 1:
-            raise ValueError("a single audio row drives a batch of 1 (1B:1008-1009); CFG batches pass 3 rows")
-        rows_v = 1 if vocal_embeddings.shape[0] > 1 else B
-        voc_rows = []
-        for r in range(rows_v):
-            src = B - 1 if rows_v == 1 else r
-            ops.cast_bf16(xfull[src * Lp:(src + 1) * Lp], lat_row)
-            vv, Fn, nper = self._vocal(pk, vocal_embeddings[src], video_sample_n_frames, lat_row, Lp,
-                                       e0[src:src + 1], e[src:src + 1], dev)
-            voc_rows.append(vv)
-        assert Fn == n_fr
-        if rows_v == 1:
-            vctx = torch.zeros(B, Fn * nper, dim, device=dev, dtype=torch.bfloat16)
-            for b in range(1, B):
-                vctx[b].copy_(voc_rows[0])
-        else:
-            vctx = torch.stack(voc_rows)
-        vctx = vctx.view(B * Fn * nper, dim)
-
-        G = Lp // n_fr
-        if NS > 1:
-            plan = sp.make_plan(NS, rank, H_)
-            exch = sp.UlyssesExchange(plan, self.sp_group)
-            Lq, hg = plan.G * Lc, plan.hg
-            segs_self = self._segs.get(("self_sp", B, Lp, Lq), [[b * Lq, Lq, b * Lp, Lp] for b in range(B)], dev)
-            o_sp = torch.empty(B * Lq, hg * self.d, device=dev, dtype=torch.bfloat16)
-            # per-row pipelining only when it adds no attention waves: a row's launch has
-            # ceil(Lq / 256) x hg workgroups; B serial launches must not need more rounds over the CUs
-            # than the batched one (N = 8: 63 workgroups per row would leave most CUs idle)
-            n_cu = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 256
-            wg_row = -(-Lq // 256) * hg
-            ov = os.environ.get("SA_SP_OVERLAP", "1")  # 0 off, 1 when it adds no waves, 2 always
-            sp_rows = ov == "2" or (ov == "1" and B * -(-wg_row // n_cu) <= -(-(B * wg_row) // n_cu))
-            if sp_rows:
-                q_sp = torch.empty(B * Lq, hg * self.d, device=dev, dtype=torch.bfloat16)
-                kv_sp = torch.empty(B * Lp, 2 * hg * self.d, device=dev, dtype=torch.bfloat16)
-                segs_rows = [self._segs.get(("self_sp_row", b, Lp, Lq), [[b * Lq, Lq, b * Lp, Lp]], dev)
-                             for b in range(B)]
-        else:
-            sp_rows = False
-            segs_self = self._segs.get(("self", B, Lp), [[b * Lp, Lp, b * Lp, Lp] for b in range(B)], dev)
-        segs_txt = self._segs.get(("txt", B, Lc, ctx.text_len), sp.local_segments(B, Lc, ctx.text_len), dev)
-        segs_img = self._segs.get(("img", B, Lc, ctx.img_len), sp.local_segments(B, Lc, ctx.img_len), dev)
-        voc_list = sp.vocal_segments(B, Lp, Lc, rank, n_fr, nper)
-        segs_voc = self._segs.get(("voc", B, Lp, Lc, rank, n_fr, nper), voc_list, dev)
-        voc_n, voc_q = len(voc_list), max(s_[1] for s_ in voc_list)
-        use_cross3 = (ctx.img_len > 0 and G % 256 == 0 and (rank * Lc) % 256 == 0
-                      and os.environ.get("SA_CROSS3", "1") != "0")
+        # TeaCache (1B:1021-1044): optional, decided on e0 before any block work
+        tc = self.teacache
         x = ws.x
-        kvv = torch.empty(B * n_fr * nper, 2 * dim, device=dev, dtype=torch.bfloat16)  # per-frame vocal K|V
-        grid = (Fw, hp, wp)
-        for li, L in enumerate(pk.layers):
-            em = emod[li]  # [B, 6, dim]
-            # self-attention (1B:675-679)
-            ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 0], scale=em[:, 1], rows_per_batch=Lc)
-            rope_kw = dict(rope=pk.rope, rows_per_batch=Lc, tok_offset=rank * Lc, grid=grid, head_dim=self.d,
-                           n_frame_pairs=self.d // 2 - 2 * (self.d // 6), n_height_pairs=self.d // 6)
-            if NS > 1 and sp_rows:
-                # Ulysses pipelined over the CFG rows: row b's Q/K/V exchange is issued right after its
-                # QKV GEMM + norm/RoPE (so it travels under rows b+1..'s GEMMs), row b's attention waits
-                # only on it, and row b's output exchange travels under the next rows' attention and
-                # the earlier rows' O-projections
-                pend = []
-                for b in range(B):
-                    rs = slice(b * Lc, (b + 1) * Lc)
-                    ops.linear(ws.mod[rs], L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv[rs])
-                    ops.qk_rmsnorm_rope(ws.qkv[rs], 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
-                    pend.append(exch.to_heads_row(ws.qkv, b, B, Lc, self.d, q_sp, kv_sp))
-                back = []
-                for b in range(B):
-                    pend[b].wait()
-                    ops.attention(q_sp, kv_sp[:, :hg * self.d], kv_sp[:, hg * self.d:], o_sp, segs_rows[b], 1, Lq,
-                                  hg)
-                    back.append(exch.to_tokens_row(o_sp, b, B, Lc, self.d, ws.att))
-                for b in range(B):
-                    rs = slice(b * Lc, (b + 1) * Lc)
-                    back[b].wait()
-                    ops.linear(ws.att[rs], L.w_o, L.b_o, ops.EPI_RES_F32, out=x[rs], residual=x[rs],
-                               gate=em[b:b + 1, 2], rows_per_batch=Lc)
+        should_calc = True if tc is None else tc.decide(e0, cond_flag)
+        if not should_calc:  # 1B:1048-1050: reuse the last computed residual
+            ws.x.add_(tc.residual(cond_flag, dev))
+        else:
+            x_in = ws.x.clone() if tc is not None else None
+            # vocal context (1B:1004-1009): projector on the last (full-condition) row only
+            n_fr = (video_sample_n_frames - 1) // 4 + 1
+            if Lp % n_fr:
+                raise ValueError("seq_len must split evenly into latent frames for the per-frame audio attention")
+            lat_row = torch.empty(Lp, dim, device=dev, dtype=torch.bfloat16)
+            if vocal_embeddings.shape[0] == 1 and B != 1:
+                raise ValueError("a single audio row drives a batch of 1 (1B:1008-1009); CFG batches pass 3 rows")
+            rows_v = 1 if vocal_embeddings.shape[0] > 1 else B
+            voc_rows = []
+            for r in range(rows_v):
+                src = B - 1 if rows_v == 1 else r
+                ops.cast_bf16(xfull[src * Lp:(src + 1) * Lp], lat_row)
+                vv, Fn, nper = self._vocal(pk, vocal_embeddings[src], video_sample_n_frames, lat_row, Lp,
+                                           e0[src:src + 1], e[src:src + 1], dev)
+                voc_rows.append(vv)
+            assert Fn == n_fr
+            if rows_v == 1:
+                vctx = torch.zeros(B, Fn * nper, dim, device=dev, dtype=torch.bfloat16)
+                for b in range(1, B):
+                    vctx[b].copy_(voc_rows[0])
             else:
-                ops.linear(ws.mod, L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv)
-                ops.qk_rmsnorm_rope(ws.qkv, 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
-                if NS > 1:  # Ulysses: tokens -> heads, full-sequence attention, heads -> tokens
-                    q_sp, kv_sp = exch.to_heads(ws.qkv, B, Lc, self.d)
-                    args_ = (q_sp, kv_sp[:, :hg * self.d], kv_sp[:, hg * self.d:], o_sp, segs_self, B, Lq, hg)
+                vctx = torch.stack(voc_rows)
+            vctx = vctx.view(B * Fn * nper, dim)
+
+            G = Lp // n_fr
+            if NS > 1:
+                plan = sp.make_plan(NS, rank, H_)
+                exch = sp.UlyssesExchange(plan, self.sp_group)
+                Lq, hg = plan.G * Lc, plan.hg
+                segs_self = self._segs.get(("self_sp", B, Lp, Lq), [[b * Lq, Lq, b * Lp, Lp] for b in range(B)], dev)
+                o_sp = torch.empty(B * Lq, hg * self.d, device=dev, dtype=torch.bfloat16)
+                # per-row pipelining only when it adds no attention waves: a row's launch has
+                # ceil(Lq / 256) x hg workgroups; B serial launches must not need more rounds over the CUs
+                # than the batched one (N = 8: 63 workgroups per row would leave most CUs idle)
+                n_cu = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 256
+                wg_row = -(-Lq // 256) * hg
+                ov = os.environ.get("SA_SP_OVERLAP", "1")  # 0 off, 1 when it adds no waves, 2 always
+                sp_rows = ov == "2" or (ov == "1" and B * -(-wg_row // n_cu) <= -(-(B * wg_row) // n_cu))
+                if sp_rows:
+                    q_sp = torch.empty(B * Lq, hg * self.d, device=dev, dtype=torch.bfloat16)
+                    kv_sp = torch.empty(B * Lp, 2 * hg * self.d, device=dev, dtype=torch.bfloat16)
+                    segs_rows = [self._segs.get(("self_sp_row", b, Lp, Lq), [[b * Lq, Lq, b * Lp, Lp]], dev)
+                                 for b in range(B)]
+            else:
+                sp_rows = False
+                segs_self = self._segs.get(("self", B, Lp), [[b * Lp, Lp, b * Lp, Lp] for b in range(B)], dev)
+            segs_txt = self._segs.get(("txt", B, Lc, ctx.text_len), sp.local_segments(B, Lc, ctx.text_len), dev)
+            segs_img = self._segs.get(("img", B, Lc, ctx.img_len), sp.local_segments(B, Lc, ctx.img_len), dev)
+            voc_list = sp.vocal_segments(B, Lp, Lc, rank, n_fr, nper)
+            segs_voc = self._segs.get(("voc", B, Lp, Lc, rank, n_fr, nper), voc_list, dev)
+            voc_n, voc_q = len(voc_list), max(s_[1] for s_ in voc_list)
+            use_cross3 = (ctx.img_len > 0 and G % 256 == 0 and (rank * Lc) % 256 == 0
+                          and os.environ.get("SA_CROSS3", "1") != "0")
+            x = ws.x
+            kvv = torch.empty(B * n_fr * nper, 2 * dim, device=dev, dtype=torch.bfloat16)  # per-frame vocal K|V
+            grid = (Fw, hp, wp)
+            for li, L in enumerate(pk.layers):
+                em = emod[li]  # [B, 6, dim]
+                # self-attention (1B:675-679)
+                ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 0], scale=em[:, 1], rows_per_batch=Lc)
+                rope_kw = dict(rope=pk.rope, rows_per_batch=Lc, tok_offset=rank * Lc, grid=grid, head_dim=self.d,
+                               n_frame_pairs=self.d // 2 - 2 * (self.d // 6), n_height_pairs=self.d // 6)
+                if NS > 1 and sp_rows:
+                    # Ulysses pipelined over the CFG rows: row b's Q/K/V exchange is issued right after its
+                    # QKV GEMM + norm/RoPE (so it travels under rows b+1..'s GEMMs), row b's attention waits
+                    # only on it, and row b's output exchange travels under the next rows' attention and
+                    # the earlier rows' O-projections
+                    pend = []
+                    for b in range(B):
+                        rs = slice(b * Lc, (b + 1) * Lc)
+                        ops.linear(ws.mod[rs], L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv[rs])
+                        ops.qk_rmsnorm_rope(ws.qkv[rs], 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
+                        pend.append(exch.to_heads_row(ws.qkv, b, B, Lc, self.d, q_sp, kv_sp))
+                    back = []
+                    for b in range(B):
+                        pend[b].wait()
+                        ops.attention(q_sp, kv_sp[:, :hg * self.d], kv_sp[:, hg * self.d:], o_sp, segs_rows[b], 1, Lq,
+                                      hg)
+                        back.append(exch.to_tokens_row(o_sp, b, B, Lc, self.d, ws.att))
+                    for b in range(B):
+                        rs = slice(b * Lc, (b + 1) * Lc)
+                        back[b].wait()
+                        ops.linear(ws.att[rs], L.w_o, L.b_o, ops.EPI_RES_F32, out=x[rs], residual=x[rs],
+                                   gate=em[b:b + 1, 2], rows_per_batch=Lc)
                 else:
-                    args_ = (ws.qkv[:, :dim], ws.qkv[:, dim:2 * dim], ws.qkv[:, 2 * dim:], ws.att, segs_self, B, Lp,
-                             H_)
-                if self._events is not None:  # bench.py: HIP events around the self-attention kernel
-                    ev0 = torch.cuda.Event(enable_timing=True)
-                    ev0.record()
-                ops.attention(*args_)
-                if self._events is not None:
-                    ev1 = torch.cuda.Event(enable_timing=True)
-                    ev1.record()
-                    self._events.append((ev0, ev1))
-                if NS > 1:
-                    exch.to_tokens(o_sp, B, Lc, self.d, ws.att)
-                ops.linear(ws.att, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2],
-                           rows_per_batch=Lc)
-            # cross-attention: text + image + per-frame vocal (1B:534-605, 684)
-            ops.layernorm_mod(x, ws.mod, self.eps, weight=L.n3w, bias=L.n3b)
-            qc = ws.qkv[:, :dim]
-            ops.linear(ws.mod, L.w_cq, L.b_cq, ops.EPI_BF16, out=qc)
-            ops.qk_rmsnorm_rope(qc, 0, -1, L.cnq, None, dim, self.eps)
-            kvt, kvi = ctx.kv[li]
-            ops.linear(vctx, L.w_kv_v, L.b_kv_v, ops.EPI_BF16, out=kvv)
-            if use_cross3:  # text + image + vocal in one launch, bf16 sum as 1B:602
-                ops.attention_cross3(qc, kvt[:, :dim], kvt[:, dim:], ctx.text_len, kvi[:, :dim], kvi[:, dim:],
-                                     ctx.img_len, kvv[:, :dim], kvv[:, dim:], nper, G, n_fr, ws.att, B, Lc, H_,
-                                     tok_offset=rank * Lc)
-            else:
-                ops.attention(qc, kvt[:, :dim], kvt[:, dim:], ws.att, segs_txt, B, Lc, H_)
-                if kvi is not None:
-                    ops.attention(qc, kvi[:, :dim], kvi[:, dim:], ws.att, segs_img, B, Lc, H_, accumulate=True)
-                ops.attention(qc, kvv[:, :dim], kvv[:, dim:], ws.att, segs_voc, voc_n, voc_q, H_, accumulate=True)
-            ops.linear(ws.att, L.w_co, L.b_co, ops.EPI_RES_F32, out=x, residual=x)
-            # FFN (1B:687-691)
-            ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 3], scale=em[:, 4], rows_per_batch=Lc)
-            ops.linear(ws.mod, L.w_f0, L.b_f0, ops.EPI_GELU_TANH_BF16, out=ws.ffn)
-            ops.linear(ws.ffn, L.w_f2, L.b_f2, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 5], rows_per_batch=Lc)
+                    ops.linear(ws.mod, L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv)
+                    ops.qk_rmsnorm_rope(ws.qkv, 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
+                    if NS > 1:  # Ulysses: tokens -> heads, full-sequence attention, heads -> tokens
+                        q_sp, kv_sp = exch.to_heads(ws.qkv, B, Lc, self.d)
+                        args_ = (q_sp, kv_sp[:, :hg * self.d], kv_sp[:, hg * self.d:], o_sp, segs_self, B, Lq, hg)
+                    else:
+                        args_ = (ws.qkv[:, :dim], ws.qkv[:, dim:2 * dim], ws.qkv[:, 2 * dim:], ws.att, segs_self, B, Lp,
+                                 H_)
+                    if self._events is not None:  # bench.py: HIP events around the self-attention kernel
+                        ev0 = torch.cuda.Event(enable_timing=True)
+                        ev0.record()
+                    ops.attention(*args_)
+                    if self._events is not None:
+                        ev1 = torch.cuda.Event(enable_timing=True)
+                        ev1.record()
+                        self._events.append((ev0, ev1))
+                    if NS > 1:
+                        exch.to_tokens(o_sp, B, Lc, self.d, ws.att)
+                    ops.linear(ws.att, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2],
+                               rows_per_batch=Lc)
+                # cross-attention: text + image + per-frame vocal (1B:534-605, 684)
+                ops.layernorm_mod(x, ws.mod, self.eps, weight=L.n3w, bias=L.n3b)
+                qc = ws.qkv[:, :dim]
+                ops.linear(ws.mod, L.w_cq, L.b_cq, ops.EPI_BF16, out=qc)
+                ops.qk_rmsnorm_rope(qc, 0, -1, L.cnq, None, dim, self.eps)
+                kvt, kvi = ctx.kv[li]
+                ops.linear(vctx, L.w_kv_v, L.b_kv_v, ops.EPI_BF16, out=kvv)
+                if use_cross3:  # text + image + vocal in one launch, bf16 sum as 1B:602
+                    ops.attention_cross3(qc, kvt[:, :dim], kvt[:, dim:], ctx.text_len, kvi[:, :dim], kvi[:, dim:],
+                                         ctx.img_len, kvv[:, :dim], kvv[:, dim:], nper, G, n_fr, ws.att, B, Lc, H_,
+                                         tok_offset=rank * Lc)
+                else:
+                    ops.attention(qc, kvt[:, :dim], kvt[:, dim:], ws.att, segs_txt, B, Lc, H_)
+                    if kvi is not None:
+                        ops.attention(qc, kvi[:, :dim], kvi[:, dim:], ws.att, segs_img, B, Lc, H_, accumulate=True)
+                    ops.attention(qc, kvv[:, :dim], kvv[:, dim:], ws.att, segs_voc, voc_n, voc_q, H_, accumulate=True)
+                ops.linear(ws.att, L.w_co, L.b_co, ops.EPI_RES_F32, out=x, residual=x)
+                # FFN (1B:687-691)
+                ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 3], scale=em[:, 4], rows_per_batch=Lc)
+                ops.linear(ws.mod, L.w_f0, L.b_f0, ops.EPI_GELU_TANH_BF16, out=ws.ffn)
+                ops.linear(ws.ffn, L.w_f2, L.b_f2, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 5], rows_per_batch=Lc)
+            if tc is not None:  # 1B:1096-1099
+                tc.store(ws.x - x_in, cond_flag)
+                del x_in
 
         # head (1B:715-723) + unpatchify (1B:1161-1184)
         hm = hmod[0]

@@ -96,6 +96,34 @@ def gen_vae_enc():
     np.savez_compressed(os.path.join(HERE, "vae_enc_small.npz"), **out)
 
 
+def gen_teacache():
+    """Reference TeaCache over 10 forwards (t from the 10-step shift-5 schedule): outputs + pattern."""
+    from golden_cases import TEACACHE, TEACACHE_STEPS
+    from wan.models.cache_utils import get_teacache_coefficients
+    from stableavatar_amd.scheduler import FlowMatchEulerDiscreteScheduler
+    m = build_ref_dit(DIT_SMALL)
+    sch = FlowMatchEulerDiscreteScheduler(1000, shift=5.0)
+    sch.set_timesteps(TEACACHE_STEPS)
+    ts = [float(t) for t in sch.timesteps]
+    inp = dit_inputs(DIT_SMALL, "full")
+    out = {"timesteps": np.array(ts, dtype=np.float32)}
+    for name, (coef, thr) in TEACACHE.items():
+        m.enable_teacache(coef if coef is not None else get_teacache_coefficients("wan2.1-fun-1.3b"),
+                          TEACACHE_STEPS, thr, num_skip_start_steps=2, offload=False)
+        outs, pat = [], []
+        for t in ts:
+            y = m(x=inp["x"], t=torch.full((3,), t), context=inp["context"], seq_len=inp["seq_len"],
+                  clip_fea=inp["clip_fea"], y=inp["y"], vocal_embeddings=inp["vocal"], is_clip_level_modeling=False,
+                  video_sample_n_frames=inp["n_frames"])
+            outs.append(y.numpy())
+            pat.append(int(m.teacache.should_calc))
+        m.disable_teacache()
+        out[name + "_out"] = np.stack(outs)
+        out[name + "_calc"] = np.array(pat, dtype=np.int32)
+        print("teacache", name, pat)
+    np.savez_compressed(os.path.join(HERE, "teacache_small.npz"), **out)
+
+
 class _Obj(types.SimpleNamespace):
     def __getitem__(self, i):
         return [self.last][i]
@@ -205,6 +233,6 @@ def gen_tables():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["tables", "dit", "vae", "vae_enc", "pipeline"]
+    which = sys.argv[1:] or ["tables", "dit", "vae", "vae_enc", "teacache", "pipeline"]
     for w in which:
         globals()["gen_" + w]()

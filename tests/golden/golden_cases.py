@@ -63,3 +63,10 @@ def pipe_fixed_inputs(P):
                 neg_embeds=synthetic.seeded_normal((P["neg_len"], P["dit"]["text_dim"]), 302),
                 pos_embeds=synthetic.seeded_normal((P["pos_len"], P["dit"]["text_dim"]), 303),
                 clip=synthetic.seeded_normal((1, 257, 1280), 304))
+
+
+# TeaCache (wan/models/cache_utils.py, 1B:1021-1103): 10 forwards of DIT_SMALL's "full" inputs over a
+# 10-step flow schedule; (coefficients, rel_l1_thresh) per case, num_skip_start_steps 2, no offload
+TEACACHE = {"identity_thr1.0": ([1.0, 0.0], 1.0), "identity_thr2.5": ([1.0, 0.0], 2.5),
+            "wan13b_thr0.1": (None, 0.1)}
+TEACACHE_STEPS = 10

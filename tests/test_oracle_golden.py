@@ -124,3 +124,15 @@ def test_pipeline_vs_reference():
     assert np.allclose([c[1] for c in calls], g["win_t"], atol=1e-2)
     assert rel(lat, g["latents"]) < 1e-3
     assert rel(video, g["video"]) < 1e-3
+
+
+def test_teacache_state_machine_matches_reference_pattern():
+    """stableavatar_amd.teacache.TeaCache.decide, fed the rel-L1 distances the reference measured on
+    DIT_SMALL's e0 sequence, reproduces the reference's compute/skip pattern (golden)."""
+    from stableavatar_amd.teacache import TeaCache
+    tc = TeaCache([1.0, 0.0], 10, 1.0, num_skip_start_steps=2, offload=False)
+    ds = iter([0.82, 0.925, 0.895, 1.016, 0.975, 1.07, 1.065])
+    tc.compute_rel_l1_distance = lambda prev, cur: next(ds)
+    pat = [int(tc.decide(torch.zeros(1), True)) for _ in range(10)]
+    assert pat == G("teacache_small.npz")["identity_thr1.0_calc"].tolist()
+    assert tc.cnt == 0 and tc.previous_modulated_input is None
