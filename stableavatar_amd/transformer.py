@@ -287,7 +287,10 @@ class WanTransformer3DFantasyModel(nn.Module):
         dev = self.patch_embedding.weight.device
         if dev.type != "cuda":
             raise RuntimeError("WanTransformer3DFantasyModel runs on the MI355X HIP kernels: move it to 'cuda'")
-        P = dict(self.named_parameters())
+        # parameters stored as float8_e4m3fn by the reference's qfloat8 memory mode
+        # (wan/utils/fp8_optimization.py:29-43, inference.py:517-518) are upcast exactly before packing
+        fp8 = (torch.float8_e4m3fn, torch.float8_e5m2)
+        P = {k: (v.detach().float() if v.dtype in fp8 else v) for k, v in self.named_parameters()}
         bf = lambda n: P[n].detach().to(torch.bfloat16).contiguous()  # noqa: E731
         f32 = lambda n: P[n].detach().float().contiguous()  # noqa: E731
         cat_bf = lambda *ns: torch.cat([P[n].detach() for n in ns], 0).to(torch.bfloat16).contiguous()  # noqa: E731

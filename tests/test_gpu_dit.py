@@ -88,3 +88,22 @@ def test_dit_fused_cross_attention_matches_unfused(monkeypatch):
     monkeypatch.setenv("SA_CROSS3", "0")
     ref = run(m, inp)
     assert rel(fused, ref) < 1e-2 and cos(fused, ref) > 0.9999, (rel(fused, ref), cos(fused, ref))
+
+
+def test_dit_qfloat8_weights():
+    """GPU_memory_mode 'model_cpu_offload_and_qfloat8' (inference.py:517-518): every parameter except
+    'modulation' stored as float8_e4m3fn (fp8_optimization.py:29-43).  The HIP path packs the fp8
+    parameters exactly; vs the CPU oracle on the same fp8-rounded weights."""
+    from oracle import dit as odit
+    P = synthetic.fill_state_dict(param_shapes(DIT_SMALL), DIT_SMALL["seed"])
+    m = make_model(DIT_SMALL, P)
+    for name, p in m.named_parameters():  # convert_model_weight_to_float8(..., exclude=["modulation"])
+        if "modulation" not in name:
+            p.data = p.data.to(torch.float8_e4m3fn)
+    Pq = {k: (v if "modulation" in k else v.to(torch.float8_e4m3fn).float()) for k, v in P.items()}
+    inp = dit_inputs(DIT_SMALL, "full")
+    out = run(m, inp)
+    with torch.no_grad():
+        ref = odit.forward(Pq, DIT_SMALL, inp["x"], inp["t"], inp["context"], inp["seq_len"], inp["clip_fea"],
+                           inp["y"], inp["vocal"], inp["n_frames"])
+    assert rel(out, ref) < 2e-2 and cos(out, ref) > 0.9995, (rel(out, ref), cos(out, ref))
