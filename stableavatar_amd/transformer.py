@@ -32,12 +32,25 @@ def rope_params(max_seq_len: int, dim: int, theta: float = 10000.0) -> torch.Ten
                        1.0 / torch.pow(theta, torch.arange(0, dim, 2, dtype=torch.float64).div(dim)))
 
 
-def rope_table(head_dim: int = 128, max_seq_len: int = 1024) -> torch.Tensor:
+def riflex_params(max_seq_len: int, dim: int, k: int, L_test: int, L_test_scale=None,
+                  theta: float = 10000.0) -> torch.Tensor:
+    """Angles of get_1d_rotary_pos_embed_riflex (1B:236-291) in fp64: rope_params with the k-th
+    intrinsic frequency replaced by 0.9 * 2 pi / L_test (then divided by L_test_scale)."""
+    freqs = 1.0 / torch.pow(theta, torch.arange(0, dim, 2, dtype=torch.float64).div(dim))
+    freqs[k - 1] = 0.9 * 2 * math.pi / L_test
+    if L_test_scale is not None:
+        freqs[k - 1] = freqs[k - 1] / L_test_scale
+    return torch.outer(torch.arange(max_seq_len, dtype=torch.float64), freqs)
+
+
+def rope_table(head_dim: int = 128, max_seq_len: int = 1024, riflex=None) -> torch.Tensor:
     """fp32 (cos, sin) table [max_seq_len, head_dim/2, 2] of the concatenated frame/height/width
-    frequencies of self.freqs (1B:855-862), computed in fp64 like the reference."""
+    frequencies of self.freqs (1B:855-862), computed in fp64 like the reference.  riflex = (k, L_test,
+    L_test_scale) swaps the frame axis for RIFLEx's frequencies (enable_riflex, 1B:890-905)."""
     d = head_dim
-    ang = torch.cat([rope_params(max_seq_len, d - 4 * (d // 6)), rope_params(max_seq_len, 2 * (d // 6)),
-                     rope_params(max_seq_len, 2 * (d // 6))], dim=1)
+    df = d - 4 * (d // 6)
+    frame = rope_params(max_seq_len, df) if riflex is None else riflex_params(max_seq_len, df, *riflex)
+    ang = torch.cat([frame, rope_params(max_seq_len, 2 * (d // 6)), rope_params(max_seq_len, 2 * (d // 6))], dim=1)
     return torch.stack([torch.cos(ang), torch.sin(ang)], -1).float().contiguous()
 
 
@@ -189,6 +202,7 @@ class WanTransformer3DFantasyModel(nn.Module):
         _register_tree(self, param_shapes(self._cfg), torch.float32)
         self.sp_world_size, self.sp_world_rank, self.sp_group = 1, 0, None
         self.teacache = None  # enable_teacache() (1B:867)
+        self._riflex = None  # enable_riflex() (1B:890-905)
         self.teacache = None
         self._packed = None
         self._ws = {}
@@ -260,6 +274,20 @@ class WanTransformer3DFantasyModel(nn.Module):
 
     def disable_teacache(self):
         self.teacache = None
+
+    def enable_riflex(self, k=6, L_test=66, L_test_scale=4.886):
+        """1B:890-905: RIFLEx frame frequencies for length extrapolation."""
+        self._riflex = (k, L_test, L_test_scale)
+        self._set_rope()
+
+    def disable_riflex(self):
+        """1B:907-916."""
+        self._riflex = None
+        self._set_rope()
+
+    def _set_rope(self):
+        if self._packed is not None:
+            self._packed.rope = rope_table(self.d, riflex=self._riflex).to(self._packed.rope.device)
 
     def enable_teacache(self, coefficients, num_steps: int, rel_l1_thresh: float, num_skip_start_steps: int = 0,
                         offload: bool = True):
@@ -360,7 +388,7 @@ class WanTransformer3DFantasyModel(nn.Module):
         V.fmod = f32(vp + "final_head.modulation").reshape(1, 2, 1536)
         V.w_fp, V.b_fp = bf(vp + "final_head.final_proj.weight"), f32(vp + "final_head.final_proj.bias")
         pk.vocal = V
-        pk.rope = rope_table(self.d).to(dev)
+        pk.rope = rope_table(self.d, riflex=self._riflex).to(dev)
         self._packed = pk
         return pk
 

@@ -58,6 +58,13 @@ def gen_dit():
               video_sample_n_frames=inp["n_frames"])
         out[f"{case}_out"] = y.numpy()
         print(case, tuple(y.shape), float(y.abs().mean()))
+    m.enable_riflex(k=6, L_test=66, L_test_scale=4.886)  # 1B:890-905
+    inp = dit_inputs(DIT_SMALL, "full")
+    y = m(x=inp["x"], t=inp["t"], context=inp["context"], seq_len=inp["seq_len"], clip_fea=inp["clip_fea"],
+          y=inp["y"], vocal_embeddings=inp["vocal"], is_clip_level_modeling=False,
+          video_sample_n_frames=inp["n_frames"])
+    out["full_riflex_out"] = y.numpy()
+    m.disable_riflex()
     # sub-module pins: vocal projector output for the full case
     inp = dit_inputs(DIT_SMALL, "full")
     np.savez_compressed(os.path.join(HERE, "dit_small.npz"), **out)
@@ -225,6 +232,11 @@ def gen_tables():
         out[f"split_{L}_{nf}_ranges"] = np.array(r)
         out[f"split_{L}_{nf}_rows"] = (sub[0, :, :, 0].numpy() - 1.0).astype(np.int64)  # -1 marks zero rows
         out[f"split_{L}_{nf}_lens"] = lens.numpy()
+    from wan.models.wan_fantasy_transformer3d_1B import get_1d_rotary_pos_embed_riflex
+    fr = get_1d_rotary_pos_embed_riflex(1024, 128 - 4 * (128 // 6), use_real=False, k=6, L_test=66,
+                                        L_test_scale=4.886)
+    out["riflex_frame_cos"] = fr.real.float().numpy()
+    out["riflex_frame_sin"] = fr.imag.float().numpy()
     s = FlowMatchEulerDiscreteScheduler(1000, shift=5.0)
     s.set_timesteps(50)
     out["sched50_timesteps"] = s.timesteps.numpy()

@@ -107,3 +107,17 @@ def test_dit_qfloat8_weights():
         ref = odit.forward(Pq, DIT_SMALL, inp["x"], inp["t"], inp["context"], inp["seq_len"], inp["clip_fea"],
                            inp["y"], inp["vocal"], inp["n_frames"])
     assert rel(out, ref) < 2e-2 and cos(out, ref) > 0.9995, (rel(out, ref), cos(out, ref))
+
+
+def test_dit_riflex_vs_reference_golden():
+    """enable_riflex() (1B:890-905) after the weights are packed swaps the frame RoPE table in place."""
+    g = np.load(os.path.join(HERE, "golden", "dit_small.npz"))
+    m = make_model(DIT_SMALL)
+    inp = dit_inputs(DIT_SMALL, "full")
+    base = run(m, inp)
+    m.enable_riflex(k=6, L_test=66, L_test_scale=4.886)
+    out = run(m, inp)
+    ref = g["full_riflex_out"]
+    assert rel(out, ref) < 2e-2 and cos(out, ref) > 0.9995, (rel(out, ref), cos(out, ref))
+    m.disable_riflex()
+    assert torch.equal(run(m, inp), base)

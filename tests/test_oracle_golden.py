@@ -136,3 +136,15 @@ def test_teacache_state_machine_matches_reference_pattern():
     pat = [int(tc.decide(torch.zeros(1), True)) for _ in range(10)]
     assert pat == G("teacache_small.npz")["identity_thr1.0_calc"].tolist()
     assert tc.cnt == 0 and tc.previous_modulated_input is None
+
+
+def test_riflex_rope_table_vs_reference():
+    """rope_table(riflex=(6, 66, 4.886)) frame axis == get_1d_rotary_pos_embed_riflex (1B:236-291)."""
+    from stableavatar_amd.transformer import rope_table
+    g = G("tables.npz")
+    tab = rope_table(128, riflex=(6, 66, 4.886))
+    nf = g["riflex_frame_cos"].shape[1]
+    assert np.allclose(tab[:, :nf, 0].numpy(), g["riflex_frame_cos"], atol=1e-6)
+    assert np.allclose(tab[:, :nf, 1].numpy(), g["riflex_frame_sin"], atol=1e-6)
+    plain = rope_table(128)
+    assert torch.equal(plain[:, nf:], tab[:, nf:]) and not torch.equal(plain[:, :nf], tab[:, :nf])
