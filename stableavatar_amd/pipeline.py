@@ -88,6 +88,10 @@ class WanI2VTalkingInferenceLongPipeline:
         forward) and every rank applies the CFG / Euler / blend steps of all windows in the
         reference order -- bit-identical latents on every rank and to the single-GPU loop."""
         import torch.distributed as dist
+        if self.transformer is not None and getattr(self.transformer, "sp_world_size", 1) > 1:
+            raise RuntimeError("window parallelism and sequence parallelism over the same ranks would deadlock "
+                               "(each rank runs different windows while SP needs all ranks in every forward); "
+                               "use one of them")
         self.window_group = group if group is not None else dist.group.WORLD
         return self
 
