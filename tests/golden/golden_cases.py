@@ -32,11 +32,13 @@ def dit_inputs(cfg, case="full"):
 
 
 VAE_SMALL = {"dim32_T3_8x8": dict(dim=32, seed=21, T=3, h=8, w=8),
-             "dim96_T2_4x4": dict(dim=96, seed=22, T=2, h=4, w=4)}
+             "dim96_T2_4x4": dict(dim=96, seed=22, T=2, h=4, w=4),
+             "dim32_T1_6x4": dict(dim=32, seed=26, T=1, h=6, w=4)}  # one latent frame, non-square
 
 
 VAE_ENC_SMALL = {"dim32_T9_32x32": dict(dim=32, seed=21, T=9, H=32, W=32),
-                 "dim96_T5_16x16": dict(dim=96, seed=22, T=5, H=16, W=16)}
+                 "dim96_T5_16x16": dict(dim=96, seed=22, T=5, H=16, W=16),
+                 "dim32_T1_24x16": dict(dim=32, seed=25, T=1, H=24, W=16)}  # a single image, non-square
 
 
 def vae_video(cfg):
