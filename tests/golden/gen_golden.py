@@ -51,7 +51,7 @@ def build_ref_dit(cfg):
 def gen_dit():
     m = build_ref_dit(DIT_SMALL)
     out = {}
-    for case in ("full", "short"):
+    for case in ("full", "short", "wide"):
         inp = dit_inputs(DIT_SMALL, case)
         y = m(x=inp["x"], t=inp["t"], context=inp["context"], seq_len=inp["seq_len"], clip_fea=inp["clip_fea"],
               y=inp["y"], vocal_embeddings=inp["vocal"], is_clip_level_modeling=False,

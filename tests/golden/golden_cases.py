@@ -13,9 +13,10 @@ DIT_SMALL = dict(model_type="i2v", dim=1536, ffn_dim=256, freq_dim=256, text_dim
 
 def dit_inputs(cfg, case="full"):
     """CFG batch of 3 at 64x64 video -> 8x8 latent, clip 17 (5 latent frames, seq_len 80).
-    'short' is the last-window case: 3 latent frames padded to the 5-frame seq_len."""
-    B, H, W = 3, 8, 8
-    Fw = 5 if case == "full" else 3
+    'short' is the last-window case: 3 latent frames padded to the 5-frame seq_len; 'wide' a
+    non-square 64x96 video (8x12 latent, 24 tokens per frame, seq_len 120)."""
+    B, H, W = 3, 8, (12 if case == "wide" else 8)
+    Fw = 3 if case == "short" else 5
     n_frames = 17
     seq_len = ((n_frames - 1) // 4 + 1) * (H // 2) * (W // 2)
     lat = synthetic.seeded_normal((1, 16, Fw, H, W), 101)

@@ -48,7 +48,7 @@ def run(m, inp):
     return out.float().cpu()
 
 
-@pytest.mark.parametrize("case", ["full", "short"])
+@pytest.mark.parametrize("case", ["full", "short", "wide"])
 def test_dit_vs_reference_golden(case):
     m = make_model(DIT_SMALL)
     out = run(m, dit_inputs(DIT_SMALL, case))

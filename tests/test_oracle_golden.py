@@ -60,7 +60,7 @@ def dit_params():
     return synthetic.fill_state_dict(odit.param_shapes(DIT_SMALL), DIT_SMALL["seed"])
 
 
-@pytest.mark.parametrize("case", ["full", "short"])
+@pytest.mark.parametrize("case", ["full", "short", "wide"])
 def test_dit_forward_vs_reference(dit_params, case):
     inp = dit_inputs(DIT_SMALL, case)
     with torch.no_grad():
