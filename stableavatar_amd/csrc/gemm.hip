@@ -1316,6 +1316,11 @@ constexpr int S7_LDS = S5_LDS + 4 * S7_STRIP;     // 145 KB
 // half) steps are loaded S7_RES_AHEAD steps ahead (the fragment registers are dead here), bias once per
 // column half, so the residual's HBM latency is paid about once per tile instead of once per step
 constexpr int S7_RES_AHEAD = 2;
+__constant__ int g_res_tile_gate = 1;  // A/B switch (SA_GEMM_TILEGATE=0 in the environment clears it)
+// TILE_GATE: every row of the tile reads the same gate row (no gate, or the tile lies inside one CFG
+// row's token range, e.g. 21 504 = 84 x 256): the gate is loaded once per column half like the bias,
+// and the freed registers deepen the residual prefetch to AHEAD = 3 steps
+template <int AHEAD, bool TILE_GATE>
 __device__ __forceinline__ void s7_res_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8], float* strip, int wm, int wn,
                                                 int fr, int fc, int er, int ec, int m0, int n0, long bz) {
   f32x4 bias_h[2][4];
@@ -1324,7 +1329,17 @@ __device__ __forceinline__ void s7_res_epilogue(const GemmArgs& g, f32x4 (&acc)[
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       bias_h[h][q] = g.bias ? *(const f32x4*)(g.bias + n0 + wn * 128 + h * 64 + ec + 4 * q) : (f32x4){0.f, 0.f, 0.f, 0.f};
-  f32x4 rb[S7_RES_AHEAD][4], gb[S7_RES_AHEAD][4];
+  f32x4 gate_h[TILE_GATE ? 2 : 1][4];
+  if constexpr (TILE_GATE) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        gate_h[h][q] = g.gate ? *(const f32x4*)(g.gate + (long)(m0 / g.rows_per_batch) * g.gate_bstride + n0 +
+                                                wn * 128 + h * 64 + ec + 4 * q)
+                              : (f32x4){1.f, 1.f, 1.f, 1.f};
+  }
+  f32x4 rb[AHEAD][4], gb[TILE_GATE ? 1 : AHEAD][4];
   auto fetch = [&](int k, int slot) {
     const int i = k >> 1, h = k & 1;
     const int row = m0 + wm * 128 + i * 16 + er;
@@ -1332,20 +1347,22 @@ __device__ __forceinline__ void s7_res_epilogue(const GemmArgs& g, f32x4 (&acc)[
     const float* R = g.R + bz * g.sR + (long)row * g.ldr + col;
 #pragma unroll
     for (int q = 0; q < 4; ++q) rb[slot][q] = *(const f32x4*)(R + 4 * q);
-    if (g.gate) {
-      const float* G = g.gate + (long)(row / g.rows_per_batch) * g.gate_bstride + col;
+    if constexpr (!TILE_GATE) {
+      if (g.gate) {
+        const float* G = g.gate + (long)(row / g.rows_per_batch) * g.gate_bstride + col;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) gb[slot][q] = *(const f32x4*)(G + 4 * q);
-    } else {
+        for (int q = 0; q < 4; ++q) gb[slot][q] = *(const f32x4*)(G + 4 * q);
+      } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) gb[slot][q] = (f32x4){1.f, 1.f, 1.f, 1.f};
+        for (int q = 0; q < 4; ++q) gb[slot][q] = (f32x4){1.f, 1.f, 1.f, 1.f};
+      }
     }
   };
 #pragma unroll
-  for (int k = 0; k < S7_RES_AHEAD; ++k) fetch(k, k);
+  for (int k = 0; k < AHEAD; ++k) fetch(k, k);
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const int i = k >> 1, h = k & 1, slot = k % S7_RES_AHEAD;
+    const int i = k >> 1, h = k & 1, slot = k % AHEAD;
 #pragma unroll
     for (int j = 0; j < 4; ++j) *(f32x4*)(strip + fr * 68 + j * 16 + fc * 4) = acc[i][4 * h + j];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1362,11 +1379,12 @@ __device__ __forceinline__ void s7_res_epilogue(const GemmArgs& g, f32x4 (&acc)[
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float t = bf2f(f2bf(v[q][e] + bias_h[h][q][e]));  // bf16 Linear output (reference autocast)
-        o[e] = rb[slot][q][e] + t * gb[slot][q][e];
+        const float gt = TILE_GATE ? gate_h[TILE_GATE ? h : 0][q][e] : gb[TILE_GATE ? 0 : slot][q][e];
+        o[e] = rb[slot][q][e] + t * gt;
       }
       *(f32x4*)(C + 4 * q) = o;
     }
-    if (k + S7_RES_AHEAD < 16) fetch(k + S7_RES_AHEAD, slot);
+    if (k + AHEAD < 16) fetch(k + AHEAD, slot);
   }
 }
 
@@ -1378,7 +1396,10 @@ __device__ __forceinline__ void s7_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8
   const int er = lane >> 2, ec = (lane & 3) * 16;
   if constexpr (EPI == EPI_RES_F32) {
     if (m0 + BM <= g.M && n0 + BN <= g.N) {  // wave-uniform
-      s7_res_epilogue(g, acc, strip, wm, wn, fr, fc, er, ec, m0, n0, bz);
+      if (g_res_tile_gate && (!g.gate || m0 / g.rows_per_batch == (m0 + BM - 1) / g.rows_per_batch))
+        s7_res_epilogue<3, true>(g, acc, strip, wm, wn, fr, fc, er, ec, m0, n0, bz);
+      else
+        s7_res_epilogue<S7_RES_AHEAD, false>(g, acc, strip, wm, wn, fr, fc, er, ec, m0, n0, bz);
       return;
     }
   }
@@ -1656,6 +1677,11 @@ int launch(const GemmArgs& g_in, int batch, hipStream_t st) {
   if (g_gemm_variant < 0) {
     const char* e = getenv("SA_GEMM_VARIANT");
     g_gemm_variant = e ? atoi(e) : 15;
+    const char* tg = getenv("SA_GEMM_TILEGATE");
+    if (tg && atoi(tg) == 0) {
+      const int zero = 0;
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_res_tile_gate), &zero, sizeof(int));
+    }
   }
   GemmArgs g = g_in;
   // 15 = default (measured, profiles/r01/gemm_ab_r4.md): the persistent one-wave-per-SIMD LDS-DMA
