@@ -3,10 +3,16 @@ audio-driven clip (BASELINE.json configs[1]): 50 sliding-window x 3-way-CFG DiT 
 the Wan-2.1 1.3B StableAvatar model + the 3-D causal VAE decode to 81 frames.
 
 One bench "step" = one whole clip (50 DiT forwards at B=3, L=21504 + 50 fused CFG/Euler steps +
-VAE decode), inputs resident in HBM.  `python bench.py --gpus N --steps K --warmup W`; for N>1 it is
-launched by torch.distributed.run, one process per GPU: by default every rank denoises its own clip
-(replicas, weak scaling); with --sp all ranks denoise ONE clip with Ulysses sequence parallelism over
-RCCL (strong scaling).  Rank 0 prints ONE JSON line.
+VAE decode), inputs resident in HBM.  `python bench.py --gpus N --steps K --warmup W`.
+
+N = 1: one clip on one GPU.  N > 1 (one process per GPU; torch.distributed.run sets RANK/WORLD_SIZE,
+and without it this script starts that launcher itself before touching the GPU):
+  --mode sp (default)   ONE clip, Ulysses sequence parallel over all ranks on RCCL (BASELINE config 3,
+                        strong scaling); the JSON also carries `replicas` = one clip per rank timed in
+                        the same processes (--replica-steps, 0 to skip)
+  --mode replicas       one clip per rank, no data-path collective (weak scaling)
+  --mode window-dp      one long clip (--video-frames) with its sliding windows spread over the ranks
+Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -14,6 +20,7 @@ import argparse
 import json
 import math
 import os
+import subprocess
 import sys
 import time
 
@@ -24,9 +31,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "denoised frames/sec, Wan-1.3B 512²×81f audio-driven, 1/2/4/8 MI355X"
 PEAK_BF16 = 2.5e15  # dense bf16 MFMA, MI355X_MICROARCH.md
+ATTN_KERNEL_NAME = "attn_fwd_v6_kernel"
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=1)
@@ -36,18 +44,148 @@ def parse():
     p.add_argument("--sample-steps", type=int, default=50)
     p.add_argument("--overlap", type=int, default=15)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-cpu-config1", action="store_true",
+                   help="skip the end-to-end config-1 run of the CPU oracle inside cpu_baseline")
     p.add_argument("--no-encode", action="store_true", help="skip the (untimed) VAE encode measurement")
-    p.add_argument("--sp", action="store_true",
-                   help="N>1: one clip sequence-parallel over all ranks (Ulysses, strong scaling) instead of "
-                        "one clip per rank (replicas, weak scaling)")
-    p.add_argument("--window-dp", action="store_true",
-                   help="N>1: one long clip with its sliding windows spread over the ranks (window parallelism, "
-                        "strong scaling; use with --video-frames)")
+    p.add_argument("--mode", choices=("sp", "replicas", "window-dp"), default=None,
+                   help="N>1 layout (default sp); ignored at N=1")
+    p.add_argument("--sp", action="store_true", help="alias of --mode sp")
+    p.add_argument("--window-dp", action="store_true", help="alias of --mode window-dp")
+    p.add_argument("--replica-steps", type=int, default=1,
+                   help="sp mode: clips per rank of the extra replicas measurement (0 = skip)")
     p.add_argument("--video-frames", type=int, default=None,
                    help="length of the generated video (default: --frames, i.e. one window); e.g. 165 = the "
                         "examples/case-1 shape (42 latent frames, 5 windows per step at overlap 15)")
-    return p.parse_args()
+    a = p.parse_args(argv)
+    if a.mode is None:
+        a.mode = "window-dp" if a.window_dp else "sp"
+    return a
 
+
+def launch_workers(args, argv) -> int:
+    """--gpus N > 1 without a launcher: start torch.distributed.run as a CHILD process (this process
+    has not touched the GPU and stays the parent) and return its exit code."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ------------------------------------------------------------------------------------------------ CPU baseline
+
+def cpu_cores() -> int:
+    """Cores this process may use: the affinity mask, capped by a cgroup-v2 CPU quota."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(size, frames, sample_steps, n_fwd, out_frames, config1=True):
+    """The CPU oracle (oracle/, fp32 restatement of the reference) on this host's cores:
+    (a) config 2, bounded sample: one of the 30 DiT blocks at the full shape + the VAE decoder on one
+        latent frame, extrapolated to the clip (n_fwd forwards x 30 blocks + out_frames frames);
+    (b) config 1 (BASELINE.json configs[0]) end to end: 5 sampling steps x 2 windows of the full 30-layer
+        DiT at 256x256 clip 17 + the full VAE decode of the 21-frame video, measured, not extrapolated."""
+    from oracle import dit as odit
+    from oracle import vae as ovae
+    from stableavatar_amd import synthetic
+    threads = cpu_cores()
+    torch.set_num_threads(threads)
+    h = size // 8
+    T = (frames - 1) // 4 + 1
+    L = T * (h // 2) ** 2
+    cfg = dict(odit.CONFIG_1_3B, num_layers=1)
+    P = synthetic.fill_state_dict({k: v for k, v in odit.param_shapes(cfg).items() if k.startswith("blocks.0.")}, 0)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(3, L, 1536, generator=g)
+    e0 = torch.randn(3, 6, 1536, generator=g) * 0.1
+    ctx = torch.randn(3, 769, 1536, generator=g)
+    voc = torch.randn(3, T, 17, 1536, generator=g)
+    grid = [(T, h // 2, h // 2)] * 3
+    with torch.no_grad():
+        t0 = time.time()
+        odit.block(P, "blocks.0", x, e0, grid, odit.model_freqs(128), ctx, voc, T, 12)
+        t_block = time.time() - t0
+        Pv = synthetic.fill_state_dict(ovae.param_shapes(), 1)
+        z = torch.randn(1, 16, 1, h, h, generator=g)
+        t0 = time.time()
+        ovae.decode(Pv, z)
+        t_vae_frame = time.time() - t0
+    del P, x, ctx, voc
+    t_clip = n_fwd * 30 * t_block + out_frames * t_vae_frame
+    out = {"value": round(out_frames / t_clip, 6), "unit": "frames/s", "cores": threads, "kind": "port",
+           "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+           "sample": f"oracle fp32 (oracle/dit.py, oracle/vae.py) on {threads} threads: 1 of 30 DiT blocks at "
+                     f"B=3,L={L} ({t_block:.1f}s) + VAE decode of 1 latent frame at {size}x{size} "
+                     f"({t_vae_frame:.1f}s), extrapolated to {n_fwd} forwards x 30 blocks + {out_frames} frames "
+                     f"= {t_clip:.0f}s per clip"}
+    if config1:
+        out["config_1"] = cpu_config1(Pv)
+    return out
+
+
+def cpu_config1(Pv):
+    """BASELINE config 1 end to end on the CPU oracle: the full 30-layer DiT (synthetic weights) through
+    the restated sliding-window loop (oracle/pipeline.py) + the full VAE decode; encoders excluded
+    (once per call).  Returns the measured frames/s."""
+    from oracle import dit as odit
+    from oracle import pipeline as opipe
+    from oracle import vae as ovae
+    from stableavatar_amd import synthetic
+    cfg = dict(odit.CONFIG_1_3B)
+    Pd = synthetic.fill_state_dict(odit.param_shapes(cfg), 41)
+    size, clip_length, steps, overlap, audio_frames = 256, 17, 5, 2, 24
+    T = (audio_frames - 1) // 4 + 1
+    lat0 = synthetic.seeded_normal((1, 16, T, size // 8, size // 8), 301)
+    y = synthetic.seeded_normal((3, 20, (clip_length - 1) // 4 + 1, size // 8, size // 8), 302)
+    ctx = [synthetic.seeded_normal((24, 4096), 303)] * 2 + [synthetic.seeded_normal((31, 4096), 304)]
+    clip = synthetic.seeded_normal((1, 257, 1280), 305).expand(3, -1, -1).contiguous()
+    audio = synthetic.seeded_normal((audio_frames * 640,), 306, 0.1)
+    n_fwd = [0]
+
+    def dit(x, t, context, seq_len, yy, clip_fea, vocal, n):
+        n_fwd[0] += 1
+        return odit.forward(Pd, cfg, x, t, context, seq_len, clip_fea, yy, vocal, n)
+
+    enc = lambda s: synthetic.fake_wav2vec_features(torch.as_tensor(s)[None])  # noqa: E731
+    with torch.no_grad():
+        t0 = time.time()
+        lat = opipe.denoise(dit, lat0, y, ctx, clip, audio, enc, num_inference_steps=steps, clip_length=clip_length,
+                            num_frames=clip_length, height=size, width=size, overlap=overlap, text_guide_scale=3.0,
+                            audio_guide_scale=5.0)
+        t_denoise = time.time() - t0
+        video = ovae.decode(Pv, lat)
+        dt = time.time() - t0
+    n_out = video.shape[2]
+    return {"value": round(n_out / dt, 5), "unit": "frames/s", "seconds": round(dt, 1),
+            "denoise_s": round(t_denoise, 1), "dit_forwards": n_fwd[0], "frames": n_out,
+            "workload": f"Wan-1.3B 30 layers {size}x{size}, clip {clip_length}, {audio_frames} frames of audio "
+                        f"(T_lat {T}, 2 windows/step), {steps} steps, fp32, + VAE decode"}
+
+
+# ------------------------------------------------------------------------------------------------ GPU workload
 
 def build(dev, seed=0):
     from stableavatar_amd import synthetic
@@ -80,176 +218,235 @@ def make_inputs(dev, frames, size, seed, video_frames=None):
     return latents, y, ctx, clip, a
 
 
-def cpu_baseline(size, frames, sample_steps, n_fwd=None, out_frames=None):
-    """Time the CPU oracle (fp32 restatement, oracle/) on a bounded sample of the same workload:
-    one of the 30 DiT blocks at the full config-2 shape and the VAE decoder on one latent frame,
-    then extrapolate to the clip (50 steps x 30 blocks + 81-frame decode)."""
-    from oracle import dit as odit
-    from oracle import vae as ovae
-    from stableavatar_amd import synthetic
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    h = size // 8
-    T = (frames - 1) // 4 + 1
-    L = T * (h // 2) ** 2
-    cfg = dict(odit.CONFIG_1_3B, num_layers=1)
-    P = synthetic.fill_state_dict({k: v for k, v in odit.param_shapes(cfg).items() if k.startswith("blocks.0.")}, 0)
-    g = torch.Generator().manual_seed(0)
-    x = torch.randn(3, L, 1536, generator=g)
-    e0 = torch.randn(3, 6, 1536, generator=g) * 0.1
-    ctx = torch.randn(3, 769, 1536, generator=g)
-    voc = torch.randn(3, T, 17, 1536, generator=g)
-    grid = [(T, h // 2, h // 2)] * 3
+class ClipWorkload:
+    """One audio-driven clip per step: the denoise loop (pipeline.denoise) + VAE decode."""
+
+    def __init__(self, args, dev, rank, world):
+        from stableavatar_amd.pipeline import WanI2VTalkingInferenceLongPipeline, window_schedule
+        from stableavatar_amd.scheduler import FlowMatchEulerDiscreteScheduler
+        self.args, self.dev, self.rank, self.world = args, dev, rank, world
+        self.dit, self.vae = build(dev, seed=0)
+        self.sched = FlowMatchEulerDiscreteScheduler(1000, shift=5.0)
+        self.sched.set_timesteps(args.sample_steps, device=dev)
+        self.pipe = WanI2VTalkingInferenceLongPipeline(vae=self.vae, transformer=self.dit, scheduler=self.sched)
+        self.fpb = (args.frames - 1) // 4 + 1
+        self.h = args.size // 8
+        self.seq_len = math.ceil(self.h * self.h / 4 * self.fpb)
+        self.window_schedule = window_schedule
+        self.set_layout("single")
+
+    def set_layout(self, layout):
+        """single | sp | replicas | window-dp: model / pipeline parallel state + this rank's inputs."""
+        self.layout = layout
+        self.dit.disable_multi_gpus_inference()
+        self.pipe.disable_window_parallel()
+        if layout == "sp":
+            self.dit.enable_multi_gpus_inference()
+        elif layout == "window-dp":
+            self.pipe.enable_window_parallel()
+        shared = layout in ("sp", "window-dp")  # one clip over all ranks
+        a = self.args
+        self.latents, self.y, self.ctx, self.clip, au = make_inputs(self.dev, a.frames, a.size,
+                                                                    seed=42 + (0 if shared else self.rank),
+                                                                    video_frames=a.video_frames)
+        self.T = self.latents.shape[2]
+        self.wins = self.window_schedule(self.T, self.fpb, a.overlap)
+        self.feats = {(s, e): torch.cat([torch.zeros_like(au), au, au]) for (s, e, _) in self.wins}
+        self.out_frames = 1 + 4 * (self.T - 1)
+
+    def step(self):
+        a = self.args
+        lat = self.pipe.denoise(self.latents, self.y, self.ctx, self.clip, self.feats, self.sched.timesteps,
+                                self.sched.sigmas, clip_length=a.frames, seq_len=self.seq_len, overlap=a.overlap,
+                                text_guide_scale=3.0, audio_guide_scale=5.0)
+        return self.vae.decode_clip(lat[0].float(), post=True)
+
+    def check(self, video):
+        assert video.shape[1] == self.out_frames and torch.isfinite(video).all()
+
+    def start_events(self):
+        self.dit._events = []
+
+    def attention_launch_ms(self):
+        """mean duration of one whole self-attention launch (per-row SP launches are summed by their
+        share of the CFG batch), from HIP events on the launching stream"""
+        ev, self.dit._events = self.dit._events or [], None
+        if not ev:
+            return None
+        tot = sum(e0.elapsed_time(e1) for e0, e1, _ in ev)
+        return tot / sum(f for _, _, f in ev)
+
+    def n_fwd(self):
+        return self.args.sample_steps * len(self.wins)
+
+
+def sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def barrier(world, dev):
+    sync(dev)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        sync(dev)
+
+
+def timed(work, steps, warmup, world, dev, events=False):
+    """W untimed warmup steps, then EXACTLY K steps between barriers; the max over ranks."""
     with torch.no_grad():
-        t0 = time.time()
-        odit.block(P, "blocks.0", x, e0, grid, odit.model_freqs(128), ctx, voc, T, 12)
-        t_block = time.time() - t0
-        Pv = synthetic.fill_state_dict(ovae.param_shapes(), 1)
-        z = torch.randn(1, 16, 1, h, h, generator=g)
-        t0 = time.time()
-        ovae.decode(Pv, z)
-        t_vae_frame = time.time() - t0
-    n_fwd = n_fwd or sample_steps
-    out_frames = out_frames or frames
-    t_clip = n_fwd * 30 * t_block + out_frames * t_vae_frame
-    return {"value": round(out_frames / t_clip, 6), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"oracle fp32: 1 of 30 DiT blocks at B=3,L={L} ({t_block:.1f}s) + VAE decode of 1 latent "
-                      f"frame at {size}x{size} ({t_vae_frame:.1f}s), extrapolated to {n_fwd} forwards x 30 "
-                      f"blocks + {out_frames} frames = {t_clip:.0f}s per clip"}
+        for _ in range(warmup):
+            work.step()
+        barrier(world, dev)
+        if events:
+            work.start_events()
+        t0 = time.perf_counter()
+        out = None
+        for _ in range(steps):
+            out = work.step()
+        barrier(world, dev)
+        dt = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev if dev.type == "cuda" else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = tt.item()
+    return dt, out
 
 
-def main():
-    args = parse()
+def vae_encode_ms(vae, frames, size, dev):
+    from stableavatar_amd import flops
+    ref = torch.zeros(1, 3, frames, size, size, device=dev)
+    ref[:, :, 0].uniform_(-1, 1)
+    with torch.no_grad():
+        vae.encode(ref)
+        sync(dev)
+        te = time.perf_counter()
+        lat_y = vae.encode(ref)[0].mode()
+        sync(dev)
+        te = time.perf_counter() - te
+    assert tuple(lat_y.shape) == (1, 16, (frames - 1) // 4 + 1, size // 8, size // 8)
+    ef = flops.vae_encode_flops(frames, size, size)
+    return {"ms": round(te * 1e3, 1), "tflop": round(ef / 1e12, 2), "tflops_per_s": round(ef / te / 1e12, 1),
+            "note": "AutoencoderKLWan.encode of the reference frame + zeros, once per call; outside the timed "
+                    "region and the metric (SURVEY.md §8(d))"}
+
+
+def attn_traffic(seq_len, layout):
+    """HBM bytes per self-attention launch from the committed rocprofv3 PMC passes, when they were
+    taken on the kernel this build runs at this shape (else None)."""
+    tpath = os.path.join(ROOT, "profiles", "pmc_attn_traffic.json")
+    if layout != "single" or seq_len != 21504 or not os.path.exists(tpath):
+        return None, None
+    with open(tpath) as f:
+        tj = json.load(f)
+    if not tj.get("kernel", "").startswith(ATTN_KERNEL_NAME):
+        return None, None
+    return tj["hbm_bytes_per_launch"], f"profiles/pmc_attn_traffic.json ({tj.get('source', 'rocprofv3 --pmc')})"
+
+
+def run(args, world, rank, dev, work_factory=ClipWorkload):
+    """The measurement; returns the JSON dict on rank 0 (None elsewhere)."""
+    from stableavatar_amd import flops
+    from stableavatar_amd import sp
+    layout = "single" if world == 1 else args.mode
+    work = work_factory(args, dev, rank, world)
+    work.set_layout(layout)
+    dt, video = timed(work, args.steps, args.warmup, world, dev, events=True)
+    work.check(video)
+    attn_ms = work.attention_launch_ms()
+    seq_len = work.seq_len
+    attn_flop = flops.self_attention_flops(B=3, L=seq_len)
+    parallelism = {"single": "single", "replicas": f"replicas{world}", "window-dp": f"windows{world}"}.get(layout)
+    if layout == "sp":
+        plan = sp.make_plan(world, rank, 12)
+        attn_flop /= world  # this rank's (head group, query part) share
+        parallelism = f"ulysses{plan.G}" + (f"x{plan.R}qsplit" if plan.R > 1 else "")
+    shared = layout in ("sp", "window-dp")
+    frames_total = (1 if shared else world) * work.out_frames * args.steps
+    value = frames_total / dt
+    n_fwd = work.n_fwd()
+    path_flop = n_fwd * flops.dit_forward_flops(B=3, L=seq_len, n_frames=work.fpb) + \
+        flops.vae_decode_flops(work.T, work.h, work.h)
+    replicas = None
+    if layout == "sp" and args.replica_steps > 0:
+        work.set_layout("replicas")
+        rdt, rvideo = timed(work, args.replica_steps, 0, world, dev)
+        work.check(rvideo)
+        replicas = {"value": round(world * work.out_frames * args.replica_steps / rdt, 4), "unit": "frames/s",
+                    "steps": args.replica_steps, "ms_per_step": round(rdt / args.replica_steps * 1e3, 1),
+                    "scaling": "weak", "parallelism": f"replicas{world}",
+                    "note": "one independent clip per rank in the same processes (no data-path collective)"}
+    enc = None
+    if not args.no_encode and rank == 0 and hasattr(work, "vae"):
+        enc = vae_encode_ms(work.vae, args.frames, args.size, dev)
+    if rank != 0:
+        return None
+    traffic, traffic_src = attn_traffic(seq_len, layout)
+    achieved = attn_flop / (attn_ms * 1e-3) if attn_ms else None
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.size, args.frames, args.sample_steps, n_fwd, work.out_frames,
+                           config1=not args.no_cpu_config1)
+    n_win = len(work.wins)
+    out = {"metric": METRIC, "value": round(value, 4), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 1), "higher_is_better": True,
+           "scaling": "strong" if shared else "weak", "vs_baseline": None, "dtype": "bf16",
+           "data": "synthetic (random-init weights by name-keyed seed; synthetic text/CLIP/wav2vec features "
+                   "and conditioning latents; CPU-generated initial noise)",
+           "config": {"workload": f"Wan-1.3B StableAvatar {args.size}x{args.size}x{work.out_frames}f"
+                                  + (f" ({n_win} windows of {args.frames}f, overlap {args.overlap})"
+                                     if work.out_frames != args.frames else "")
+                                  + f", {args.sample_steps} steps, CFG x3, single audio clip, VAE decode",
+                      "global_batch": 3 * (1 if shared else world), "seq_len": seq_len,
+                      "dit_forwards_per_clip": n_fwd, "parallelism": parallelism},
+           "roofline": {"bound": "mfma", "kernel": f"{ATTN_KERNEL_NAME} (self-attention, flash, D=128)",
+                        "achieved": round(achieved / 1e12, 1) if achieved else None, "peak": PEAK_BF16 / 1e12,
+                        "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16, 4) if achieved else None,
+                        "traffic": traffic, "traffic_source": traffic_src,
+                        "algorithmic_bytes": 4 * 3 * seq_len * 1536 * 2,
+                        "launch_ms": round(attn_ms, 3) if attn_ms else None, "flop_per_launch": attn_flop},
+           "path_mfma_frac": round(path_flop * args.steps / dt / PEAK_BF16 / (world if shared else 1), 4),
+           "cpu_baseline": cpu, "vae_encode": enc}
+    if replicas is not None:
+        out["replicas"] = replicas
+    return out
+
+
+def main(argv=None, work_factory=ClipWorkload, device=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    if args.sp:
+        args.mode = "sp"
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_workers(args, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    dev = torch.device(f"cuda:{local}")
-    torch.cuda.set_device(dev)
+    if device is None:
+        dev = torch.device(f"cuda:{local}")
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device(device)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
-    from stableavatar_amd import flops
-    from stableavatar_amd.pipeline import WanI2VTalkingInferenceLongPipeline, window_schedule
-    from stableavatar_amd.scheduler import FlowMatchEulerDiscreteScheduler
-
-    sp_mode = args.sp and world > 1
-    wdp = args.window_dp and world > 1
-    if sp_mode and wdp:
-        raise SystemExit("--sp and --window-dp are exclusive")
-    dit, vae = build(dev, seed=0)
-    if sp_mode:
-        dit.enable_multi_gpus_inference()
-    latents, y, ctx, clip, a = make_inputs(dev, args.frames, args.size, seed=42 + (0 if sp_mode or wdp else rank),
-                                           video_frames=args.video_frames)
-    sched = FlowMatchEulerDiscreteScheduler(1000, shift=5.0)
-    sched.set_timesteps(args.sample_steps, device=dev)
-    pipe = WanI2VTalkingInferenceLongPipeline(vae=vae, transformer=dit, scheduler=sched)
-    if wdp:
-        pipe.enable_window_parallel()
-    T = latents.shape[2]
-    fpb = (args.frames - 1) // 4 + 1
-    feats = {(s, e): torch.cat([torch.zeros_like(a), a, a]) for (s, e, _) in window_schedule(T, fpb, args.overlap)}
-    h = args.size // 8
-    seq_len = math.ceil(h * h / 4 * fpb)
-
-    def clip_step():
-        lat = pipe.denoise(latents, y, ctx, clip, feats, sched.timesteps, sched.sigmas, clip_length=args.frames,
-                           seq_len=seq_len, overlap=args.overlap, text_guide_scale=3.0, audio_guide_scale=5.0)
-        return vae.decode_clip(lat[0].float(), post=True)
-
-    def barrier():
-        torch.cuda.synchronize()
-        if world > 1:
-            import torch.distributed as dist
-            dist.barrier()
-            torch.cuda.synchronize()
-
-    with torch.no_grad():
-        for _ in range(args.warmup):
-            clip_step()
-        barrier()
-        dit._events = []
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            video = clip_step()
-        barrier()
-        dt = time.perf_counter() - t0
-        events = dit._events
-        dit._events = None
-    out_frames = 1 + 4 * (T - 1)
-    assert video.shape[1] == out_frames and torch.isfinite(video).all()
-    enc = None
-    if not args.no_encode:  # once-per-call VAE encode of reference frame + zeros (pipeline:679-692), untimed
-        ref = torch.zeros(1, 3, args.frames, args.size, args.size, device=dev)
-        ref[:, :, 0].uniform_(-1, 1)
-        with torch.no_grad():
-            vae.encode(ref)
-            torch.cuda.synchronize()
-            te = time.perf_counter()
-            lat_y = vae.encode(ref)[0].mode()
-            torch.cuda.synchronize()
-            te = time.perf_counter() - te
-        assert tuple(lat_y.shape) == (1, 16, (args.frames - 1) // 4 + 1, args.size // 8, args.size // 8)
-        ef = flops.vae_encode_flops(args.frames, args.size, args.size)
-        enc = {"ms": round(te * 1e3, 1), "tflop": round(ef / 1e12, 2), "tflops_per_s": round(ef / te / 1e12, 1),
-               "note": "AutoencoderKLWan.encode of the reference frame + zeros, once per call; outside the timed "
-                       "region and the metric (SURVEY.md §8(d))"}
-    if world > 1:
-        import torch.distributed as dist
-        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = tt.item()
-    attn_ms = sum(e0.elapsed_time(e1) for e0, e1 in events) / max(len(events), 1)
-    attn_flop = flops.self_attention_flops(B=3, L=seq_len)
-    traffic, traffic_src = None, None
-    tpath = os.path.join(ROOT, "profiles", "pmc_attn_traffic.json")
-    if os.path.exists(tpath) and not args.sp and seq_len == 21504:
-        with open(tpath) as f:
-            tj = json.load(f)
-        traffic = tj["hbm_bytes_per_launch"]
-        traffic_src = f"profiles/pmc_attn_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, {tj['kernel'][:60]})"
-    parallelism = f"replicas{world}" if world > 1 else "single"
-    if wdp:
-        parallelism = f"windows{world}"
-    if sp_mode:
-        from stableavatar_amd import sp
-        plan = sp.make_plan(world, rank, 12)
-        attn_flop /= world  # this rank's (head group, query part) share
-        parallelism = f"ulysses{plan.G}" + (f"x{plan.R}qsplit" if plan.R > 1 else "")
-    achieved = attn_flop / (attn_ms * 1e-3)
-    n_fwd = args.sample_steps * len(window_schedule(T, fpb, args.overlap))
-    path_flop = n_fwd * flops.dit_forward_flops(B=3, L=seq_len, n_frames=fpb) + flops.vae_decode_flops(T, h, h)
-    frames_total = (1 if sp_mode or wdp else world) * out_frames * args.steps
-    value = frames_total / dt
-    if rank == 0:
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.size, args.frames, args.sample_steps, n_fwd, out_frames)
-        out = {"metric": METRIC, "value": round(value, 4), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
-               "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 1), "higher_is_better": True,
-               "scaling": "strong" if sp_mode or wdp else "weak", "vs_baseline": None, "dtype": "bf16",
-               "data": "synthetic (random-init weights by name-keyed seed; synthetic text/CLIP/wav2vec features "
-                       "and conditioning latents; CPU-generated initial noise)",
-               "config": {"workload": f"Wan-1.3B StableAvatar {args.size}x{args.size}x{out_frames}f"
-                                      + (f" ({len(window_schedule(T, fpb, args.overlap))} windows of {args.frames}f,"
-                                         f" overlap {args.overlap})" if out_frames != args.frames else "")
-                                      + f", {args.sample_steps} steps, CFG x3, single audio clip, VAE decode",
-                          "global_batch": 3 * (1 if sp_mode or wdp else world), "seq_len": seq_len,
-                          "dit_forwards_per_clip": n_fwd, "parallelism": parallelism},
-               "roofline": {"bound": "mfma", "kernel": "attn_fwd (self-attention, flash, D=128)",
-                            "achieved": round(achieved / 1e12, 1), "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
-                            "frac": round(achieved / PEAK_BF16, 4), "traffic": traffic, "traffic_source": traffic_src,
-                            "algorithmic_bytes": 4 * 3 * seq_len * 1536 * 2,
-                            "launch_ms": round(attn_ms, 3), "flop_per_launch": attn_flop},
-               "path_mfma_frac": round(path_flop * args.steps / dt / PEAK_BF16 / (world if sp_mode or wdp else 1), 4),
-               "cpu_baseline": cpu, "vae_encode": enc}
+        if not dist.is_initialized():
+            if dev.type == "cuda":
+                dist.init_process_group("nccl", device_id=dev)
+            else:
+                dist.init_process_group("gloo")
+    out = run(args, world, rank, dev, work_factory)
+    if out is not None:
         print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist
+        dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

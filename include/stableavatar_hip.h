@@ -36,20 +36,14 @@ int sa_gemm_bf16(const void* A, int64_t lda, int64_t strideA, const void* W, int
                  int epilogue, const float* residual, int64_t ldr, int64_t strideR, const float* gate,
                  int64_t gate_bstride, int rows_per_batch, void* stream);
 
-/* Kernel-variant selection for A/B benchmarking in one process (also env SA_GEMM_VARIANT /
- * SA_ATTN_VARIANT).  gemm: 0 = 2-phase 8-wave, 1 = 4-phase 8-wave, 2 = 4-wave AGPR, 3 = 8-phase
- * ping-pong, 4 = ping-pong with operand-swapped direct epilogue, 5 = one wave per SIMD with a 32-deep
- * LDS-DMA ring, 9 = same with 64-deep K-tiles, 10 = register-staged, 11 = persistent register-staged,
- * 14 = 9 with spread DMA, 16 = persistent 14, 15 = 16 where K % 128 == 0 else 4 (default);
- * 6-8, 12-13 are
- * measurement ablations (wrong results by construction).  attention: 0 = 2-deep ring, 1 = 3-deep ring
- * with pipelined QK^T, 2 = 0 + deferred rescale, 3 = asm LDS reads with counted waits + XCD order,
- * 4 = 3 + two-group ping-pong, 5 = 3 with prescaled Q and -m as the QK^T accumulator,
- * 6 = 5 on mfma_f32_16x16x32_bf16 (default). */
-int sa_gemm_set_variant(int variant);
-int sa_attn_set_variant(int variant);
-/* GEMM tile raster: runs of group_m tile rows walked column-major (0 = env SA_GEMM_GROUP_M / default). */
-int sa_gemm_set_group_m(int group_m);
+/* sa_gemm_bf16 with the kernel chosen per call (re-entrant A/B; no process-wide state):
+ * kernel 0 = auto (the persistent one-wave-per-SIMD kernel where K % 128 == 0, else the 8-wave
+ * ping-pong), 1 = ping-pong, 2 = persistent (rejected with 1 when K % 128 != 0);
+ * group_m = tile-raster run length (0 = per-kernel default, or env SA_GEMM_GROUP_M read once). */
+int sa_gemm_bf16_ex(const void* A, int64_t lda, int64_t strideA, const void* W, int64_t ldw, int64_t strideW,
+                    const float* bias, void* C, int64_t ldc, int64_t strideC, int M, int N, int K, int batch,
+                    int epilogue, const float* residual, int64_t ldr, int64_t strideR, const float* gate,
+                    int64_t gate_bstride, int rows_per_batch, int kernel, int group_m, void* stream);
 
 /* attention(q,k,v,...) of wan/models/wan_fantasy_transformer3d_1B.py:158-207 (SDPA path, no mask,
  * q_lens/k_lens ignored) for head_dim 128.  Rows of q/k/v/o are flat [rows, stride] bf16 matrices,
@@ -59,6 +53,12 @@ int sa_gemm_set_group_m(int group_m);
 int sa_attn_fwd(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg, int max_q_len,
                 int heads, int head_dim, int64_t q_stride, int64_t k_stride, int64_t v_stride, int64_t o_stride,
                 float scale, int accumulate, void* stream);
+
+/* sa_attn_fwd with the kernel chosen per call (A/B without process-wide state): 0 = auto,
+ * 1 = 8 waves x 32 queries on mfma_f32_16x16x32_bf16. */
+int sa_attn_fwd_ex(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
+                   int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride, int64_t v_stride,
+                   int64_t o_stride, float scale, int accumulate, int kernel, void* stream);
 
 /* The three attentions of WanI2VTalkingCrossAttention.forward (1B:556-603) in one launch: per batch
  * row b, queries q[b*q_len + i] attend to text k/v rows [b*t_len, +t_len), image rows [b*i_len, +i_len)

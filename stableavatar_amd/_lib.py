@@ -16,10 +16,9 @@ HEADER = PKG.parent / "include" / "stableavatar_hip.h"
 # argument codes: p = pointer, i = int32, l = int64, f = float
 SIGNATURES = {
     "sa_gemm_bf16": "pllpllpplliiiiipllplip",
-    "sa_gemm_set_variant": "i",
-    "sa_gemm_set_group_m": "i",
-    "sa_attn_set_variant": "i",
+    "sa_gemm_bf16_ex": "pllpllpplliiiiipllpliiip",
     "sa_attn_fwd": "pppppiiiillllfip",
+    "sa_attn_fwd_ex": "pppppiiiillllfiip",
     "sa_layernorm_mod": "pliplipppplpiiifp",
     "sa_qk_rmsnorm_rope": "pliippiiifpiiiiiiip",
     "sa_patch_im2col": "plllipllliiiiipiip",

@@ -11,9 +11,11 @@
 //
 // Structure (cdna_hip_programming.md App. B "Fused attention prefill"): 8 waves x 32 query rows,
 // KV blocks of 64 keys staged by global_load_lds into a 2-deep LDS ring (XOR-swizzled 256-B rows).
-// Swapped product S^T = K·Q^T (mfma_f32_32x32x16_bf16) puts one query per lane, so the online
-// softmax is lane-local; P^T is fed back as the B operand straight from the accumulator and V^T
-// comes from ds_read_b64_tr_b16, giving O^T with the query on the lane (rescale is per lane).
+// Swapped product S^T = K·Q^T puts one query per lane, so the online softmax is lane-local; P^T is
+// fed back as the B operand straight from the accumulator and V^T comes from ds_read_b64_tr_b16,
+// giving O^T with the query on the lane (rescale is per lane).  Self-attention runs the
+// mfma_f32_16x16x32_bf16 kernel (attn_fwd_v6_kernel); the fused cross-attention reuses the
+// 32x32x16 block body (attn_v3_block).
 #include <stdlib.h>
 
 #include "common.h"
@@ -48,369 +50,13 @@ __device__ __forceinline__ float half_swap_max(float v) {
   return fmax_nc(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
-// OPT adds (cdna_hip_programming.md §5.5): static priority for the younger half (T5 static form),
-// non-canonicalising max chain + permlane32 half-swap (T12), and the deferred rescale (T13): O and l
-// are rescaled only when some query's running max grows by more than RESCALE_THR (log2 units).
-template <bool OPT>
-__global__ __launch_bounds__(512) void attn_fwd_kernel(AttnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int* sg = a.segs + blockIdx.z * 4;
-  const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
-  const int qb = blockIdx.x, h = blockIdx.y;
-  if (qb * QB >= q_len || kv_len <= 0) return;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hi = lane >> 5;
-
-  const int qi = qb * QB + wave * 32 + (lane & 31);
-  const int qc = min(qi, q_len - 1);
-  const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * hi;
-  bf16x8 qf[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
-
-  // staging: each wave moves 2 x 1-KB pieces (4 rows each) of K and of V per block
-  const bf16* kbase = a.k + h * D;
-  const bf16* vbase = a.v + h * D;
-  int srow[2], schunk[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    srow[i] = (wave * 2 + i) * 4 + (lane >> 4);
-    schunk[i] = (lane & 15) ^ gsw(srow[i]);
-  }
-  auto stage = [&](int kb, int buf) {
-    char* base = smem + buf * STAGE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const long key = kv_row0 + min(kb * KVB + srow[i], kv_len - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(kbase + key * a.ks + schunk[i] * 8),
-                                       LDS_PTR(base + (wave * 2 + i) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(vbase + key * a.vs + schunk[i] * 8),
-                                       LDS_PTR(base + TILE_BYTES + (wave * 2 + i) * 1024), 16, 0, 0);
-    }
-  };
-
-  f32x16 O[4];
-#pragma unroll
-  for (int db = 0; db < 4; ++db)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) O[db][r] = 0.f;
-  float m_run = -INFINITY, l_run = 0.f;
-
-  const int nkb = (kv_len + KVB - 1) / KVB;
-  stage(0, 0);
-  if constexpr (OPT)
-    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-  for (int kb = 0; kb < nkb; ++kb) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kb + 1 < nkb) stage(kb + 1, (kb + 1) & 1);
-    const char* Ks = smem + (kb & 1) * STAGE_BYTES;
-    const char* Vs = Ks + TILE_BYTES;
-
-    // S^T[key][query] = K · Q^T
-    f32x16 S[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) S[t][r] = 0.f;
-      const int row = t * 32 + (lane & 31);
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const int ch = 2 * s + hi;
-        const bf16x8 kf = *(const bf16x8*)(Ks + row * 256 + ((ch ^ gsw(row)) << 4));
-        S[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], S[t], 0, 0, 0);
-      }
-    }
-    if (kb * KVB + KVB > kv_len) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kb * KVB + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-          if (key >= kv_len) S[t][r] = -INFINITY;
-        }
-    }
-    if constexpr (OPT) {
-      float mx = S[0][0];
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmax_nc(mx, S[t][r]);
-      mx = half_swap_max(mx) * a.c;
-      if (!__all(mx <= m_run + RESCALE_THR)) {  // wave-uniform decision, before this block's P exists
-        const float m_new = fmax_nc(m_run, mx);
-        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-        l_run *= alpha;
-        m_run = m_new;
-#pragma unroll
-        for (int db = 0; db < 4; ++db)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) O[db][r] *= alpha;
-      }
-      float ps = 0.f;
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(S[t][r], a.c, -m_run));
-          S[t][r] = p;
-          ps += p;
-        }
-      l_run += ps;
-    } else {
-      float mx = S[0][0];
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[t][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_run, mx * a.c);
-      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-      float ps = 0.f;
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(S[t][r], a.c, -m_new));
-          S[t][r] = p;
-          ps += p;
-        }
-      l_run = fmaf(l_run, alpha, ps);
-      m_run = m_new;
-#pragma unroll
-      for (int db = 0; db < 4; ++db)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) O[db][r] *= alpha;
-    }
-
-    // O^T[d][query] += V^T · P^T
-    const int q4 = (lane & 15) >> 2, p4 = lane & 3;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 pb;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pb[j] = f2bf(S[t][8 * s + j]);
-        const int r0 = t * 32 + 16 * s + 4 * hi + q4;
-        const int r1 = r0 + 8;
-#pragma unroll
-        for (int db = 0; db < 4; ++db) {
-          const int col = db * 32 + 16 * ((lane >> 4) & 1) + 4 * p4;
-          const int off0 = r0 * 256 + (((col >> 3) ^ gsw(r0)) << 4) + 8 * ((col >> 2) & 1);
-          const int off1 = r1 * 256 + (((col >> 3) ^ gsw(r1)) << 4) + 8 * ((col >> 2) & 1);
-          const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(Vs + off0));
-          const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(Vs + off1));
-          const bf16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-          O[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb, O[db], 0, 0, 0);
-        }
-      }
-  }
-
-  const float lt = l_run + __shfl_xor(l_run, 32, 64);
-  const float inv = 1.0f / lt;
-  if (qi < q_len) {
-    bf16* op = a.o + (long)(q_row0 + qi) * a.os + h * D;
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {
-        const int d0 = db * 32 + 8 * r4 + 4 * hi;
-        float v0 = O[db][4 * r4 + 0] * inv, v1 = O[db][4 * r4 + 1] * inv;
-        float v2 = O[db][4 * r4 + 2] * inv, v3 = O[db][4 * r4 + 3] * inv;
-        if (a.accumulate) {
-          const bf16x4 old = *(const bf16x4*)(op + d0);
-          v0 += bf2f(old[0]); v1 += bf2f(old[1]); v2 += bf2f(old[2]); v3 += bf2f(old[3]);
-        }
-        *(bf16x4*)(op + d0) = (bf16x4){f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
-      }
-  }
-}
-
-// ---- v2: 3-deep K/V ring, software-pipelined QK^T of block j+1 beside the softmax of block j
-// (T15), deferred rescale with threshold (T13), permlane32 half-wave reductions (T12).
-constexpr int LDS_BYTES_V2 = 3 * STAGE_BYTES;  // 96 KB
-
-__global__ __launch_bounds__(512) void attn_fwd_v2_kernel(AttnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int* sg = a.segs + blockIdx.z * 4;
-  const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
-  const int qb = blockIdx.x, h = blockIdx.y;
-  if (qb * QB >= q_len || kv_len <= 0) return;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hi = lane >> 5;
-
-  const int qi = qb * QB + wave * 32 + (lane & 31);
-  const int qc = min(qi, q_len - 1);
-  const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * hi;
-  bf16x8 qf[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
-
-  const bf16* kbase = a.k + h * D;
-  const bf16* vbase = a.v + h * D;
-  int srow[2], schunk[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    srow[i] = (wave * 2 + i) * 4 + (lane >> 4);
-    schunk[i] = (lane & 15) ^ gsw(srow[i]);
-  }
-  auto stage = [&](int kb) {
-    char* base = smem + (kb % 3) * STAGE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const long key = kv_row0 + min(kb * KVB + srow[i], kv_len - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(kbase + key * a.ks + schunk[i] * 8),
-                                       LDS_PTR(base + (wave * 2 + i) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(vbase + key * a.vs + schunk[i] * 8),
-                                       LDS_PTR(base + TILE_BYTES + (wave * 2 + i) * 1024), 16, 0, 0);
-    }
-  };
-  auto qk = [&](int kb, f32x16* S) {
-    const char* Ks = smem + (kb % 3) * STAGE_BYTES;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) S[t][r] = 0.f;
-      const int row = t * 32 + (lane & 31);
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const int ch = 2 * s + hi;
-        const bf16x8 kf = *(const bf16x8*)(Ks + row * 256 + ((ch ^ gsw(row)) << 4));
-        S[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], S[t], 0, 0, 0);
-      }
-    }
-  };
-
-  f32x16 O[4];
-#pragma unroll
-  for (int db = 0; db < 4; ++db)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) O[db][r] = 0.f;
-  float m_run = -INFINITY, l_run = 0.f;
-  const int nkb = (kv_len + KVB - 1) / KVB;
-  // transposed V reads: with r0 = 32t + 16s + 4hi + q4 the swizzle term gsw(r0) = (q4<<2)|hi does not
-  // depend on (t, s), so each lane needs 8 base addresses and (t, s) become immediate offsets
-  int vaddr[4][2];
-  {
-    const int q4 = (lane & 15) >> 2, p4 = lane & 3;
-    const int g0 = (q4 << 2) | hi, g1 = (q4 << 2) | ((hi + 2) & 3);
-#pragma unroll
-    for (int db = 0; db < 4; ++db) {
-      const int ch = db * 4 + 2 * ((lane >> 4) & 1) + (p4 >> 1);
-      vaddr[db][0] = (4 * hi + q4) * 256 + ((ch ^ g0) << 4) + 8 * (p4 & 1);
-      vaddr[db][1] = (4 * hi + q4 + 8) * 256 + ((ch ^ g1) << 4) + 8 * (p4 & 1);
-    }
-  }
-
-  stage(0);
-  if (nkb > 1) stage(1);
-  if (nkb > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-
-  auto body = [&](int kb, f32x16 (&Sc)[2], f32x16 (&Sn)[2]) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K/V(kb+1) landed (issued one iteration ago)
-    __builtin_amdgcn_s_barrier();                     // ... for every wave; and PV(kb-1) done everywhere
-    asm volatile("" ::: "memory");
-    if (kb + 2 < nkb) stage(kb + 2);  // into the slot PV(kb-1) just released
-    if (kb + 1 < nkb) qk(kb + 1, Sn);  // MFMA work independent of the softmax below
-
-    // ---- softmax of block kb (lane = query; 32 scores here, 32 on the partner half)
-    if (kb * KVB + KVB > kv_len) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kb * KVB + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-          if (key >= kv_len) Sc[t][r] = -INFINITY;
-        }
-    }
-    float mx = Sc[0][0];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmax_nc(mx, Sc[t][r]);
-    mx = half_swap_max(mx) * a.c;
-    if (!__all(mx <= m_run + RESCALE_THR)) {  // wave-uniform: rescale O, l to a new running max
-      const float m_new = fmax_nc(m_run, mx);
-      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-      l_run *= alpha;
-#pragma unroll
-      for (int db = 0; db < 4; ++db)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) O[db][r] *= alpha;
-      m_run = m_new;
-    }
-    float ps = 0.f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(Sc[t][r], a.c, -m_run));
-        Sc[t][r] = p;
-        ps += p;
-      }
-    l_run += ps;
-
-    // ---- O^T += V^T · P^T for block kb
-    const char* Vs = smem + (kb % 3) * STAGE_BYTES + TILE_BYTES;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 pb;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pb[j] = f2bf(Sc[t][8 * s + j]);
-#pragma unroll
-        for (int db = 0; db < 4; ++db) {
-          const char* vb = Vs + (t * 32 + 16 * s) * 256;
-          const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-              (__attribute__((address_space(3))) bf16x4*)(vb + vaddr[db][0]));
-          const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-              (__attribute__((address_space(3))) bf16x4*)(vb + vaddr[db][1]));
-          const bf16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-          O[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb, O[db], 0, 0, 0);
-        }
-      }
-  };
-  f32x16 SA[2], SB[2];
-  qk(0, SA);
-  for (int kb = 0; kb < nkb; kb += 2) {
-    body(kb, SA, SB);
-    if (kb + 1 < nkb) body(kb + 1, SB, SA);
-  }
-
-  const float lt = l_run + __shfl_xor(l_run, 32, 64);
-  const float inv = 1.0f / lt;
-  if (qi < q_len) {
-    bf16* op = a.o + (long)(q_row0 + qi) * a.os + h * D;
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {
-        const int d0 = db * 32 + 8 * r4 + 4 * hi;
-        float v0 = O[db][4 * r4 + 0] * inv, v1 = O[db][4 * r4 + 1] * inv;
-        float v2 = O[db][4 * r4 + 2] * inv, v3 = O[db][4 * r4 + 3] * inv;
-        if (a.accumulate) {
-          const bf16x4 old = *(const bf16x4*)(op + d0);
-          v0 += bf2f(old[0]); v1 += bf2f(old[1]); v2 += bf2f(old[2]); v3 += bf2f(old[3]);
-        }
-        *(bf16x4*)(op + d0) = (bf16x4){f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
-      }
-  }
-}
-
-// ---- v3: v1's structure with every LDS read issued from inline asm at base+immediate addresses
-// and retired by counted lgkmcnt waits (cdna_hip_programming.md §5.7 item 1 form (ii)).  hipcc
-// cannot see these reads, so it neither serialises each K fragment behind its own wait nor drains
-// the next block's LDS-DMA (vmcnt(0)) before the V^T reads, which is what the compiler-scheduled v1
-// does.  K fragments come in groups of 4 (16 VGPR) two groups ahead of their MFMAs; V^T fragments
-// in groups of 8 (one per (t, s) P slice), the first two issued before the softmax.  Deferred
-// rescale as in OPT.
+// ---- 32x32x16 block body (used by the fused cross-attention): every LDS read issued from inline asm
+// at base+immediate addresses and retired by counted lgkmcnt waits (cdna_hip_programming.md §5.7
+// item 1 form (ii)), so hipcc neither serialises each K fragment behind its own wait nor drains the
+// next block's LDS-DMA (vmcnt(0)) before the V^T reads.  K fragments come in groups of 4 (16 VGPR)
+// two groups ahead of their MFMAs; V^T fragments in groups of 8 (one per (t, s) P slice), the first
+// two issued before the softmax.  Deferred rescale (T13): O and l are rescaled only when some
+// query's running max grows by more than RESCALE_THR (log2 units).
 template <int OFF>
 __device__ __forceinline__ void ds_b128(u32x4& d, uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF));
@@ -595,394 +241,6 @@ __device__ __forceinline__ void attn_v3_block(V3State& st, const bf16x8* qf, con
   wait_v<0>(v1);
   mfma_v8(st.O, v1, pslice(S[1], 1));
 }
-
-template <bool NEGM>
-__global__ __launch_bounds__(512) void attn_fwd_v3_kernel(AttnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  // XCD-aware order (T1): consecutive query blocks of one (segment, head) share an XCD, so its L2
-  // serves their common K/V stream
-  const int nx = gridDim.x, ny = gridDim.y;
-  const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
-  const int qb = flat % nx, h = (flat / nx) % ny, seg = flat / (nx * ny);
-  const int* sg = a.segs + seg * 4;
-  const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
-  if (qb * QB >= q_len || kv_len <= 0) return;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hi = lane >> 5;
-
-  const int qi = qb * QB + wave * 32 + (lane & 31);
-  const int qc = min(qi, q_len - 1);
-  const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * hi;
-  bf16x8 qf[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
-  if constexpr (NEGM) {
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[s][j] = f2bf(bf2f(qf[s][j]) * a.c);
-  }
-
-  const bf16* kbase = a.k + h * D;
-  const bf16* vbase = a.v + h * D;
-  int srow[2], schunk[2];
-  const bf16 *kp[2], *vp[2];  // this lane's source of block 0; full blocks advance by a uniform step
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    srow[i] = (wave * 2 + i) * 4 + (lane >> 4);
-    schunk[i] = (lane & 15) ^ gsw(srow[i]);
-    const long key = kv_row0 + min(srow[i], kv_len - 1);
-    kp[i] = kbase + key * a.ks + schunk[i] * 8;
-    vp[i] = vbase + key * a.vs + schunk[i] * 8;
-  }
-  auto stage = [&](int kb, int buf) {
-    char* base = smem + buf * STAGE_BYTES;
-    const bool full = kb * KVB + KVB <= kv_len;  // wave-uniform
-    const long ko = (long)kb * KVB * a.ks, vo = (long)kb * KVB * a.vs;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const bf16 *ksrc = kp[i] + ko, *vsrc = vp[i] + vo;
-      if (!full) {
-        const long key = kv_row0 + min(kb * KVB + srow[i], kv_len - 1);
-        ksrc = kbase + key * a.ks + schunk[i] * 8;
-        vsrc = vbase + key * a.vs + schunk[i] * 8;
-      }
-      __builtin_amdgcn_global_load_lds((const void*)ksrc, LDS_PTR(base + (wave * 2 + i) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)vsrc, LDS_PTR(base + TILE_BYTES + (wave * 2 + i) * 1024), 16,
-                                       0, 0);
-    }
-  };
-
-  // per-lane LDS byte addresses of stage 0 (t = s = 0); every other read is +immediate
-  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
-  uint32_t ka[8], va[8];
-  {
-    const int row = lane & 31;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) ka[s] = lds0 + row * 256 + (((2 * s + hi) ^ gsw(row)) << 4);
-    const int q4 = (lane & 15) >> 2, p4 = lane & 3;
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const int r = 4 * hi + q4 + 8 * hh;
-        const int col = db * 32 + 16 * ((lane >> 4) & 1) + 4 * p4;
-        va[2 * db + hh] = lds0 + r * 256 + (((col >> 3) ^ gsw(r)) << 4) + 8 * ((col >> 2) & 1);
-      }
-  }
-
-  V3State st;
-#pragma unroll
-  for (int db = 0; db < 4; ++db)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) st.O[db][r] = 0.f;
-  st.m_run = NEGM ? 0.f : -INFINITY;
-  st.l_run = 0.f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) st.negm[r] = 0.f;
-
-  const int nkb = (kv_len + KVB - 1) / KVB;
-  stage(0, 0);
-  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-  for (int kb = 0; kb < nkb; kb += 2) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kb + 1 < nkb) stage(kb + 1, 1);
-    attn_v3_block<0, NEGM>(st, qf, ka, va, kb, kv_len, a.c, hi);
-    if (kb + 1 >= nkb) break;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kb + 2 < nkb) stage(kb + 2, 0);
-    attn_v3_block<1, NEGM>(st, qf, ka, va, kb + 1, kv_len, a.c, hi);
-  }
-
-  const float lt = st.l_run + __shfl_xor(st.l_run, 32, 64);
-  const float inv = 1.0f / lt;
-  // lanes q and q+32 hold alternating 4-column groups k (columns 8k..8k+3 / 8k+4..8k+7) of one query
-  // row; one permlane32 swap per dword pairs groups (k, k+1) so every lane stores 16 contiguous bytes
-  // (cdna_hip_programming.md T21: 8 dwordx4 stores instead of 16 dwordx2)
-  bf16* op = a.o + (long)(q_row0 + min(qi, q_len - 1)) * a.os + h * D + 8 * hi;
-#pragma unroll
-  for (int k = 0; k < 16; k += 2) {
-    const f32x16& Oa = st.O[k >> 2];
-    const f32x16& Ob = st.O[(k + 1) >> 2];
-    const int ia = 4 * (k & 3), ib = 4 * ((k + 1) & 3);
-    const bf16x4 pa = {f2bf(Oa[ia] * inv), f2bf(Oa[ia + 1] * inv), f2bf(Oa[ia + 2] * inv), f2bf(Oa[ia + 3] * inv)};
-    const bf16x4 pb = {f2bf(Ob[ib] * inv), f2bf(Ob[ib + 1] * inv), f2bf(Ob[ib + 2] * inv), f2bf(Ob[ib + 3] * inv)};
-    const u32x2 ga = __builtin_bit_cast(u32x2, pa), gb = __builtin_bit_cast(u32x2, pb);
-    const auto rx = __builtin_amdgcn_permlane32_swap(ga[0], gb[0], false, false);
-    const auto ry = __builtin_amdgcn_permlane32_swap(ga[1], gb[1], false, false);
-    u32x4 out = {rx[0], ry[0], rx[1], ry[1]};
-    bf16* p = op + 8 * k;
-    if (a.accumulate) {  // bf16 + bf16 as the reference's sum of attention outputs (1B:602)
-      const bf16x8 ov = *(const bf16x8*)p;
-      bf16x8 nv = __builtin_bit_cast(bf16x8, out);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) nv[j] = f2bf(bf2f(ov[j]) + bf2f(nv[j]));
-      out = __builtin_bit_cast(u32x4, nv);
-    }
-    if (qi < q_len) *(u32x4*)p = out;
-  }
-}
-
-// ---- v4: v3's reads plus a two-group ping-pong (cdna_hip_programming.md §5.5 T5/T16,
-// MI355X_MICROARCH.md "Two waves per SIMD").  Each SIMD holds one wave of group 0 (waves 0-3) and
-// one of group 1 (waves 4-7); group 1 runs one barrier behind, so in every barrier interval one
-// wave of the pair is in its matrix segment (P_j·V_j then K_{j+1}·Q^T: 32 MFMAs) while the other
-// is in its softmax segment (VALU).  K and V live in separate 2-slot rings: K_{j+2} and V_{j+1}
-// are issued in interval 2j+1 (group 0 inside its matrix segment, group 1 inside its softmax) and
-// retired by each issuer's vmcnt(0) before barrier 2j+2, after which both groups read them.
-constexpr int V4_K0 = 0, V4_V0 = 2 * TILE_BYTES;  // K slots 0/1, then V slots 0/1 (64 KB)
-
-template <int SLOT>
-__device__ __forceinline__ void v4_issue_k(const bf16* kb, long ks, const int* srow, const int* schunk, int kv_row0,
-                                           int blk, int kv_len, char* smem, int wave) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const long key = kv_row0 + min(blk * KVB + srow[i], kv_len - 1);
-    __builtin_amdgcn_global_load_lds((const void*)(kb + key * ks + schunk[i] * 8),
-                                     LDS_PTR(smem + V4_K0 + SLOT * TILE_BYTES + (wave * 2 + i) * 1024), 16, 0, 0);
-  }
-}
-template <int SLOT>
-__device__ __forceinline__ void v4_issue_v(const bf16* vb, long vs, const int* srow, const int* schunk, int kv_row0,
-                                           int blk, int kv_len, char* smem, int wave) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const long key = kv_row0 + min(blk * KVB + srow[i], kv_len - 1);
-    __builtin_amdgcn_global_load_lds((const void*)(vb + key * vs + schunk[i] * 8),
-                                     LDS_PTR(smem + V4_V0 + SLOT * TILE_BYTES + (wave * 2 + i) * 1024), 16, 0, 0);
-  }
-}
-
-template <int SLOT, int T, int S0>
-__device__ __forceinline__ void v4_read_k4(u32x4* f, const uint32_t* ka) {
-  constexpr int base = V4_K0 + SLOT * TILE_BYTES + T * 8192;
-  ds_b128<base>(f[0], ka[S0 + 0]);
-  ds_b128<base>(f[1], ka[S0 + 1]);
-  ds_b128<base>(f[2], ka[S0 + 2]);
-  ds_b128<base>(f[3], ka[S0 + 3]);
-}
-template <int SLOT, int T, int S>
-__device__ __forceinline__ void v4_read_v8(u32x2* f, const uint32_t* va) {
-  constexpr int base = V4_V0 + SLOT * TILE_BYTES + T * 8192 + S * 4096;
-  ds_tr64<base>(f[0], va[0]); ds_tr64<base>(f[1], va[1]);
-  ds_tr64<base>(f[2], va[2]); ds_tr64<base>(f[3], va[3]);
-  ds_tr64<base>(f[4], va[4]); ds_tr64<base>(f[5], va[5]);
-  ds_tr64<base>(f[6], va[6]); ds_tr64<base>(f[7], va[7]);
-}
-
-// S^T of one block from K slot SLOT (prologue / tail of the matrix segment)
-template <int SLOT>
-__device__ __forceinline__ void v4_qk(f32x16* S, const bf16x8* qf, const uint32_t* ka) {
-  u32x4 ka0[4], ka1[4], kb0[4], kb1[4];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) { S[0][r] = 0.f; S[1][r] = 0.f; }
-  v4_read_k4<SLOT, 0, 0>(ka0, ka);
-  v4_read_k4<SLOT, 0, 4>(ka1, ka);
-  wait_k<4>(ka0);
-  mfma_k4(S[0], ka0, qf);
-  __builtin_amdgcn_sched_barrier(0);
-  v4_read_k4<SLOT, 1, 0>(kb0, ka);
-  wait_k<4>(ka1);
-  mfma_k4(S[0], ka1, qf + 4);
-  __builtin_amdgcn_sched_barrier(0);
-  v4_read_k4<SLOT, 1, 4>(kb1, ka);
-  wait_k<4>(kb0);
-  mfma_k4(S[1], kb0, qf);
-  __builtin_amdgcn_sched_barrier(0);
-  wait_k<0>(kb1);
-  mfma_k4(S[1], kb1, qf + 4);
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-// softmax segment of block kb: S -> P (fp32, in place), deferred rescale of O / l
-__device__ __forceinline__ void v4_softmax(V3State& st, f32x16* S, int kb, int kv_len, float c, int hi) {
-  if (kb * KVB + KVB > kv_len) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kb * KVB + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-        if (key >= kv_len) S[t][r] = -INFINITY;
-      }
-  }
-  float mx = S[0][0];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[t][r]);
-  {
-    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-    mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * c;
-  }
-  if (!__all(mx <= st.m_run + RESCALE_THR)) {
-    const float m_new = fmaxf(st.m_run, mx);
-    const float alpha = __builtin_amdgcn_exp2f(st.m_run - m_new);
-    st.l_run *= alpha;
-    st.m_run = m_new;
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) st.O[db][r] *= alpha;
-  }
-  float ps = 0.f;
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float p = __builtin_amdgcn_exp2f(fmaf(S[t][r], c, -st.m_run));
-      S[t][r] = p;
-      ps += p;
-    }
-  st.l_run += ps;
-}
-
-// matrix segment of block j: O += V_j^T P_j^T (V slot VS), then S = K_{j+1} Q^T (K slot VS ^ 1)
-template <int VS>
-__device__ __forceinline__ void v4_matrix(V3State& st, f32x16* S, const bf16x8* qf, const uint32_t* ka,
-                                          const uint32_t* va, bool next) {
-  u32x2 v0[8], v1[8];
-  v4_read_v8<VS, 0, 0>(v0, va);
-  v4_read_v8<VS, 0, 1>(v1, va);
-  wait_v<8>(v0);
-  mfma_v8(st.O, v0, pslice(S[0], 0));
-  __builtin_amdgcn_sched_barrier(0);
-  v4_read_v8<VS, 1, 0>(v0, va);
-  wait_v<8>(v1);
-  mfma_v8(st.O, v1, pslice(S[0], 1));
-  __builtin_amdgcn_sched_barrier(0);
-  v4_read_v8<VS, 1, 1>(v1, va);
-  wait_v<8>(v0);
-  mfma_v8(st.O, v0, pslice(S[1], 0));
-  __builtin_amdgcn_sched_barrier(0);
-  wait_v<0>(v1);
-  mfma_v8(st.O, v1, pslice(S[1], 1));
-  __builtin_amdgcn_sched_barrier(0);
-  if (next) v4_qk<VS ^ 1>(S, qf, ka);
-}
-
-template <bool G1>
-__device__ __forceinline__ void v4_loop(V3State& st, const bf16x8* qf, const uint32_t* ka, const uint32_t* va,
-                                        const bf16* kb, const bf16* vb, long ks, long vs, const int* srow,
-                                        const int* schunk, int kv_row0, int kv_len, float c, int hi, char* smem,
-                                        int wave) {
-  const int nkb = (kv_len + KVB - 1) / KVB;
-  f32x16 S[2];
-  // prologue: K_0, V_0 -> slot 0, K_1 -> slot 1; S = K_0 Q^T
-  v4_issue_k<0>(kb, ks, srow, schunk, kv_row0, 0, kv_len, smem, wave);
-  v4_issue_v<0>(vb, vs, srow, schunk, kv_row0, 0, kv_len, smem, wave);
-  if (nkb > 1) v4_issue_k<1>(kb, ks, srow, schunk, kv_row0, 1, kv_len, smem, wave);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  v4_qk<0>(S, qf, ka);
-  if (G1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind
-#define SA_V4_STEP(PAR, J)                                                                              \
-  {                                                                                                     \
-    const int j = (J);                                                                                  \
-    v4_softmax(st, S, j, kv_len, c, hi);                                                                \
-    if (G1) {                                                                                           \
-      if (j + 2 < nkb) v4_issue_k<PAR>(kb, ks, srow, schunk, kv_row0, j + 2, kv_len, smem, wave);       \
-      if (j + 1 < nkb) v4_issue_v<PAR ^ 1>(vb, vs, srow, schunk, kv_row0, j + 1, kv_len, smem, wave);   \
-    } else {                                                                                            \
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                                  \
-    }                                                                                                   \
-    __builtin_amdgcn_s_barrier();                                                                       \
-    __builtin_amdgcn_sched_barrier(0);                                                                  \
-    if (!G1) {                                                                                          \
-      if (j + 2 < nkb) v4_issue_k<PAR>(kb, ks, srow, schunk, kv_row0, j + 2, kv_len, smem, wave);       \
-      if (j + 1 < nkb) v4_issue_v<PAR ^ 1>(vb, vs, srow, schunk, kv_row0, j + 1, kv_len, smem, wave);   \
-    }                                                                                                   \
-    v4_matrix<PAR>(st, S, qf, ka, va, j + 1 < nkb);                                                     \
-    if (G1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                           \
-    __builtin_amdgcn_s_barrier();                                                                       \
-    __builtin_amdgcn_sched_barrier(0);                                                                  \
-  }
-  for (int j0 = 0; j0 < nkb; j0 += 2) {
-    SA_V4_STEP(0, j0)
-    if (j0 + 1 >= nkb) break;
-    SA_V4_STEP(1, j0 + 1)
-  }
-#undef SA_V4_STEP
-  if (!G1) __builtin_amdgcn_s_barrier();  // balance group 1's extra barrier
-}
-
-__global__ __launch_bounds__(512) void attn_fwd_v4_kernel(AttnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int* sg = a.segs + blockIdx.z * 4;
-  const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
-  const int qb = blockIdx.x, h = blockIdx.y;
-  if (qb * QB >= q_len || kv_len <= 0) return;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hi = lane >> 5;
-
-  const int qi = qb * QB + wave * 32 + (lane & 31);
-  const int qc = min(qi, q_len - 1);
-  const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * hi;
-  bf16x8 qf[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
-
-  int srow[2], schunk[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    srow[i] = (wave * 2 + i) * 4 + (lane >> 4);
-    schunk[i] = (lane & 15) ^ gsw(srow[i]);
-  }
-  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
-  uint32_t ka[8], va[8];
-  {
-    const int row = lane & 31;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) ka[s] = lds0 + row * 256 + (((2 * s + hi) ^ gsw(row)) << 4);
-    const int q4 = (lane & 15) >> 2, p4 = lane & 3;
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const int r = 4 * hi + q4 + 8 * hh;
-        const int col = db * 32 + 16 * ((lane >> 4) & 1) + 4 * p4;
-        va[2 * db + hh] = lds0 + r * 256 + (((col >> 3) ^ gsw(r)) << 4) + 8 * ((col >> 2) & 1);
-      }
-  }
-
-  V3State st;
-#pragma unroll
-  for (int db = 0; db < 4; ++db)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) st.O[db][r] = 0.f;
-  st.m_run = -INFINITY;
-  st.l_run = 0.f;
-
-  const bf16* kbase = a.k + h * D;
-  const bf16* vbase = a.v + h * D;
-  if (wave >= 4)
-    v4_loop<true>(st, qf, ka, va, kbase, vbase, a.ks, a.vs, srow, schunk, kv_row0, kv_len, a.c, hi, smem, wave);
-  else
-    v4_loop<false>(st, qf, ka, va, kbase, vbase, a.ks, a.vs, srow, schunk, kv_row0, kv_len, a.c, hi, smem, wave);
-
-  const float lt = st.l_run + __shfl_xor(st.l_run, 32, 64);
-  const float inv = 1.0f / lt;
-  if (qi < q_len) {
-    bf16* op = a.o + (long)(q_row0 + qi) * a.os + h * D;
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {
-        const int d0 = db * 32 + 8 * r4 + 4 * hi;
-        float v0 = st.O[db][4 * r4 + 0] * inv, v1 = st.O[db][4 * r4 + 1] * inv;
-        float v2 = st.O[db][4 * r4 + 2] * inv, v3 = st.O[db][4 * r4 + 3] * inv;
-        if (a.accumulate) {
-          const bf16x4 old = *(const bf16x4*)(op + d0);
-          v0 += bf2f(old[0]); v1 += bf2f(old[1]); v2 += bf2f(old[2]); v3 += bf2f(old[3]);
-        }
-        *(bf16x4*)(op + d0) = (bf16x4){f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
-      }
-  }
-}
-
 // ---- fused cross-attention of WanI2VTalkingCrossAttention (1B:556-603): per query block, the text
 // (1B:564-570), image (1B:556-562) and per-frame vocal (1B:575-586) attentions run back to back over
 // one K/V block stream, each with its own online softmax, and the three outputs are summed with the
@@ -1496,66 +754,34 @@ __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) {
   }
 }
 
-int g_attn_variant = -1;  // 0 = v1 (2-deep ring), 1 = v2 (3-deep ring, pipelined QK^T, deferred rescale),
-                          // 2 = v1 + static priority, half-swap max, deferred rescale,
-                          // 3 = v1 structure with asm LDS reads + counted waits (v3),
-                          // 4 = v3 reads + two-group ping-pong (v4), 5 = v3 with prescaled Q and -m as
-                          // the QK^T initial accumulator, 6 = v5 on mfma_f32_16x16x32_bf16
-
-extern "C" int sa_attn_set_variant(int variant) {
-  if (variant < 0 || variant > 6) return SA_ERR_ARG;
-  g_attn_variant = variant;
+// kernel: 0 = auto, 1 = attn_fwd_v6_kernel (8 waves x 32 queries, mfma_f32_16x16x32_bf16)
+extern "C" int sa_attn_fwd_ex(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
+                              int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride,
+                              int64_t v_stride, int64_t o_stride, float scale, int accumulate, int kernel,
+                              void* stream) {
+  if (!q || !k || !v || !o || !segs || nseg <= 0 || max_q_len <= 0 || heads <= 0) return SA_ERR_ARG;
+  if (head_dim != D) return SA_ERR_ARG;
+  if ((q_stride | k_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
+  if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)o)) & 15) return SA_ERR_ARG;
+  if (kernel < 0 || kernel > 1) return SA_ERR_ARG;
+  static const bool attr = [] {  // one-time, thread-safe
+    (void)hipFuncSetAttribute((const void*)attn_fwd_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    return true;
+  }();
+  (void)attr;
+  AttnArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, segs,
+             q_stride, k_stride, v_stride, o_stride, scale * 1.4426950408889634f, accumulate};
+  dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
+  hipLaunchKernelGGL(attn_fwd_v6_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+  SA_LAUNCH_CHECK();
   return SA_OK;
 }
 
 extern "C" int sa_attn_fwd(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
                            int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride,
                            int64_t v_stride, int64_t o_stride, float scale, int accumulate, void* stream) {
-  if (!q || !k || !v || !o || !segs || nseg <= 0 || max_q_len <= 0 || heads <= 0) return SA_ERR_ARG;
-  if (head_dim != D) return SA_ERR_ARG;
-  if ((q_stride | k_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
-  if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)o)) & 15) return SA_ERR_ARG;
-  static bool attr = false;
-  if (g_attn_variant < 0) {
-    const char* e = getenv("SA_ATTN_VARIANT");
-    g_attn_variant = e ? atoi(e) : 6;
-  }
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_v3_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_v3_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_v4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_v2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES_V2);
-    attr = true;
-  }
-  AttnArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, segs,
-             q_stride, k_stride, v_stride, o_stride, scale * 1.4426950408889634f, accumulate};
-  dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
-  if (g_attn_variant == 0)
-    hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
-  else if (g_attn_variant == 2)
-    hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
-  else if (g_attn_variant == 3)
-    hipLaunchKernelGGL(attn_fwd_v3_kernel<false>, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
-  else if (g_attn_variant == 5)
-    hipLaunchKernelGGL(attn_fwd_v3_kernel<true>, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
-  else if (g_attn_variant == 4)
-    hipLaunchKernelGGL(attn_fwd_v4_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
-  else if (g_attn_variant == 6)
-    hipLaunchKernelGGL(attn_fwd_v6_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL(attn_fwd_v2_kernel, grid, dim3(512), LDS_BYTES_V2, (hipStream_t)stream, a);
-  SA_LAUNCH_CHECK();
-  return SA_OK;
+  return sa_attn_fwd_ex(q, k, v, o, segs, nseg, max_q_len, heads, head_dim, q_stride, k_stride, v_stride, o_stride,
+                        scale, accumulate, 0, stream);
 }
 
 extern "C" int sa_attn_cross3(const void* q, int64_t q_stride, const void* kt, const void* vt, int64_t t_stride,
@@ -1573,12 +799,12 @@ extern "C" int sa_attn_cross3(const void* q, int64_t q_stride, const void* kt, c
   if ((((uintptr_t)q) | ((uintptr_t)kt) | ((uintptr_t)vt) | ((uintptr_t)ki) | ((uintptr_t)vi) | ((uintptr_t)kv) |
        ((uintptr_t)vv) | ((uintptr_t)o)) & 15)
     return SA_ERR_ARG;
-  static bool attr = false;
-  if (!attr) {
+  static const bool attr = [] {
     (void)hipFuncSetAttribute((const void*)attn_cross3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
-    attr = true;
-  }
+    return true;
+  }();
+  (void)attr;
   Cross3Args a{(const bf16*)q, q_stride, (const bf16*)kt, (const bf16*)vt, t_stride, t_len, (const bf16*)ki,
                (const bf16*)vi, i_stride, i_len, (const bf16*)kv, (const bf16*)vv, v_stride, nper,
                tokens_per_frame, n_frames, tok_offset, (bf16*)o, o_stride, q_len, scale * 1.4426950408889634f};

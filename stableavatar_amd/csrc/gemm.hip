@@ -5,13 +5,13 @@
 // Replaces the aten::addmm sites listed in SURVEY.md §2.2 (wan_fantasy_transformer3d_1B.py
 // :376-379,550-554,577-578,644-646,832-838,710, vocal_projector_fantasy_1B.py:238-241,313-316).
 //
-// Main kernel (gemm_phased_kernel): 256x256 block tile, BK = 64, 8 waves, mfma_f32_16x16x32_bf16.
-// Each K-tile is split into four 128x64 half-tiles {A0, A1, B0, B1} staged by global_load_lds into
-// a 2-deep LDS ring (XOR-swizzled 128-B rows, source-side swizzle, lane-linear LDS image).  A K-tile is
-// computed in four phases, one block-quadrant (A_i x B_j) per phase, each wave owning a 64x32
-// sub-tile of every quadrant; each phase issues the next K-tile's half-tile for the slot it frees,
-// so three half-tiles stay in flight across the raw s_barrier and the wait is a counted vmcnt(6)
-// (cdna_hip_programming.md §5 "256^2 8-phase template", T3/T4/T5).  XCD-aware block order (T1).
+// Two kernels, chosen per call (sa_gemm_bf16_ex; auto = the persistent one wherever it applies):
+//  * gemm_s8_kernel: persistent, one wave per SIMD, 256x256 tile, 4 waves x 128x128 with the
+//    accumulators in AGPRs, K-tiles of 64 staged by buffer_load...lds into a 2-stage XOR-swizzled
+//    LDS ring, the K pipeline running across tile seams (needs K % 128 == 0);
+//  * gemm_pp_kernel: 8-wave ping-pong over the same 256x256 tile for any K % 64 == 0
+//    (cdna_hip_programming.md §5 "256^2 8-phase template", T3/T4/T5).
+// Both use an XCD-aware tile order (T1) and fuse bias / GELU / SiLU / fp32 gated-residual epilogues.
 #include <stdlib.h>
 
 #include "common.h"
@@ -124,172 +124,8 @@ __device__ __forceinline__ void epi_row(const GemmArgs& g, float* v, long bz, in
 }
 
 // ------------------------------------------------------------------------------------------------
-// phased kernel
-
-template <int EPI>
-__global__ __launch_bounds__(512) void gemm_phased_kernel(GemmArgs g) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int qm = wave >> 2, qn = wave & 3;  // this wave's 64x32 sub-tile inside each 128x128 quadrant
-  const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
-  const int wg = xcd_remap(blockIdx.x, nm * nn);
-  int mt, nt;
-  tile_coords(wg, nm, nn, g.group_m, mt, nt);
-  const int m0 = mt * BM, n0 = nt * BN;
-  const long bz = blockIdx.z;
-  const bf16* A = g.A + bz * g.sA;
-  const bf16* W = g.W + bz * g.sW;
-
-  // staging: half-tile h in {0:A0, 1:A1, 2:B0, 3:B1}; 2 glds per thread per half-tile
-  long goff[4][2];
-#pragma unroll
-  for (int h = 0; h < 4; ++h)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int j = i * 8 + wave;
-      const int row = j * 8 + (lane >> 3);
-      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-      if (h < 2) {
-        const int r = min(m0 + h * 128 + row, g.M - 1);
-        goff[h][i] = (long)r * g.lda + chunk * 8;
-      } else {
-        const int r = min(n0 + (h - 2) * 128 + row, g.N - 1);
-        goff[h][i] = (long)r * g.ldw + chunk * 8;
-      }
-    }
-  auto issue = [&](int h, int kt, int buf) {
-    const long k0 = (long)kt * BK;
-    const bf16* base = h < 2 ? A : W;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int j = i * 8 + wave;
-      __builtin_amdgcn_global_load_lds((const void*)(base + goff[h][i] + k0),
-                                       LDS_PTR(smem + buf * STAGE_BYTES + h * HALF_BYTES + j * 1024), 16, 0, 0);
-    }
-  };
-
-  f32x4 acc[4][4][2];
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int n = 0; n < 2; ++n) acc[q][m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  // phase p reads quadrant (A_i, B_j): p0 (A0,B0) p1 (A0,B1) p2 (A1,B1) p3 (A1,B0);
-  // it issues the next K-tile's half-tile in order A0, B0, B1, A1 (the slot freed earliest first)
-  const int nk = g.K / BK;
-  issue(0, 0, 0);
-  issue(2, 0, 0);
-  issue(3, 0, 0);
-  issue(1, 0, 0);
-  bf16x8 a[4][2], b0[2][2], b1[2][2];
-  const int c0 = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool nxt = kt + 1 < nk;
-    const char* S = smem + cur * STAGE_BYTES;
-#define SA_PHASE_WAIT(VN, VL)                                          \
-  if (nxt) asm volatile("s_waitcnt vmcnt(" #VN ")" ::: "memory");     \
-  else asm volatile("s_waitcnt vmcnt(" #VL ")" ::: "memory");          \
-  __builtin_amdgcn_s_barrier();                                        \
-  asm volatile("" ::: "memory");
-    // ---- phase 0: A0 x B0
-    if (nxt) issue(0, kt + 1, cur ^ 1);
-    SA_PHASE_WAIT(6, 4)
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) a[m][kk] = *(const bf16x8*)(S + 0 * HALF_BYTES + swz128(qm * 64 + m * 16 + (lane & 15), kk * 4 + c0));
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) b0[n][kk] = *(const bf16x8*)(S + 2 * HALF_BYTES + swz128(qn * 32 + n * 16 + (lane & 15), kk * 4 + c0));
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 2; ++n) acc[0][m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m][kk], b0[n][kk], acc[0][m][n], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    // ---- phase 1: A0 x B1
-    if (nxt) issue(2, kt + 1, cur ^ 1);
-    SA_PHASE_WAIT(6, 2)
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) b1[n][kk] = *(const bf16x8*)(S + 3 * HALF_BYTES + swz128(qn * 32 + n * 16 + (lane & 15), kk * 4 + c0));
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 2; ++n) acc[1][m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m][kk], b1[n][kk], acc[1][m][n], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    // ---- phase 2: A1 x B1
-    if (nxt) issue(3, kt + 1, cur ^ 1);
-    SA_PHASE_WAIT(6, 0)
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) a[m][kk] = *(const bf16x8*)(S + 1 * HALF_BYTES + swz128(qm * 64 + m * 16 + (lane & 15), kk * 4 + c0));
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 2; ++n) acc[2][m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m][kk], b1[n][kk], acc[2][m][n], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    // ---- phase 3: A1 x B0 (operands already in registers)
-    if (nxt) issue(1, kt + 1, cur ^ 1);
-    SA_PHASE_WAIT(8, 0)
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 2; ++n) acc[3][m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m][kk], b0[n][kk], acc[3][m][n], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-#undef SA_PHASE_WAIT
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  // epilogue: per wave and per (quadrant, m-tile) a 16x32 fp32 strip through LDS; 8 columns per lane
-  float* strip = (float*)(smem + wave * (16 * 36 * 4));
-  const int er = lane >> 2, ec = (lane & 3) * 8;
-  const int qa[4] = {0, 0, 1, 1}, qb[4] = {0, 1, 1, 0};
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) strip[((lane >> 4) * 4 + i) * 36 + n * 16 + (lane & 15)] = acc[q][m][n][i];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-      float v[8];
-      const f32x4 t0 = *(const f32x4*)(strip + er * 36 + ec);
-      const f32x4 t1 = *(const f32x4*)(strip + er * 36 + ec + 4);
-      v[0] = t0[0]; v[1] = t0[1]; v[2] = t0[2]; v[3] = t0[3];
-      v[4] = t1[0]; v[5] = t1[1]; v[6] = t1[2]; v[7] = t1[3];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-      const int grow = m0 + qa[q] * 128 + qm * 64 + m * 16 + er;
-      const int gcol = n0 + qb[q] * 128 + qn * 32 + ec;
-      if (grow < g.M && gcol < g.N) epi_row<EPI, 8>(g, v, bz, grow, gcol);
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
 // ping-pong kernel (cdna_hip_programming.md "The 256² 8-phase template"): same tile, waves and
-// quadrant phases as gemm_phased_kernel, but every phase is {ds_read the phase's fragments, issue one
+// quadrant phases (one block quadrant A_i x B_j per phase), but every phase is {ds_read the phase's fragments, issue one
 // half-tile, counted vmcnt} barrier {16 MFMAs} barrier, and waves 4-7 run one barrier behind waves
 // 0-3, so on each SIMD one wave reads while its partner multiplies.  Two K-tiles per iteration
 // (E = 2i in buffer 0, O = 2i+1 in buffer 1); phase ph issues, in order,
@@ -554,230 +390,11 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// w4 kernel: 4 waves x (128x128 per wave), one wave per SIMD with the 256 accumulators in AGPRs.
-// K is staged in 32-deep sub-tiles (A 256x32 + B 256x32 = 32 KB) through a 4-slot LDS ring: while
-// sub-tile s is multiplied, s+1 is already landed (its fragments are read between the MFMAs of s)
-// and s+2, s+3 are in flight -> one barrier per 64 MFMAs/wave and a counted vmcnt(8).
-constexpr int W4_SLOT = 2 * 256 * 64;  // A + B sub-tile, 64-B rows
-constexpr int W4_LDS = 4 * W4_SLOT;    // 128 KB
-
-__device__ __forceinline__ int swz64(int r, int c) { return r * 64 + ((c ^ ((r >> 1) & 3)) << 4); }
-
-template <int EPI>
-__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs g) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
-  const int wg = xcd_remap(blockIdx.x, nm * nn);
-  int mt, nt;
-  tile_coords(wg, nm, nn, g.group_m, mt, nt);
-  const int m0 = mt * BM, n0 = nt * BN;
-  const long bz = blockIdx.z;
-  const bf16* A = g.A + bz * g.sA;
-  const bf16* W = g.W + bz * g.sW;
-
-  // staging: per sub-tile each wave issues 4 A + 4 B wave-instructions of 16 rows x 64 B
-  long aoff[4], woff[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = (i * 4 + wave) * 16 + (lane >> 2);
-    const int chunk = (lane & 3) ^ ((row >> 1) & 3);
-    aoff[i] = (long)min(m0 + row, g.M - 1) * g.lda + chunk * 8;
-    woff[i] = (long)min(n0 + row, g.N - 1) * g.ldw + chunk * 8;
-  }
-  const int ns = g.K / 32;
-  auto issue = [&](int s) {
-    char* base = smem + (s & 3) * W4_SLOT;
-    const long k0 = (long)s * 32;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      __builtin_amdgcn_global_load_lds((const void*)(A + aoff[i] + k0), LDS_PTR(base + (i * 4 + wave) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(W + woff[i] + k0),
-                                       LDS_PTR(base + 256 * 64 + (i * 4 + wave) * 1024), 16, 0, 0);
-    }
-  };
-  auto read = [&](int s, bf16x8 (&a)[8], bf16x8 (&b)[8]) {
-    const char* base = smem + (s & 3) * W4_SLOT;
-    const int c = lane >> 4;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a[i] = *(const bf16x8*)(base + swz64(wm * 128 + i * 16 + (lane & 15), c));
-#pragma unroll
-    for (int j = 0; j < 8; ++j) b[j] = *(const bf16x8*)(base + 256 * 64 + swz64(wn * 128 + j * 16 + (lane & 15), c));
-  };
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  // prologue: sub-tiles 0..2 in flight, wait for 0 and 1
-  issue(0);
-  if (ns > 1) issue(1);
-  if (ns > 2) issue(2);
-  if (ns > 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  bf16x8 a0[8], b0[8], a1[8], b1[8];
-  read(0, a0, b0);
-  // sub-tile s+1 must be visible before its fragments are read: own DMA of s+1 retired (s+2, s+3
-  // may fly), then the barrier, which also certifies every wave finished reading slot (s+3)&3.
-  // (ns is even: K % 64 == 0.)  Reads past the last sub-tile hit a stale slot and are never used.
-  for (int s = 0; s < ns; s += 2) {
-    if (s + 2 < ns) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (s + 3 < ns) issue(s + 3);
-    read(s + 1, a1, b1);
-    for (int i = 0; i < 8; ++i)
-      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], b0[j], acc[i][j], 0, 0, 0);
-    if (s + 3 < ns) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (s + 4 < ns) issue(s + 4);
-    read(s + 2, a0, b0);
-    for (int i = 0; i < 8; ++i)
-      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  // epilogue: per wave 16x128 fp32 strips through LDS, 32 columns per lane
-  float* strip = (float*)(smem + wave * (16 * 132 * 4));
-  const int er = lane >> 2, ec = (lane & 3) * 32;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) strip[((lane >> 4) * 4 + r) * 132 + j * 16 + (lane & 15)] = acc[i][j][r];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    const int grow = m0 + wm * 128 + i * 16 + er;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      float v[16];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 t = *(const f32x4*)(strip + er * 132 + ec + h * 16 + q * 4);
-        v[4 * q] = t[0]; v[4 * q + 1] = t[1]; v[4 * q + 2] = t[2]; v[4 * q + 3] = t[3];
-      }
-      const int gcol = n0 + wn * 128 + ec + h * 16;
-      if (grow < g.M && gcol < g.N) epi_row<EPI, 16>(g, v, bz, grow, gcol);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// v1 kernel (2-phase, kept for A/B measurements: SA_GEMM_V1=1)
-
-template <int EPI>
-__global__ __launch_bounds__(512) void gemm_nt_kernel(GemmArgs g) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
-  const int wg = xcd_remap(blockIdx.x, nm * nn);
-  int mt, nt;
-  tile_coords(wg, nm, nn, g.group_m, mt, nt);
-  const int m0 = mt * BM, n0 = nt * BN;
-  const long bz = blockIdx.z;
-  const bf16* A = g.A + bz * g.sA;
-  const bf16* W = g.W + bz * g.sW;
-  long aoff[4], woff[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = (wave * 4 + i) * 8 + (lane >> 3);
-    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-    const int ar = min(m0 + row, g.M - 1), wr = min(n0 + row, g.N - 1);
-    aoff[i] = (long)ar * g.lda + chunk * 8;
-    woff[i] = (long)wr * g.ldw + chunk * 8;
-  }
-  auto stage = [&](int kt, int buf) {
-    char* base = smem + buf * STAGE_BYTES;
-    const long k0 = (long)kt * BK;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      __builtin_amdgcn_global_load_lds((const void*)(A + aoff[i] + k0), LDS_PTR(base + (wave * 4 + i) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(W + woff[i] + k0), LDS_PTR(base + BM * BK * 2 + (wave * 4 + i) * 1024), 16, 0, 0);
-    }
-  };
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int m = 0; m < 8; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const int nk = g.K / BK;
-  stage(0, 0);
-  for (int kt = 0; kt < nk; ++kt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kt + 1 < nk) stage(kt + 1, (kt + 1) & 1);
-    const char* As = smem + (kt & 1) * STAGE_BYTES;
-    const char* Bs = As + BM * BK * 2;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 a[8], b[4];
-      const int c = kk * 4 + (lane >> 4);
-#pragma unroll
-      for (int m = 0; m < 8; ++m) a[m] = *(const bf16x8*)(As + swz128(wm * 128 + m * 16 + (lane & 15), c));
-#pragma unroll
-      for (int n = 0; n < 4; ++n) b[n] = *(const bf16x8*)(Bs + swz128(wn * 64 + n * 16 + (lane & 15), c));
-#pragma unroll
-      for (int m = 0; m < 8; ++m)
-#pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], b[n], acc[m][n], 0, 0, 0);
-    }
-  }
-  __syncthreads();
-  float* strip = (float*)(smem + wave * (16 * 68 * 4));
-  const int er = lane >> 2, ec = (lane & 3) * 16;
-#pragma unroll
-  for (int m = 0; m < 8; ++m) {
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) strip[((lane >> 4) * 4 + i) * 68 + n * 16 + (lane & 15)] = acc[m][n][i];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    float v[16];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      f32x4 t = *(const f32x4*)(strip + er * 68 + ec + j * 4);
-      v[j * 4 + 0] = t[0]; v[j * 4 + 1] = t[1]; v[j * 4 + 2] = t[2]; v[j * 4 + 3] = t[3];
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    const int grow = m0 + wm * 128 + m * 16 + er;
-    const int gcol = n0 + wn * 64 + ec;
-    if (grow < g.M && gcol < g.N) epi_row<EPI, 16>(g, v, bz, grow, gcol);
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// s4 kernel: one wave per SIMD (4 waves, 2x2, 128x128 per wave, 256 accumulators in AGPRs), the
-// structure hipBLASLt's MT256x256x64 kernel has on gfx950 (rocprof: 256 threads, 130 KB LDS), with
-// our own schedule.  K is staged in 32-deep sub-tiles (A 256x32 + B 256x32 = 32 KB) through a 4-slot
-// LDS ring by buffer_load ... lds (per-lane voffset fixed, the K step in soffset: no address VALU).
-// Step s: vmcnt(8) (sub-tile s+1 landed; s+2 still flying) + one barrier, then the 64 MFMAs of
-// sub-tile s from registers, with the 16 ds_read_b128 of sub-tile s+1's fragments placed two per
-// four MFMAs in the first half and the 8 DMA pieces of sub-tile s+3 (into the slot of s-1) one per
-// four MFMAs in the second half.  Past the end of K the DMA re-reads the last sub-tile and the
-// fragment reads hit a dead slot, so every step issues the same 8 pieces and vmcnt(8) is exact.
-// MFMAs and LDS reads are inline asm (cdna_hip_programming.md §5.7): hipcc keeps them in program
-// order, the accumulators stay in AGPRs ("+a"), and the fragment waits are explicit.  Operands are
-// swapped in the MFMA (C^T = W·A^T) so each lane holds 4 consecutive output columns of one row.
-constexpr int S4_SLOT = 2 * 256 * 64;  // A + B sub-tile, 64-B rows (32 KB)
-constexpr int S4_LDS = 4 * S4_SLOT;    // 128 KB
-
+// persistent one-wave-per-SIMD kernel (4 waves, 2x2, 128x128 per wave, 256 accumulators in AGPRs; the
+// structure hipBLASLt's MT256x256x64 kernel has on gfx950, with our own schedule).  MFMAs and LDS
+// reads are inline asm (cdna_hip_programming.md §5.7): hipcc keeps them in program order, the
+// accumulators stay in AGPRs ("+a") and the fragment waits are explicit.  Operands are swapped in the
+// MFMA (C^T = W·A^T) so each lane holds 4 consecutive output columns of one row.
 template <int OFF>
 __device__ __forceinline__ void s4_ds(u32x4& d, uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF));
@@ -791,219 +408,11 @@ __device__ __forceinline__ void s4_wait_frags(u32x4 (&a)[8], u32x4 (&b)[8]) {
   asm volatile("" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]), "+v"(b[6]), "+v"(b[7]));
 }
 
-struct S4Ctx {
-  __amdgpu_buffer_rsrc_t ra, rw;
-  int aoff[4], woff[4];
-  uint32_t lds_dma;           // wave-uniform LDS byte address of this wave's piece 0 in slot 0
-  uint32_t ard[2], wrd[2];    // per-lane fragment read bases (slots 0-1, slots 2-3)
-};
-
-// DMA of sub-tile s (clamped to the last one) into slot SLOT; PIECE selects one of the 8 pieces
-template <int SLOT, int PIECE>
-__device__ __forceinline__ void s4_dma(const S4Ctx& c, int ks) {
-  constexpr int i = PIECE & 3;
-  if constexpr (PIECE < 4)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(c.ra, LDS_PTR((uintptr_t)(c.lds_dma + SLOT * S4_SLOT + i * 4096)), 16,
-                                             c.aoff[i], ks, 0, 0);
-  else
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rw, LDS_PTR((uintptr_t)(c.lds_dma + SLOT * S4_SLOT + 256 * 64 + i * 4096)),
-                                             16, c.woff[i], ks, 0, 0);
-}
-
-// fragment read R (0..15: A frags 0-7, then W frags 0-7) of slot SLOT
-template <int SLOT, int R>
-__device__ __forceinline__ void s4_read(const S4Ctx& c, u32x4 (&a)[8], u32x4 (&b)[8]) {
-  constexpr int off = (SLOT & 1) * S4_SLOT + (R & 7) * 1024;
-  if constexpr (R < 8)
-    s4_ds<off>(a[R], c.ard[SLOT >> 1]);
-  else
-    s4_ds<off>(b[R & 7], c.wrd[SLOT >> 1]);
-}
-
-template <int SLOT, int Q, int ABL>
-__device__ __forceinline__ void s4_quarter(const S4Ctx& c, f32x4 (&acc)[8][8], u32x4 (&ac)[8], u32x4 (&bc)[8],
-                                           u32x4 (&an)[8], u32x4 (&bn)[8], int ks3) {
-  // Q = 0..7: MFMA row i = Q; reads of the next fragments in Q 0-3, DMA pieces in Q 4-7
-#pragma unroll
-  for (int j = 0; j < 4; ++j) s4_mma(acc[Q][j], bc[j], ac[Q]);
-  if constexpr (Q < 4) {
-    if constexpr (!(ABL & 2)) {
-      s4_read<(SLOT + 1) & 3, 4 * Q + 0>(c, an, bn);
-      s4_read<(SLOT + 1) & 3, 4 * Q + 1>(c, an, bn);
-    }
-  } else {
-    if constexpr (!(ABL & 1)) s4_dma<(SLOT + 3) & 3, 2 * (Q - 4)>(c, ks3);
-  }
-#pragma unroll
-  for (int j = 4; j < 8; ++j) s4_mma(acc[Q][j], bc[j], ac[Q]);
-  if constexpr (Q < 4) {
-    if constexpr (!(ABL & 2)) {
-      s4_read<(SLOT + 1) & 3, 4 * Q + 2>(c, an, bn);
-      s4_read<(SLOT + 1) & 3, 4 * Q + 3>(c, an, bn);
-    }
-  } else {
-    if constexpr (!(ABL & 1)) s4_dma<(SLOT + 3) & 3, 2 * (Q - 4) + 1>(c, ks3);
-  }
-}
-
-template <int SLOT, int ABL>
-__device__ __forceinline__ void s4_step(const S4Ctx& c, f32x4 (&acc)[8][8], u32x4 (&ac)[8], u32x4 (&bc)[8],
-                                        u32x4 (&an)[8], u32x4 (&bn)[8], int s, int ns) {
-  if constexpr (ABL & 1)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  s4_wait_frags(ac, bc);
-  const int ks3 = min(s + 3, ns - 1) * 64;
-  s4_quarter<SLOT, 0, ABL>(c, acc, ac, bc, an, bn, ks3);
-  s4_quarter<SLOT, 1, ABL>(c, acc, ac, bc, an, bn, ks3);
-  s4_quarter<SLOT, 2, ABL>(c, acc, ac, bc, an, bn, ks3);
-  s4_quarter<SLOT, 3, ABL>(c, acc, ac, bc, an, bn, ks3);
-  s4_quarter<SLOT, 4, ABL>(c, acc, ac, bc, an, bn, ks3);
-  s4_quarter<SLOT, 5, ABL>(c, acc, ac, bc, an, bn, ks3);
-  s4_quarter<SLOT, 6, ABL>(c, acc, ac, bc, an, bn, ks3);
-  s4_quarter<SLOT, 7, ABL>(c, acc, ac, bc, an, bn, ks3);
-}
-
-// ABL (measurement builds only): 1 = no DMA in the loop, 2 = no fragment reads in the loop (results
-// are wrong; the schedule's cost anatomy is what is measured)
-template <int EPI, int ABL = 0>
-__global__ __launch_bounds__(256, 1) void gemm_s4_kernel(GemmArgs g) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
-  const int wg = xcd_remap(blockIdx.x, nm * nn);
-  int mt, nt;
-  tile_coords(wg, nm, nn, g.group_m, mt, nt);
-  const int m0 = mt * BM, n0 = nt * BN;
-  const long bz = blockIdx.z;
-  S4Ctx c;
-  c.ra = __builtin_amdgcn_make_buffer_rsrc((void*)(g.A + bz * g.sA + (long)m0 * g.lda), (short)0, 0x7fffffff, 0x00020000);
-  c.rw = __builtin_amdgcn_make_buffer_rsrc((void*)(g.W + bz * g.sW + (long)n0 * g.ldw), (short)0, 0x7fffffff, 0x00020000);
-  // DMA piece i (0..3) of each operand: rows (i*4+wave)*16 + lane/4, 16-B chunk lane%4 (source-swizzled)
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = (i * 4 + wave) * 16 + (lane >> 2);
-    const int chunk = (lane & 3) ^ ((row >> 1) & 3);
-    c.aoff[i] = (min(m0 + row, g.M - 1) - m0) * (int)g.lda * 2 + chunk * 16;
-    c.woff[i] = (min(n0 + row, g.N - 1) - n0) * (int)g.ldw * 2 + chunk * 16;
-  }
-  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
-  c.lds_dma = __builtin_amdgcn_readfirstlane(lds0 + wave * 1024);
-  // fragment reads: row r = w*128 + i*16 + lane%16, chunk lane/16 -> the swizzle term is independent of i
-  const int fr = lane & 15, fc = lane >> 4;
-  c.ard[0] = lds0 + (wm * 128 + fr) * 64 + ((fc ^ ((fr >> 1) & 3)) << 4);
-  c.wrd[0] = lds0 + 256 * 64 + (wn * 128 + fr) * 64 + ((fc ^ ((fr >> 1) & 3)) << 4);
-  c.ard[1] = c.ard[0] + 2 * S4_SLOT;
-  c.wrd[1] = c.wrd[0] + 2 * S4_SLOT;
-  const int ns = g.K / 32;  // multiple of 4 (launcher: K % 128 == 0); a mid-loop exit makes hipcc spill
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  u32x4 a0[8], b0[8], a1[8], b1[8];
-#define SA_S4_DMA_ALL(SLOT, S)                                                                   \
-  {                                                                                              \
-    const int ks = min((S), ns - 1) * 64;                                                        \
-    s4_dma<SLOT, 0>(c, ks); s4_dma<SLOT, 1>(c, ks); s4_dma<SLOT, 2>(c, ks); s4_dma<SLOT, 3>(c, ks); \
-    s4_dma<SLOT, 4>(c, ks); s4_dma<SLOT, 5>(c, ks); s4_dma<SLOT, 6>(c, ks); s4_dma<SLOT, 7>(c, ks); \
-  }
-  SA_S4_DMA_ALL(0, 0)
-  SA_S4_DMA_ALL(1, 1)
-  SA_S4_DMA_ALL(2, 2)
-#undef SA_S4_DMA_ALL
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  s4_read<0, 0>(c, a0, b0); s4_read<0, 1>(c, a0, b0); s4_read<0, 2>(c, a0, b0); s4_read<0, 3>(c, a0, b0);
-  s4_read<0, 4>(c, a0, b0); s4_read<0, 5>(c, a0, b0); s4_read<0, 6>(c, a0, b0); s4_read<0, 7>(c, a0, b0);
-  s4_read<0, 8>(c, a0, b0); s4_read<0, 9>(c, a0, b0); s4_read<0, 10>(c, a0, b0); s4_read<0, 11>(c, a0, b0);
-  s4_read<0, 12>(c, a0, b0); s4_read<0, 13>(c, a0, b0); s4_read<0, 14>(c, a0, b0); s4_read<0, 15>(c, a0, b0);
-
-  for (int s = 0; s < ns; s += 4) {
-    s4_step<0, ABL>(c, acc, a0, b0, a1, b1, s, ns);
-    s4_step<1, ABL>(c, acc, a1, b1, a0, b0, s + 1, ns);
-    s4_step<2, ABL>(c, acc, a0, b0, a1, b1, s + 2, ns);
-    s4_step<3, ABL>(c, acc, a1, b1, a0, b0, s + 3, ns);
-  }
-  // drain: DMA, the (dead) last fragment reads, and the MFMA -> v_accvgpr_read hazard
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-
-  // epilogue: per 16-row block a [16][128] fp32 strip per wave (b128 writes of the 4-column lane
-  // vectors), read back 16 consecutive columns per lane for the fused epilogue and 16-B stores
-  float* strip = (float*)(smem + wave * (16 * 132 * 4));
-  const int er = lane >> 2, ec = (lane & 3) * 32;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) *(f32x4*)(strip + fr * 132 + j * 16 + fc * 4) = acc[i][j];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    const int grow = m0 + wm * 128 + i * 16 + er;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      float v[16];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 t = *(const f32x4*)(strip + er * 132 + ec + h * 16 + q * 4);
-        v[4 * q] = t[0]; v[4 * q + 1] = t[1]; v[4 * q + 2] = t[2]; v[4 * q + 3] = t[3];
-      }
-      const int gcol = n0 + wn * 128 + ec + h * 16;
-      if (grow < g.M && gcol < g.N) epi_row<EPI, 16>(g, v, bz, grow, gcol);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
-// epilogue shared by the one-wave-per-SIMD kernels: per 16-row block a [16][128] fp32 strip per wave
-// (b128 writes of the operand-swapped 4-column lane vectors), read back 16 consecutive columns per
-// lane for the fused epilogue and 16-B stores.  LDS must be free (caller drains DMA + barrier).
-template <int EPI>
-__device__ __forceinline__ void s4_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8], char* smem, int wave, int lane,
-                                            int m0, int n0, long bz) {
-  const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fc = lane >> 4;
-  float* strip = (float*)(smem + wave * (16 * 132 * 4));
-  const int er = lane >> 2, ec = (lane & 3) * 32;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) *(f32x4*)(strip + fr * 132 + j * 16 + fc * 4) = acc[i][j];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    const int grow = m0 + wm * 128 + i * 16 + er;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      float v[16];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 t = *(const f32x4*)(strip + er * 132 + ec + h * 16 + q * 4);
-        v[4 * q] = t[0]; v[4 * q + 1] = t[1]; v[4 * q + 2] = t[2]; v[4 * q + 3] = t[3];
-      }
-      const int gcol = n0 + wn * 128 + ec + h * 16;
-      if (grow < g.M && gcol < g.N) epi_row<EPI, 16>(g, v, bz, grow, gcol);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// s5 kernel: s4's one-wave-per-SIMD 128x128 wave tiles, but K-tiles of 64 (128-B rows, so every
-// 1-KB DMA piece is 8 whole cache lines; the 64-B rows of s4 halve the line per request and the
-// DMA issue then throttles the wave) in a 2-stage ring (64 KB per stage: A 256 rows, W 256 rows).
-// Step t (stage t&1), fragments of (t, k 0-31) already in registers:
-//   half 0: 64 MFMAs, with the 16 reads of (t, k 32-63) in its first 32
-//   mid:    vmcnt(0) (tile t+1 landed) + lgkmcnt(0) + one barrier: t+1 visible, stage t&1 free
-//   half 1: 64 MFMAs, with the 16 reads of (t+1, k 0-31) and the 16 DMA pieces of tile t+2 (into
-//           stage t&1) in its first 32
-// so a DMA piece has from half 1 of step t to the middle of step t+1 to land.
+// K-tiles of 64 (128-B rows, so every 1-KB DMA piece is 8 whole cache lines) in a 2-stage LDS ring
+// (64 KB per stage: A 256 rows, W 256 rows).  Step t (stage t&1), fragments of (t, k 0-31) already in
+// registers: half 0 = 64 MFMAs with the 16 reads of (t, k 32-63) in its first 32; vmcnt(0) + one
+// barrier; half 1 = 64 MFMAs with the 16 reads of (t+1, k 0-31) and the 16 DMA pieces of tile t+2
+// (into stage t&1) spread over all 8 MFMA rows.
 constexpr int S5_STAGE = 2 * 256 * 128;  // 64 KB
 constexpr int S5_LDS = 2 * S5_STAGE;     // 128 KB
 
@@ -1069,246 +478,10 @@ __device__ __forceinline__ void s5_half(const S5Ctx& c, f32x4 (&acc)[8][8], u32x
 #undef SA_S5_ROW
 }
 
-template <int S, bool SPREAD>
-__device__ __forceinline__ void s5_step(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8], u32x4 (&b0)[8],
-                                        u32x4 (&a1)[8], u32x4 (&b1)[8], int t, int nk) {
-  s4_wait_frags(a0, b0);
-  s5_half<S, 1, false, 0>(c, acc, a0, b0, a1, b1, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  s4_wait_frags(a1, b1);
-  __builtin_amdgcn_s_barrier();
-  s5_half<S ^ 1, 0, true, S, SPREAD>(c, acc, a1, b1, a0, b0, min(t + 2, nk - 1) * 128);
-}
-
-template <int EPI, bool SPREAD = false>
-__global__ __launch_bounds__(256, 1) void gemm_s5_kernel(GemmArgs g) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
-  const int wg = xcd_remap(blockIdx.x, nm * nn);
-  int mt, nt;
-  tile_coords(wg, nm, nn, g.group_m, mt, nt);
-  const int m0 = mt * BM, n0 = nt * BN;
-  const long bz = blockIdx.z;
-  S5Ctx c;
-  c.ra = __builtin_amdgcn_make_buffer_rsrc((void*)(g.A + bz * g.sA + (long)m0 * g.lda), (short)0, 0x7fffffff, 0x00020000);
-  c.rw = __builtin_amdgcn_make_buffer_rsrc((void*)(g.W + bz * g.sW + (long)n0 * g.ldw), (short)0, 0x7fffffff, 0x00020000);
-  // DMA piece i (0..7) of each operand: rows (i*4+wave)*8 + lane/8, 16-B chunk lane%8 (source-swizzled)
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int row = (i * 4 + wave) * 8 + (lane >> 3);
-    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-    c.aoff[i] = (min(m0 + row, g.M - 1) - m0) * (int)g.lda * 2 + chunk * 16;
-    c.woff[i] = (min(n0 + row, g.N - 1) - n0) * (int)g.ldw * 2 + chunk * 16;
-  }
-  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
-  c.lds_dma = __builtin_amdgcn_readfirstlane(lds0 + wave * 1024);
-  // fragment (row r = w*128 + i*16 + lane%16, chunk 4*kh + lane/16): the swizzle term is independent of i
-  const int fr = lane & 15, fc = lane >> 4;
-#pragma unroll
-  for (int st = 0; st < 2; ++st)
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      const int sw = ((4 * kh + fc) ^ ((fr >> 1) & 7)) << 4;
-      c.ard[st][kh] = lds0 + st * S5_STAGE + (wm * 128 + fr) * 128 + sw;
-      c.wrd[st][kh] = lds0 + st * S5_STAGE + 256 * 128 + (wn * 128 + fr) * 128 + sw;
-    }
-  const int nk = g.K / 64;  // even (launcher: K % 128 == 0); a mid-loop exit makes hipcc spill
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  u32x4 a0[8], b0[8], a1[8], b1[8];
-#define SA_S5_DMA_ALL(STAGE, T)                                                                       \
-  {                                                                                                   \
-    const int ks = (T) * 128;                                                                         \
-    s5_dma<STAGE, 0>(c, ks); s5_dma<STAGE, 1>(c, ks); s5_dma<STAGE, 2>(c, ks); s5_dma<STAGE, 3>(c, ks);     \
-    s5_dma<STAGE, 4>(c, ks); s5_dma<STAGE, 5>(c, ks); s5_dma<STAGE, 6>(c, ks); s5_dma<STAGE, 7>(c, ks);     \
-    s5_dma<STAGE, 8>(c, ks); s5_dma<STAGE, 9>(c, ks); s5_dma<STAGE, 10>(c, ks); s5_dma<STAGE, 11>(c, ks);   \
-    s5_dma<STAGE, 12>(c, ks); s5_dma<STAGE, 13>(c, ks); s5_dma<STAGE, 14>(c, ks); s5_dma<STAGE, 15>(c, ks); \
-  }
-  SA_S5_DMA_ALL(0, 0)
-  SA_S5_DMA_ALL(1, 1)
-#undef SA_S5_DMA_ALL
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  s5_read<0, 0, 0>(c, a0, b0); s5_read<0, 0, 1>(c, a0, b0); s5_read<0, 0, 2>(c, a0, b0); s5_read<0, 0, 3>(c, a0, b0);
-  s5_read<0, 0, 4>(c, a0, b0); s5_read<0, 0, 5>(c, a0, b0); s5_read<0, 0, 6>(c, a0, b0); s5_read<0, 0, 7>(c, a0, b0);
-  s5_read<0, 0, 8>(c, a0, b0); s5_read<0, 0, 9>(c, a0, b0); s5_read<0, 0, 10>(c, a0, b0); s5_read<0, 0, 11>(c, a0, b0);
-  s5_read<0, 0, 12>(c, a0, b0); s5_read<0, 0, 13>(c, a0, b0); s5_read<0, 0, 14>(c, a0, b0); s5_read<0, 0, 15>(c, a0, b0);
-
-  for (int t = 0; t < nk; t += 2) {
-    s5_step<0, SPREAD>(c, acc, a0, b0, a1, b1, t, nk);
-    s5_step<1, SPREAD>(c, acc, a0, b0, a1, b1, t + 1, nk);
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  s4_epilogue<EPI>(g, acc, smem, wave, lane, m0, n0, bz);
-}
-
-// ------------------------------------------------------------------------------------------------
-// s6 kernel: s5 with register staging instead of LDS-DMA (measured: the LDS-DMA path caps the
-// one-wave-per-SIMD loop well below the MFMA rate, s5 972 TF vs 1709 TF with the DMA removed, at
-// 8192^3).  Tile t+2 is fetched by 16 buffer_load_dwordx4 per wave into 64 staging VGPRs in the
-// first half of step t and written (ds_write_b128, same swizzled image as the DMA) into stage t&1
-// in the second half, after the mid barrier has freed it; hipcc counts these loads itself.
-template <int STAGE, int P>
-__device__ __forceinline__ void s6_load(const S5Ctx& c, u32x4 (&stg)[16], int ks) {
-  constexpr int i = P & 7;
-  if constexpr (P < 8)
-    stg[P] = __builtin_amdgcn_raw_buffer_load_b128(c.ra, c.aoff[i], ks, 0);
-  else
-    stg[P] = __builtin_amdgcn_raw_buffer_load_b128(c.rw, c.woff[i], ks, 0);
-}
-template <int STAGE, int P>
-__device__ __forceinline__ void s6_store(char* lds_lane, const u32x4 (&stg)[16]) {
-  // lds_lane = smem + wave*1024 + lane*16; piece P of operand (P>>3) at +(P&7)*4096
-  constexpr int off = STAGE * S5_STAGE + (P >> 3) * 256 * 128 + (P & 7) * 4096;
-  *(u32x4*)(lds_lane + off) = stg[P];
-}
-
-template <int RS, int RK, int MODE, int DS, int ABL = 0>
-__device__ __forceinline__ void s6_half(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&ac)[8], u32x4 (&bc)[8],
-                                        u32x4 (&an)[8], u32x4 (&bn)[8], u32x4 (&stg)[16], char* lds_lane, int ks) {
-  // MODE 0: reads of the next fragments in rows 0-3, global loads (tile ks) in rows 4-7
-  // MODE 1: reads in rows 0-3, staged ds_writes into stage DS in rows 4-7
-#define SA_S6_ROW(Q)                                                                          \
-  {                                                                                           \
-    s4_mma(acc[Q][0], bc[0], ac[Q]); s4_mma(acc[Q][1], bc[1], ac[Q]);                         \
-    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q>(c, an, bn); }                               \
-    else if constexpr (MODE == 0) { if constexpr (!(ABL & 1)) s6_load<DS, 4 * (Q - 4)>(c, stg, ks); }                   \
-    else { if constexpr (!(ABL & 2)) s6_store<DS, 4 * (Q - 4)>(lds_lane, stg); else asm volatile("" :: "v"(stg[4 * (Q - 4)])); }                                        \
-    s4_mma(acc[Q][2], bc[2], ac[Q]); s4_mma(acc[Q][3], bc[3], ac[Q]);                         \
-    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 1>(c, an, bn); }                           \
-    else if constexpr (MODE == 0) { if constexpr (!(ABL & 1)) s6_load<DS, 4 * (Q - 4) + 1>(c, stg, ks); }               \
-    else { if constexpr (!(ABL & 2)) s6_store<DS, 4 * (Q - 4) + 1>(lds_lane, stg); else asm volatile("" :: "v"(stg[4 * (Q - 4) + 1])); }                                    \
-    s4_mma(acc[Q][4], bc[4], ac[Q]); s4_mma(acc[Q][5], bc[5], ac[Q]);                         \
-    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 2>(c, an, bn); }                           \
-    else if constexpr (MODE == 0) { if constexpr (!(ABL & 1)) s6_load<DS, 4 * (Q - 4) + 2>(c, stg, ks); }               \
-    else { if constexpr (!(ABL & 2)) s6_store<DS, 4 * (Q - 4) + 2>(lds_lane, stg); else asm volatile("" :: "v"(stg[4 * (Q - 4) + 2])); }                                    \
-    s4_mma(acc[Q][6], bc[6], ac[Q]); s4_mma(acc[Q][7], bc[7], ac[Q]);                         \
-    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 3>(c, an, bn); }                           \
-    else if constexpr (MODE == 0) { if constexpr (!(ABL & 1)) s6_load<DS, 4 * (Q - 4) + 3>(c, stg, ks); }               \
-    else { if constexpr (!(ABL & 2)) s6_store<DS, 4 * (Q - 4) + 3>(lds_lane, stg); else asm volatile("" :: "v"(stg[4 * (Q - 4) + 3])); }                                    \
-  }
-  SA_S6_ROW(0) SA_S6_ROW(1) SA_S6_ROW(2) SA_S6_ROW(3) SA_S6_ROW(4) SA_S6_ROW(5) SA_S6_ROW(6) SA_S6_ROW(7)
-#undef SA_S6_ROW
-}
-
-template <int S, int ABL = 0>
-__device__ __forceinline__ void s6_step(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8], u32x4 (&b0)[8],
-                                        u32x4 (&a1)[8], u32x4 (&b1)[8], u32x4 (&stg)[16], char* lds_lane, int t,
-                                        int nk) {
-  s4_wait_frags(a0, b0);
-  s6_half<S, 1, 0, S, ABL>(c, acc, a0, b0, a1, b1, stg, lds_lane, min(t + 2, nk - 1) * 128);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of stage S and its ds_writes
-  s4_wait_frags(a1, b1);
-  __builtin_amdgcn_s_barrier();
-  s6_half<S ^ 1, 0, 1, S, ABL>(c, acc, a1, b1, a0, b0, stg, lds_lane, 0);
-}
-
-// ABL (measurement builds only): 1 = no staged global loads, 2 = no staged ds_writes
-template <int EPI, int ABL = 0>
-__global__ __launch_bounds__(256, 1) void gemm_s6_kernel(GemmArgs g) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
-  const int wg = xcd_remap(blockIdx.x, nm * nn);
-  int mt, nt;
-  tile_coords(wg, nm, nn, g.group_m, mt, nt);
-  const int m0 = mt * BM, n0 = nt * BN;
-  const long bz = blockIdx.z;
-  S5Ctx c;
-  c.ra = __builtin_amdgcn_make_buffer_rsrc((void*)(g.A + bz * g.sA + (long)m0 * g.lda), (short)0, 0x7fffffff, 0x00020000);
-  c.rw = __builtin_amdgcn_make_buffer_rsrc((void*)(g.W + bz * g.sW + (long)n0 * g.ldw), (short)0, 0x7fffffff, 0x00020000);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int row = (i * 4 + wave) * 8 + (lane >> 3);
-    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-    c.aoff[i] = (min(m0 + row, g.M - 1) - m0) * (int)g.lda * 2 + chunk * 16;
-    c.woff[i] = (min(n0 + row, g.N - 1) - n0) * (int)g.ldw * 2 + chunk * 16;
-  }
-  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
-  char* lds_lane = smem + wave * 1024 + lane * 16;
-  const int fr = lane & 15, fc = lane >> 4;
-#pragma unroll
-  for (int st = 0; st < 2; ++st)
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      const int sw = ((4 * kh + fc) ^ ((fr >> 1) & 7)) << 4;
-      c.ard[st][kh] = lds0 + st * S5_STAGE + (wm * 128 + fr) * 128 + sw;
-      c.wrd[st][kh] = lds0 + st * S5_STAGE + 256 * 128 + (wn * 128 + fr) * 128 + sw;
-    }
-  const int nk = g.K / 64;  // even (launcher: K % 128 == 0)
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  u32x4 a0[8], b0[8], a1[8], b1[8], stg[16];
-#define SA_S6_FILL(STAGE, T)                                                                              \
-  {                                                                                                       \
-    const int ks = (T) * 128;                                                                             \
-    s6_load<STAGE, 0>(c, stg, ks); s6_load<STAGE, 1>(c, stg, ks); s6_load<STAGE, 2>(c, stg, ks);          \
-    s6_load<STAGE, 3>(c, stg, ks); s6_load<STAGE, 4>(c, stg, ks); s6_load<STAGE, 5>(c, stg, ks);          \
-    s6_load<STAGE, 6>(c, stg, ks); s6_load<STAGE, 7>(c, stg, ks); s6_load<STAGE, 8>(c, stg, ks);          \
-    s6_load<STAGE, 9>(c, stg, ks); s6_load<STAGE, 10>(c, stg, ks); s6_load<STAGE, 11>(c, stg, ks);        \
-    s6_load<STAGE, 12>(c, stg, ks); s6_load<STAGE, 13>(c, stg, ks); s6_load<STAGE, 14>(c, stg, ks);       \
-    s6_load<STAGE, 15>(c, stg, ks);                                                                       \
-    s6_store<STAGE, 0>(lds_lane, stg); s6_store<STAGE, 1>(lds_lane, stg); s6_store<STAGE, 2>(lds_lane, stg);     \
-    s6_store<STAGE, 3>(lds_lane, stg); s6_store<STAGE, 4>(lds_lane, stg); s6_store<STAGE, 5>(lds_lane, stg);     \
-    s6_store<STAGE, 6>(lds_lane, stg); s6_store<STAGE, 7>(lds_lane, stg); s6_store<STAGE, 8>(lds_lane, stg);     \
-    s6_store<STAGE, 9>(lds_lane, stg); s6_store<STAGE, 10>(lds_lane, stg); s6_store<STAGE, 11>(lds_lane, stg);   \
-    s6_store<STAGE, 12>(lds_lane, stg); s6_store<STAGE, 13>(lds_lane, stg); s6_store<STAGE, 14>(lds_lane, stg);  \
-    s6_store<STAGE, 15>(lds_lane, stg);                                                                   \
-  }
-  SA_S6_FILL(0, 0)
-  SA_S6_FILL(1, 1)
-#undef SA_S6_FILL
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  s5_read<0, 0, 0>(c, a0, b0); s5_read<0, 0, 1>(c, a0, b0); s5_read<0, 0, 2>(c, a0, b0); s5_read<0, 0, 3>(c, a0, b0);
-  s5_read<0, 0, 4>(c, a0, b0); s5_read<0, 0, 5>(c, a0, b0); s5_read<0, 0, 6>(c, a0, b0); s5_read<0, 0, 7>(c, a0, b0);
-  s5_read<0, 0, 8>(c, a0, b0); s5_read<0, 0, 9>(c, a0, b0); s5_read<0, 0, 10>(c, a0, b0); s5_read<0, 0, 11>(c, a0, b0);
-  s5_read<0, 0, 12>(c, a0, b0); s5_read<0, 0, 13>(c, a0, b0); s5_read<0, 0, 14>(c, a0, b0); s5_read<0, 0, 15>(c, a0, b0);
-
-  for (int t = 0; t < nk; t += 2) {
-    s6_step<0, ABL>(c, acc, a0, b0, a1, b1, stg, lds_lane, t, nk);
-    s6_step<1, ABL>(c, acc, a0, b0, a1, b1, stg, lds_lane, t + 1, nk);
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  s4_epilogue<EPI>(g, acc, smem, wave, lane, m0, n0, bz);
-}
-
-// ------------------------------------------------------------------------------------------------
-// s7 kernel: s6 made persistent.  One workgroup per CU walks output tiles u = blockIdx.x + k*gridDim.x
-// and the K pipeline runs on across tile seams: in the last two K steps of tile u the staged loads
-// fetch K-tiles 0 and 1 of tile u+gridDim.x, and the last step's fragment reads take that tile's
-// first fragments, so the next tile starts with its operands already in LDS and registers (no
-// prologue) while the epilogue of tile u runs from a private LDS strip (the 4 x 4.3 KB above the
-// 128-KB ring).  Rows past M / N read as zeros from the buffer range check (num_records), so the
-// per-lane load offsets are the same for every tile.
-template <int S>
-__device__ __forceinline__ void s7_step(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8], u32x4 (&b0)[8],
-                                        u32x4 (&a1)[8], u32x4 (&b1)[8], u32x4 (&stg)[16], char* lds_lane, int ks) {
-  s4_wait_frags(a0, b0);
-  s6_half<S, 1, 0, S>(c, acc, a0, b0, a1, b1, stg, lds_lane, ks);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  s4_wait_frags(a1, b1);
-  __builtin_amdgcn_s_barrier();
-  s6_half<S ^ 1, 0, 1, S>(c, acc, a1, b1, a0, b0, stg, lds_lane, 0);
-}
-
+// persistence: one workgroup per CU walks output tiles u = blockIdx.x + k*gridDim.x and the K
+// pipeline runs on across tile seams; the epilogue of tile u runs from a private LDS strip (the
+// 4 x 4.3 KB above the 128-KB ring).  Rows past M / N read as zeros from the buffer range check
+// (num_records), so the per-lane load offsets are the same for every tile.
 constexpr int S7_STRIP = 16 * 68 * 4;             // [16 rows][64 (+4) cols] fp32 per wave
 constexpr int S7_LDS = S5_LDS + 4 * S7_STRIP;     // 145 KB
 
@@ -1316,7 +489,6 @@ constexpr int S7_LDS = S5_LDS + 4 * S7_STRIP;     // 145 KB
 // half) steps are loaded S7_RES_AHEAD steps ahead (the fragment registers are dead here), bias once per
 // column half, so the residual's HBM latency is paid about once per tile instead of once per step
 constexpr int S7_RES_AHEAD = 2;
-__constant__ int g_res_tile_gate = 1;  // A/B switch (SA_GEMM_TILEGATE=0 in the environment clears it)
 // TILE_GATE: every row of the tile reads the same gate row (no gate, or the tile lies inside one CFG
 // row's token range, e.g. 21 504 = 84 x 256): the gate is loaded once per column half like the bias,
 // and the freed registers deepen the residual prefetch to AHEAD = 3 steps
@@ -1396,7 +568,7 @@ __device__ __forceinline__ void s7_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8
   const int er = lane >> 2, ec = (lane & 3) * 16;
   if constexpr (EPI == EPI_RES_F32) {
     if (m0 + BM <= g.M && n0 + BN <= g.N) {  // wave-uniform
-      if (g_res_tile_gate && (!g.gate || m0 / g.rows_per_batch == (m0 + BM - 1) / g.rows_per_batch))
+      if (!g.gate || m0 / g.rows_per_batch == (m0 + BM - 1) / g.rows_per_batch)
         s7_res_epilogue<3, true>(g, acc, strip, wm, wn, fr, fc, er, ec, m0, n0, bz);
       else
         s7_res_epilogue<S7_RES_AHEAD, false>(g, acc, strip, wm, wn, fr, fc, er, ec, m0, n0, bz);
@@ -1443,110 +615,6 @@ __device__ __forceinline__ void s7_tile(const GemmArgs& g, int u, int total, int
                                          (int)(rows_a * g.lda * 2), 0x00020000);
   rw = __builtin_amdgcn_make_buffer_rsrc((void*)(g.W + bz * g.sW + (long)n0 * g.ldw), (short)0,
                                          (int)(rows_w * g.ldw * 2), 0x00020000);
-}
-
-template <int EPI>
-__global__ __launch_bounds__(256, 1) void gemm_s7_kernel(GemmArgs g, int batch) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
-  const int total = nm * nn * batch, G = gridDim.x;
-  int u = blockIdx.x;
-  S5Ctx c;
-  int m0, n0;
-  long bz;
-  s7_tile(g, u, total, G, nm, nn, m0, n0, bz, c.ra, c.rw);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int row = (i * 4 + wave) * 8 + (lane >> 3);
-    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-    c.aoff[i] = row * (int)g.lda * 2 + chunk * 16;
-    c.woff[i] = row * (int)g.ldw * 2 + chunk * 16;
-  }
-  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
-  char* lds_lane = smem + wave * 1024 + lane * 16;
-  const int fr = lane & 15, fc = lane >> 4;
-#pragma unroll
-  for (int st = 0; st < 2; ++st)
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      const int sw = ((4 * kh + fc) ^ ((fr >> 1) & 7)) << 4;
-      c.ard[st][kh] = lds0 + st * S5_STAGE + (wm * 128 + fr) * 128 + sw;
-      c.wrd[st][kh] = lds0 + st * S5_STAGE + 256 * 128 + (wn * 128 + fr) * 128 + sw;
-    }
-  const int nk = g.K / 64;  // even (launcher: K % 128 == 0)
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  u32x4 a0[8], b0[8], a1[8], b1[8], stg[16];
-#define SA_S7_FILL(STAGE, T)                                                                              \
-  {                                                                                                       \
-    const int ks = (T) * 128;                                                                             \
-    s6_load<STAGE, 0>(c, stg, ks); s6_load<STAGE, 1>(c, stg, ks); s6_load<STAGE, 2>(c, stg, ks);          \
-    s6_load<STAGE, 3>(c, stg, ks); s6_load<STAGE, 4>(c, stg, ks); s6_load<STAGE, 5>(c, stg, ks);          \
-    s6_load<STAGE, 6>(c, stg, ks); s6_load<STAGE, 7>(c, stg, ks); s6_load<STAGE, 8>(c, stg, ks);          \
-    s6_load<STAGE, 9>(c, stg, ks); s6_load<STAGE, 10>(c, stg, ks); s6_load<STAGE, 11>(c, stg, ks);        \
-    s6_load<STAGE, 12>(c, stg, ks); s6_load<STAGE, 13>(c, stg, ks); s6_load<STAGE, 14>(c, stg, ks);       \
-    s6_load<STAGE, 15>(c, stg, ks);                                                                       \
-    s6_store<STAGE, 0>(lds_lane, stg); s6_store<STAGE, 1>(lds_lane, stg); s6_store<STAGE, 2>(lds_lane, stg);     \
-    s6_store<STAGE, 3>(lds_lane, stg); s6_store<STAGE, 4>(lds_lane, stg); s6_store<STAGE, 5>(lds_lane, stg);     \
-    s6_store<STAGE, 6>(lds_lane, stg); s6_store<STAGE, 7>(lds_lane, stg); s6_store<STAGE, 8>(lds_lane, stg);     \
-    s6_store<STAGE, 9>(lds_lane, stg); s6_store<STAGE, 10>(lds_lane, stg); s6_store<STAGE, 11>(lds_lane, stg);   \
-    s6_store<STAGE, 12>(lds_lane, stg); s6_store<STAGE, 13>(lds_lane, stg); s6_store<STAGE, 14>(lds_lane, stg);  \
-    s6_store<STAGE, 15>(lds_lane, stg);                                                                   \
-  }
-  SA_S7_FILL(0, 0)
-  SA_S7_FILL(1, 1)
-#undef SA_S7_FILL
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  s5_read<0, 0, 0>(c, a0, b0); s5_read<0, 0, 1>(c, a0, b0); s5_read<0, 0, 2>(c, a0, b0); s5_read<0, 0, 3>(c, a0, b0);
-  s5_read<0, 0, 4>(c, a0, b0); s5_read<0, 0, 5>(c, a0, b0); s5_read<0, 0, 6>(c, a0, b0); s5_read<0, 0, 7>(c, a0, b0);
-  s5_read<0, 0, 8>(c, a0, b0); s5_read<0, 0, 9>(c, a0, b0); s5_read<0, 0, 10>(c, a0, b0); s5_read<0, 0, 11>(c, a0, b0);
-  s5_read<0, 0, 12>(c, a0, b0); s5_read<0, 0, 13>(c, a0, b0); s5_read<0, 0, 14>(c, a0, b0); s5_read<0, 0, 15>(c, a0, b0);
-
-  while (true) {
-    const int un = u + G;
-    const bool has_next = un < total;
-    __amdgpu_buffer_rsrc_t cra = c.ra, crw = c.rw, nra = c.ra, nrw = c.rw;
-    int nm0 = m0, nn0 = n0;
-    long nbz = bz;
-    if (has_next) s7_tile(g, un, total, G, nm, nn, nm0, nn0, nbz, nra, nrw);
-    for (int t = 0; t < nk; t += 2) {
-      {
-        const bool nx = t + 2 >= nk;  // stage the next tile's K-tile t+2-nk (or re-read the last one)
-        c.ra = nx ? nra : cra;
-        c.rw = nx ? nrw : crw;
-        s7_step<0>(c, acc, a0, b0, a1, b1, stg, lds_lane, (nx ? (has_next ? t + 2 - nk : nk - 1) : t + 2) * 128);
-      }
-      {
-        const bool nx = t + 3 >= nk;
-        c.ra = nx ? nra : cra;
-        c.rw = nx ? nrw : crw;
-        s7_step<1>(c, acc, a0, b0, a1, b1, stg, lds_lane, (nx ? (has_next ? t + 3 - nk : nk - 1) : t + 3) * 128);
-      }
-    }
-    asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // MFMA -> v_accvgpr_read
-    s7_epilogue<EPI>(g, acc, smem, wave, lane, m0, n0, bz);
-    if (!has_next) break;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    u = un;
-    m0 = nm0;
-    n0 = nn0;
-    bz = nbz;
-    c.ra = nra;
-    c.rw = nrw;
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1661,126 +729,55 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 
-int g_num_cus = 0;
+constexpr int KERNEL_AUTO = 0, KERNEL_PINGPONG = 1, KERNEL_PERSISTENT = 2;
 
-int g_gemm_variant = -1;  // 0 = v1 (2-phase), 1 = phased (8 waves), 2 = w4 (4 waves, AGPR accumulators),
-                          // 3 = ping-pong 8-phase, 4 = ping-pong with direct (operand-swapped) epilogue,
-                          // 5 = s4 (one wave per SIMD, buffer-DMA ring, scheduled interleave),
-                          // 6-8 = s4 measurement ablations, 9 = s5 (s4 with 128-B rows, 2-stage ring),
-                          // 10 = s6 (s5 with register-staged loads), 11 = s7 (persistent s6),
-                          // 12-13 = s6 ablations, 14 = s5 with the DMA pieces spread over the half,
-                          // 15 = default: 16 where K % 128 == 0, else 4; 16 = s8 (persistent 14)
+int num_cus() {
+  // per device: the persistent grid is one workgroup per CU
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+// the launch-time tile raster override (SA_GEMM_GROUP_M), read once per process
+int env_group_m() {
+  static const int gm = [] {
+    const char* e = getenv("SA_GEMM_GROUP_M");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 0;
+  }();
+  return gm;
+}
 
 template <int EPI>
-int launch(const GemmArgs& g_in, int batch, hipStream_t st) {
-  static int attr = 0;
-  if (g_gemm_variant < 0) {
-    const char* e = getenv("SA_GEMM_VARIANT");
-    g_gemm_variant = e ? atoi(e) : 15;
-    const char* tg = getenv("SA_GEMM_TILEGATE");
-    if (tg && atoi(tg) == 0) {
-      const int zero = 0;
-      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_res_tile_gate), &zero, sizeof(int));
-    }
-  }
-  GemmArgs g = g_in;
-  // 15 = default (measured, profiles/r01/gemm_ab_r4.md): the persistent one-wave-per-SIMD LDS-DMA
-  // kernel wherever its K % 128 tiling applies (over the ping-pong: QKV +8-15 %, cross-Q +7-10 %,
-  // FFN-up +3-4 %, FFN-down with the prefetched residual epilogue +4 %, O-proj +-1 %), else the
-  // ping-pong kernel (e.g. the K = 192 patch embedding)
-  constexpr bool BF16_OUT = EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16;
-  const int variant = g_gemm_variant != 15 ? g_gemm_variant
-                      : (g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
-                         (long)BN * g.ldw * 2 < 0x7fffffffL) ? 16 : 4;
-  if (g.group_m == 0)
-    g.group_m = variant == 14 ? 4 : variant == 16 ? (BF16_OUT ? 8 : 4) : (g.N >= 4096 ? 8 : 1);
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)gemm_phased_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)gemm_w4_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, W4_LDS);
-    (void)hipFuncSetAttribute((const void*)gemm_s4_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S4_LDS);
-    (void)hipFuncSetAttribute((const void*)gemm_s5_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S5_LDS);
-    (void)hipFuncSetAttribute((const void*)gemm_s5_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              S5_LDS);
-    (void)hipFuncSetAttribute((const void*)gemm_s6_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S5_LDS);
-    (void)hipFuncSetAttribute((const void*)gemm_s7_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S7_LDS);
+int launch(const GemmArgs& g_in, int batch, int kernel, hipStream_t st) {
+  // one-time per epilogue instantiation: allow the dynamic LDS sizes (idempotent, thread-safe init)
+  static const bool attr = [] {
     (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S7_LDS);
-    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
-    attr = 1;
-  }
+    return true;
+  }();
+  (void)attr;
+  GemmArgs g = g_in;
+  // auto (measured, profiles/r01/gemm_ab_r4.md): the persistent one-wave-per-SIMD LDS-DMA kernel
+  // wherever its K % 128 tiling and 32-bit buffer offsets apply (over the ping-pong: QKV +8-15 %,
+  // cross-Q +7-10 %, FFN-up +3-4 %, FFN-down +4 %, O-proj +-1 %), else the ping-pong kernel (e.g. the
+  // K = 192 patch embedding)
+  const bool persistent_ok = g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL && (long)BN * g.ldw * 2 < 0x7fffffffL;
+  if (kernel == KERNEL_PERSISTENT && !persistent_ok) return SA_ERR_ARG;
+  const bool persistent = kernel == KERNEL_PERSISTENT || (kernel == KERNEL_AUTO && persistent_ok);
+  constexpr bool BF16_OUT = EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16;
+  if (g.group_m == 0) g.group_m = persistent ? (BF16_OUT ? 8 : 4) : (g.N >= 4096 ? 8 : 1);
   const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
-  if (variant == 0)
-    hipLaunchKernelGGL(gemm_nt_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
-  else if (variant == 1)
-    hipLaunchKernelGGL(gemm_phased_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
-  else if (variant == 2)
-    hipLaunchKernelGGL(gemm_w4_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(256), W4_LDS, st, g);
-  else if (variant == 3) {
-    // fp32 outputs store straight from the (operand-swapped) accumulators; bf16 outputs go through
-    // the LDS transpose for 16-B row stores
-    constexpr bool F32_OUT = EPI == EPI_RES_F32 || EPI == EPI_F32 || EPI == EPI_SILU_F32;
-    hipLaunchKernelGGL((gemm_pp_kernel<EPI, F32_OUT>), dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
-  } else if (variant == 5 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
-             (long)BN * g.ldw * 2 < 0x7fffffffL)
-    hipLaunchKernelGGL(gemm_s4_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(256), S4_LDS, st, g);
-  else if (variant == 9 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
-           (long)BN * g.ldw * 2 < 0x7fffffffL)
-    hipLaunchKernelGGL(gemm_s5_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(256), S5_LDS, st, g);
-  else if (variant == 16 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
-           (long)BN * g.ldw * 2 < 0x7fffffffL) {
-    if (!g_num_cus) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_num_cus <= 0)
-        g_num_cus = 256;
-    }
-    hipLaunchKernelGGL(gemm_s8_kernel<EPI>, dim3(min(nm * nn * batch, g_num_cus)), dim3(256), S7_LDS, st, g, batch);
-  } else if (variant == 14 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
-           (long)BN * g.ldw * 2 < 0x7fffffffL)
-    hipLaunchKernelGGL((gemm_s5_kernel<EPI, true>), dim3(nm * nn, 1, batch), dim3(256), S5_LDS, st, g);
-  else if (variant == 10 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
-           (long)BN * g.ldw * 2 < 0x7fffffffL)
-    hipLaunchKernelGGL(gemm_s6_kernel<EPI>, dim3(nm * nn, 1, batch), dim3(256), S5_LDS, st, g);
-  else if (variant == 11 && g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL &&
-           (long)BN * g.ldw * 2 < 0x7fffffffL) {
-    if (!g_num_cus) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_num_cus <= 0)
-        g_num_cus = 256;
-    }
-    const int total = nm * nn * batch;
-    hipLaunchKernelGGL(gemm_s7_kernel<EPI>, dim3(min(total, g_num_cus)), dim3(256), S7_LDS, st, g, batch);
-  } else if ((variant == 12 || variant == 13) && EPI == EPI_BF16 && g.K % 128 == 0) {
-    static int attr6 = 0;
-    if (!attr6) {
-      (void)hipFuncSetAttribute((const void*)gemm_s6_kernel<EPI, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S5_LDS);
-      (void)hipFuncSetAttribute((const void*)gemm_s6_kernel<EPI, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, S5_LDS);
-      attr6 = 1;
-    }
-    if (variant == 12)
-      hipLaunchKernelGGL((gemm_s6_kernel<EPI, 1>), dim3(nm * nn, 1, batch), dim3(256), S5_LDS, st, g);
-    else
-      hipLaunchKernelGGL((gemm_s6_kernel<EPI, 2>), dim3(nm * nn, 1, batch), dim3(256), S5_LDS, st, g);
-  } else if (variant >= 6 && variant <= 8 && EPI == EPI_BF16 && g.K % 128 == 0) {
-    static int attr_abl = 0;
-    if (!attr_abl) {
-      (void)hipFuncSetAttribute((const void*)gemm_s4_kernel<EPI, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, S4_LDS);
-      (void)hipFuncSetAttribute((const void*)gemm_s4_kernel<EPI, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, S4_LDS);
-      (void)hipFuncSetAttribute((const void*)gemm_s4_kernel<EPI, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, S4_LDS);
-      attr_abl = 1;
-    }
-    if (variant == 6)
-      hipLaunchKernelGGL((gemm_s4_kernel<EPI, 1>), dim3(nm * nn, 1, batch), dim3(256), S4_LDS, st, g);
-    else if (variant == 7)
-      hipLaunchKernelGGL((gemm_s4_kernel<EPI, 2>), dim3(nm * nn, 1, batch), dim3(256), S4_LDS, st, g);
-    else
-      hipLaunchKernelGGL((gemm_s4_kernel<EPI, 3>), dim3(nm * nn, 1, batch), dim3(256), S4_LDS, st, g);
-  } else
+  if (persistent)
+    hipLaunchKernelGGL(gemm_s8_kernel<EPI>, dim3(min(nm * nn * batch, num_cus())), dim3(256), S7_LDS, st, g, batch);
+  else
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, true>), dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
   SA_LAUNCH_CHECK();
   return SA_OK;
@@ -1788,47 +785,35 @@ int launch(const GemmArgs& g_in, int batch, hipStream_t st) {
 
 }  // namespace
 
-int g_group_m_override = 0;
-extern "C" int sa_gemm_set_group_m(int gm) {
-  if (gm < 0) return SA_ERR_ARG;
-  g_group_m_override = gm;
-  return SA_OK;
-}
-
-extern "C" int sa_gemm_set_variant(int variant) {
-  if (variant < 0 || variant > 16) return SA_ERR_ARG;
-  g_gemm_variant = variant;
-  return SA_OK;
+extern "C" int sa_gemm_bf16_ex(const void* A, int64_t lda, int64_t strideA, const void* W, int64_t ldw,
+                               int64_t strideW, const float* bias, void* C, int64_t ldc, int64_t strideC, int M, int N,
+                               int K, int batch, int epilogue, const float* residual, int64_t ldr, int64_t strideR,
+                               const float* gate, int64_t gate_bstride, int rows_per_batch, int kernel, int group_m,
+                               void* stream) {
+  if (!A || !W || !C || M <= 0 || N <= 0 || K <= 0 || batch <= 0) return SA_ERR_ARG;
+  if (K % BK != 0 || lda % 8 != 0 || ldw % 8 != 0) return SA_ERR_ARG;
+  if ((((uintptr_t)A) & 15) || (((uintptr_t)W) & 15)) return SA_ERR_ARG;
+  if (epilogue == EPI_RES_F32 && (!residual || (gate && rows_per_batch <= 0))) return SA_ERR_ARG;
+  if (kernel < KERNEL_AUTO || kernel > KERNEL_PERSISTENT || group_m < 0) return SA_ERR_ARG;
+  GemmArgs g{(const bf16*)A, lda, strideA, (const bf16*)W, ldw, strideW, bias, C, ldc, strideC,
+             residual, ldr, strideR, gate, gate_bstride, rows_per_batch > 0 ? rows_per_batch : 1, M, N, K,
+             group_m > 0 ? group_m : env_group_m()};
+  hipStream_t st = (hipStream_t)stream;
+  switch (epilogue) {
+    case EPI_BF16: return launch<EPI_BF16>(g, batch, kernel, st);
+    case EPI_GELU_BF16: return launch<EPI_GELU_BF16>(g, batch, kernel, st);
+    case EPI_F32: return launch<EPI_F32>(g, batch, kernel, st);
+    case EPI_RES_F32: return launch<EPI_RES_F32>(g, batch, kernel, st);
+    case EPI_GELU_ERF_BF16: return launch<EPI_GELU_ERF_BF16>(g, batch, kernel, st);
+    case EPI_SILU_F32: return launch<EPI_SILU_F32>(g, batch, kernel, st);
+    default: return SA_ERR_ARG;
+  }
 }
 
 extern "C" int sa_gemm_bf16(const void* A, int64_t lda, int64_t strideA, const void* W, int64_t ldw, int64_t strideW,
                             const float* bias, void* C, int64_t ldc, int64_t strideC, int M, int N, int K, int batch,
                             int epilogue, const float* residual, int64_t ldr, int64_t strideR, const float* gate,
                             int64_t gate_bstride, int rows_per_batch, void* stream) {
-  if (!A || !W || !C || M <= 0 || N <= 0 || K <= 0 || batch <= 0) return SA_ERR_ARG;
-  if (K % BK != 0 || lda % 8 != 0 || ldw % 8 != 0) return SA_ERR_ARG;
-  if ((((uintptr_t)A) & 15) || (((uintptr_t)W) & 15)) return SA_ERR_ARG;
-  if (epilogue == EPI_RES_F32 && (!residual || (gate && rows_per_batch <= 0))) return SA_ERR_ARG;
-  static int group_m_env = -1;
-  if (group_m_env < 0) {
-    const char* e = getenv("SA_GEMM_GROUP_M");
-    group_m_env = e ? atoi(e) : 0;
-    if (group_m_env < 0) group_m_env = 0;
-  }
-  // 0 = chosen per kernel in launch(): ping-pong runs of 8 tile rows for N >= 4096 (QKV +2.3 %, FFN-up
-  // +2.8 %; the N = 1536 ones lose up to 2.7 %), LDS-DMA kernel runs of 4
-  const int group_m = group_m_env;
-  GemmArgs g{(const bf16*)A, lda, strideA, (const bf16*)W, ldw, strideW, bias, C, ldc, strideC,
-             residual, ldr, strideR, gate, gate_bstride, rows_per_batch > 0 ? rows_per_batch : 1, M, N, K,
-             g_group_m_override > 0 ? g_group_m_override : group_m};
-  hipStream_t st = (hipStream_t)stream;
-  switch (epilogue) {
-    case EPI_BF16: return launch<EPI_BF16>(g, batch, st);
-    case EPI_GELU_BF16: return launch<EPI_GELU_BF16>(g, batch, st);
-    case EPI_F32: return launch<EPI_F32>(g, batch, st);
-    case EPI_RES_F32: return launch<EPI_RES_F32>(g, batch, st);
-    case EPI_GELU_ERF_BF16: return launch<EPI_GELU_ERF_BF16>(g, batch, st);
-    case EPI_SILU_F32: return launch<EPI_SILU_F32>(g, batch, st);
-    default: return SA_ERR_ARG;
-  }
+  return sa_gemm_bf16_ex(A, lda, strideA, W, ldw, strideW, bias, C, ldc, strideC, M, N, K, batch, epilogue, residual,
+                         ldr, strideR, gate, gate_bstride, rows_per_batch, KERNEL_AUTO, 0, stream);
 }

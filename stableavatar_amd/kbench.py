@@ -24,15 +24,14 @@ def _time(fn, iters=10, warmup=2):
 
 
 def main(which=("gemm", "attn")):
-    from ._lib import call
     dev = "cuda"
     torch.manual_seed(0)
     M = 3 * 21504
     res = []
-    if "gemmvar" in which:  # A/B of the GEMM variants in one process (rule: interleaved rounds)
+    if "gemmvar" in which:  # A/B of the GEMM kernels in one process (rule: interleaved rounds)
         import os
-        # variant spec "V" or "V:G" (G = tile-raster group_m)
-        gvars = tuple(os.environ.get("SA_KB_GVARS", "3,4").split(","))
+        # spec "K" or "K:G": K = kernel (0 auto, 1 ping-pong, 2 persistent), G = tile-raster group_m
+        gvars = tuple(os.environ.get("SA_KB_GVARS", "1,2").split(","))
         for (Mx, N, K, epi, name) in [(M, 4608, 1536, ops.EPI_BF16, "qkv"), (M, 1536, 1536, ops.EPI_RES_F32, "o_proj"),
                                       (M, 1536, 1536, ops.EPI_BF16, "cross_q"),
                                       (M, 8960, 1536, ops.EPI_GELU_TANH_BF16, "ffn_up"),
@@ -50,15 +49,15 @@ def main(which=("gemm", "attn")):
             for rnd in range(3):
                 for v in gvars:
                     vv, _, gm = v.partition(":")
-                    call("sa_gemm_set_variant", int(vv))
-                    call("sa_gemm_set_group_m", int(gm or 0))
+                    kw = dict(kernel=int(vv), group_m=int(gm or 0))
                     if epi == ops.EPI_RES_F32:
                         out.zero_()
-                        fn = lambda: ops.linear(x, w, b, epi, out=out, residual=out, gate=gate, rows_per_batch=21504)
+                        fn = lambda: ops.linear(x, w, b, epi, out=out, residual=out, gate=gate, rows_per_batch=21504,
+                                                **kw)
                     else:
-                        fn = lambda: ops.linear(x, w, b, epi, out=out)
+                        fn = lambda: ops.linear(x, w, b, epi, out=out, **kw)
                     times[v].append(_time(fn, iters=5, warmup=1))
-                    if epi != ops.EPI_RES_F32 and int(vv) not in (6, 7, 8, 12, 13):
+                    if epi != ops.EPI_RES_F32:
                         o = out.float()
                         if ref is None:
                             ref = o.clone()
@@ -75,8 +74,6 @@ def main(which=("gemm", "attn")):
             res.append(r)
             print(json.dumps(r), flush=True)
             del x, w, out
-        call("sa_gemm_set_variant", 15)
-        call("sa_gemm_set_group_m", 0)
     if "attnvar" in which:
         import os
         L, H, D = 21504, 12, 128
@@ -84,13 +81,12 @@ def main(which=("gemm", "attn")):
         segs = torch.tensor([[b * L, L, b * L, L] for b in range(3)], dtype=torch.int32, device=dev)
         q, k, v_ = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
         outs = {}
-        variants = tuple(int(v) for v in os.environ.get("SA_KB_AVARS", "0,3,5").split(","))
+        variants = tuple(int(v) for v in os.environ.get("SA_KB_AVARS", "1").split(","))
         times = {v: [] for v in variants}
         for rnd in range(3):
             for v in variants:
-                call("sa_attn_set_variant", v)
                 o = torch.empty(3 * L, H * D, device=dev, dtype=torch.bfloat16)
-                times[v].append(_time(lambda: ops.attention(q, k, v_, o, segs, 3, L, H), iters=3, warmup=1))
+                times[v].append(_time(lambda: ops.attention(q, k, v_, o, segs, 3, L, H, kernel=v), iters=3, warmup=1))
                 outs[v] = o.float()
         fl = 4.0 * 3 * H * L * L * D
         r = {"kernel": "attn_self"}
@@ -101,7 +97,6 @@ def main(which=("gemm", "attn")):
             r[f"v{v}_tflops"] = round(fl / ms / 1e9, 1)
         res.append(r)
         print(json.dumps(r), flush=True)
-        call("sa_attn_set_variant", 6)
     if "gemm" in which:
         for (N, K, epi, name) in [(4608, 1536, ops.EPI_BF16, "qkv"), (1536, 1536, ops.EPI_RES_F32, "o_proj"),
                                   (8960, 1536, ops.EPI_GELU_TANH_BF16, "ffn_up"),
@@ -185,7 +180,7 @@ def main(which=("gemm", "attn")):
         print(json.dumps(res[-1]), flush=True)
     if "ditvar" in which:  # in-situ A/B of attention variants inside full DiT forwards (interleaved)
         import os
-        avars = tuple(int(v) for v in os.environ.get("SA_KB_AVARS", "5,6").split(","))
+        avars = tuple(int(v) for v in os.environ.get("SA_KB_AVARS", "1").split(","))
         res.append(bench_dit(attn_variants=avars))
         print(json.dumps(res[-1]), flush=True)
     return res
@@ -216,14 +211,13 @@ def bench_dit(iters=3, attn_variants=None):
     from .flops import dit_forward_flops
     fl = dit_forward_flops()
     if attn_variants:
-        from ._lib import call
         times = {v: [] for v in attn_variants}
         with torch.no_grad():
             for _ in range(3):
                 for v in attn_variants:
-                    call("sa_attn_set_variant", v)
+                    m.attn_kernel = v
                     times[v].append(_time(fwd, iters=2, warmup=1))
-        call("sa_attn_set_variant", 6)
+        m.attn_kernel = 0
         r = {"kernel": "dit_forward_attn_ab", "tflop": round(fl / 1e12, 1)}
         for v in attn_variants:
             r[f"attn_v{v}_ms"] = round(sorted(times[v])[1], 2)

@@ -35,9 +35,14 @@ def _check(t, dtype, name):
         raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
 
 
-def linear(x, weight, bias=None, epilogue=EPI_BF16, out=None, residual=None, gate=None, rows_per_batch=0):
+GEMM_AUTO, GEMM_PINGPONG, GEMM_PERSISTENT = 0, 1, 2
+
+
+def linear(x, weight, bias=None, epilogue=EPI_BF16, out=None, residual=None, gate=None, rows_per_batch=0,
+           kernel=GEMM_AUTO, group_m=0):
     """y = epi(x @ weight^T + bias).  x: bf16 [M, K] (row stride may exceed K), weight: bf16 [N, K].
-    EPI_RES_F32: out(f32) = residual + y * gate[row // rows_per_batch] (gate f32 [B, N] view)."""
+    EPI_RES_F32: out(f32) = residual + y * gate[row // rows_per_batch] (gate f32 [B, N] view).
+    kernel / group_m: per-call GEMM schedule selection (A/B benchmarks and tests; default auto)."""
     _check(x, torch.bfloat16, "linear.x")
     _check(weight, torch.bfloat16, "linear.weight")
     M, K = x.shape
@@ -59,32 +64,37 @@ def linear(x, weight, bias=None, epilogue=EPI_BF16, out=None, residual=None, gat
         if gate is not None:
             assert gate.dtype == torch.float32 and gate.stride(-1) == 1
             gstride = gate.stride(0)
-    call("sa_gemm_bf16", x.data_ptr(), x.stride(0), 0, weight.data_ptr(), weight.stride(0), 0, _p(bias),
+    call("sa_gemm_bf16_ex", x.data_ptr(), x.stride(0), 0, weight.data_ptr(), weight.stride(0), 0, _p(bias),
          out.data_ptr(), out.stride(0), 0, M, N, K, 1, epilogue, _p(residual), ldr, 0, _p(gate), gstride,
-         rows_per_batch, _stream())
+         rows_per_batch, kernel, group_m, _stream())
     return out
 
 
-def bmm_nt(a, b, out, epilogue=EPI_F32):
+def bmm_nt(a, b, out, epilogue=EPI_F32, kernel=GEMM_AUTO):
     """out[z] = a[z] @ b[z]^T for 3-D bf16 a [Z, M, K], b [Z, N, K]."""
     Z, M, K = a.shape
     N = b.shape[1]
-    call("sa_gemm_bf16", a.data_ptr(), a.stride(1), a.stride(0), b.data_ptr(), b.stride(1), b.stride(0), 0,
-         out.data_ptr(), out.stride(1), out.stride(0), M, N, K, Z, epilogue, 0, 0, 0, 0, 0, 0, _stream())
+    call("sa_gemm_bf16_ex", a.data_ptr(), a.stride(1), a.stride(0), b.data_ptr(), b.stride(1), b.stride(0), 0,
+         out.data_ptr(), out.stride(1), out.stride(0), M, N, K, Z, epilogue, 0, 0, 0, 0, 0, 0, kernel, 0, _stream())
     return out
 
 
-def attention(q, k, v, out, segs, nseg, max_q_len, heads, head_dim=128, scale=None, accumulate=False):
-    """Flash attention over row-segment table `segs` (int32 [nseg,4] on device)."""
+ATTN_AUTO = 0
+
+
+def attention(q, k, v, out, segs, nseg, max_q_len, heads, head_dim=128, scale=None, accumulate=False,
+              kernel=ATTN_AUTO):
+    """Flash attention over row-segment table `segs` (int32 [nseg,4] on device); kernel = per-call
+    schedule selection (sa_attn_fwd_ex; 0 = auto)."""
     for t, n in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
         _check(t, torch.bfloat16, f"attention.{n}")
         assert t.stride(-1) == 1
     assert segs.dtype == torch.int32 and segs.is_cuda
     if scale is None:
         scale = head_dim ** -0.5
-    call("sa_attn_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), segs.data_ptr(), nseg, max_q_len,
-         heads, head_dim, q.stride(0), k.stride(0), v.stride(0), out.stride(0), float(scale), int(accumulate),
-         _stream())
+    call("sa_attn_fwd_ex", q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), segs.data_ptr(), nseg,
+         max_q_len, heads, head_dim, q.stride(0), k.stride(0), v.stride(0), out.stride(0), float(scale),
+         int(accumulate), kernel, _stream())
     return out
 
 

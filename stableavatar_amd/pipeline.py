@@ -88,12 +88,26 @@ class WanI2VTalkingInferenceLongPipeline:
         forward) and every rank applies the CFG / Euler / blend steps of all windows in the
         reference order -- bit-identical latents on every rank and to the single-GPU loop."""
         import torch.distributed as dist
-        if self.transformer is not None and getattr(self.transformer, "sp_world_size", 1) > 1:
+        self._check_window_parallel(self.transformer)
+        self.window_group = group if group is not None else dist.group.WORLD
+        return self
+
+    def disable_window_parallel(self):
+        self.window_group = None
+        return self
+
+    @staticmethod
+    def _check_window_parallel(transformer):
+        if transformer is None:
+            return
+        if getattr(transformer, "sp_world_size", 1) > 1:
             raise RuntimeError("window parallelism and sequence parallelism over the same ranks would deadlock "
                                "(each rank runs different windows while SP needs all ranks in every forward); "
                                "use one of them")
-        self.window_group = group if group is not None else dist.group.WORLD
-        return self
+        if getattr(transformer, "teacache", None) is not None:
+            raise RuntimeError("window parallelism cannot be combined with TeaCache: its skip decisions and reused "
+                               "residual follow the sequence of forwards one process runs (cache_utils.py:59-80), "
+                               "which window parallelism changes (rank r sees windows r, r+N, ..)")
 
     def to(self, device=None, **_):
         if device is not None:
@@ -187,6 +201,7 @@ class WanI2VTalkingInferenceLongPipeline:
         import torch.distributed as dist
 
         from . import sp
+        self._check_window_parallel(self.transformer)  # the transformer may have changed since enable
         grp = self.window_group
         N, r = dist.get_world_size(grp), dist.get_rank(grp)
         dev = lat.device

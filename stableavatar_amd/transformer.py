@@ -203,7 +203,7 @@ class WanTransformer3DFantasyModel(nn.Module):
         self.sp_world_size, self.sp_world_rank, self.sp_group = 1, 0, None
         self.teacache = None  # enable_teacache() (1B:867)
         self._riflex = None  # enable_riflex() (1B:890-905)
-        self.teacache = None
+        self.attn_kernel = 0  # self-attention schedule (sa_attn_fwd_ex; 0 = auto), for in-situ A/B
         self._packed = None
         self._ws = {}
         self._ctx_cache = None
@@ -269,12 +269,6 @@ class WanTransformer3DFantasyModel(nn.Module):
         self._ws = {}
         return super()._apply(fn, recurse)
 
-    def enable_teacache(self, *a, **k):
-        raise NotImplementedError("TeaCache changes the numerics and is out of scope (SURVEY.md §2 #11)")
-
-    def disable_teacache(self):
-        self.teacache = None
-
     def enable_riflex(self, k=6, L_test=66, L_test_scale=4.886):
         """1B:890-905: RIFLEx frame frequencies for length extrapolation."""
         self._riflex = (k, L_test, L_test_scale)
@@ -306,6 +300,10 @@ class WanTransformer3DFantasyModel(nn.Module):
         self.sp_group = group
         self.sp_world_size = dist.get_world_size(group)
         self.sp_world_rank = dist.get_rank(group)
+
+    def disable_multi_gpus_inference(self):
+        """back to single-GPU forwards (every rank its own clip)"""
+        self.sp_group, self.sp_world_size, self.sp_world_rank = None, 1, 0
 
     # ------------------------------------------------------------------ packing
 
@@ -492,6 +490,24 @@ class WanTransformer3DFantasyModel(nn.Module):
         ops.layernorm_mod(x, hb, 1e-6, shift=ef[0, 0, 0:1], scale=ef[0, 0, 1:2], rows_per_batch=Mv)
         return ops.linear(hb, V.w_fp, V.b_fp, ops.EPI_BF16), Fn, nper
 
+    # ------------------------------------------------------------------ timing hooks (bench.py)
+
+    def _record_event(self):
+        """HIP event on the current stream (the one the attention kernel is launched on), or None."""
+        if self._events is None:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def _record_span(self, ev0, rows, batch):
+        """close a self-attention span opened by _record_event; `rows` of the `batch` CFG rows ran in it"""
+        if ev0 is None:
+            return
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev1.record()
+        self._events.append((ev0, ev1, rows / batch))
+
     # ------------------------------------------------------------------ forward
 
     def forward(self, x, t, context, seq_len, clip_fea=None, y=None, cond_flag=True, vocal_embeddings=None,
@@ -644,8 +660,10 @@ class WanTransformer3DFantasyModel(nn.Module):
                     back = []
                     for b in range(B):
                         pend[b].wait()
+                        ev0 = self._record_event()
                         ops.attention(q_sp, kv_sp[:, :hg * self.d], kv_sp[:, hg * self.d:], o_sp, segs_rows[b], 1, Lq,
-                                      hg)
+                                      hg, kernel=self.attn_kernel)
+                        self._record_span(ev0, rows=1, batch=B)
                         back.append(exch.to_tokens_row(o_sp, b, B, Lc, self.d, ws.att))
                     for b in range(B):
                         rs = slice(b * Lc, (b + 1) * Lc)
@@ -661,14 +679,9 @@ class WanTransformer3DFantasyModel(nn.Module):
                     else:
                         args_ = (ws.qkv[:, :dim], ws.qkv[:, dim:2 * dim], ws.qkv[:, 2 * dim:], ws.att, segs_self, B, Lp,
                                  H_)
-                    if self._events is not None:  # bench.py: HIP events around the self-attention kernel
-                        ev0 = torch.cuda.Event(enable_timing=True)
-                        ev0.record()
-                    ops.attention(*args_)
-                    if self._events is not None:
-                        ev1 = torch.cuda.Event(enable_timing=True)
-                        ev1.record()
-                        self._events.append((ev0, ev1))
+                    ev0 = self._record_event()
+                    ops.attention(*args_, kernel=self.attn_kernel)
+                    self._record_span(ev0, rows=B, batch=B)
                     if NS > 1:
                         exch.to_tokens(o_sp, B, Lc, self.d, ws.att)
                     ops.linear(ws.att, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2],

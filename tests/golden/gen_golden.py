@@ -136,12 +136,13 @@ class _Obj(types.SimpleNamespace):
         return [self.last][i]
 
 
-def gen_pipeline():
+def gen_pipeline(P=PIPE, name="pipeline_small"):
+    import time
     from PIL import Image
     from wan.pipeline.wan_inference_long_pipeline import WanI2VTalkingInferenceLongPipeline
     from _refstub import FlowMatchEulerDiscreteScheduler
 
-    P = PIPE
+    t_start = time.time()
     dit = build_ref_dit(P["dit"])
     vae = build_ref_vae(P["vae"])
     fx = pipe_fixed_inputs(P)
@@ -217,8 +218,23 @@ def gen_pipeline():
            "win_F": np.array([c["F"] for c in calls]), "win_t": np.array([c["t"] for c in calls]),
            "win_seq_len": np.array([c["seq_len"] for c in calls]),
            "win_n_audio": np.array([c["n_audio"] for c in calls])}
-    print("pipeline windows", [(c["F"], round(c["t"], 2), c["n_audio"]) for c in calls], tuple(video.shape))
-    np.savez_compressed(os.path.join(HERE, "pipeline_small.npz"), **out)
+    if name != "pipeline_small":  # big video: keep a few decoded frames in fp16
+        from golden_cases import PIPE_C1_VIDEO_FRAMES
+        out["video"] = out["video"][:, :, list(PIPE_C1_VIDEO_FRAMES)].astype(np.float16)
+        out["video_frames"] = np.array(PIPE_C1_VIDEO_FRAMES)
+        out["y"] = out["y"][:1]  # the 3 CFG rows are identical (pipeline:700)
+        out["ref_cpu_seconds"] = np.array(time.time() - t_start)
+        out["ref_cpu_threads"] = np.array(torch.get_num_threads())
+    print(name, "windows", [(c["F"], round(c["t"], 2), c["n_audio"]) for c in calls], tuple(video.shape),
+          f"{time.time() - t_start:.1f}s")
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+
+
+def gen_pipeline_c1():
+    """BASELINE config 1 through the reference's own __call__: full 30-layer 1.3B DiT + full VAE at
+    256x256, clip 17, 5 steps, 2 windows per step (golden_cases.PIPE_C1)."""
+    from golden_cases import PIPE_C1
+    gen_pipeline(PIPE_C1, "pipeline_c1")
 
 
 def gen_tables():

@@ -56,6 +56,16 @@ PIPE = dict(dit=dict(DIT_SMALL, num_layers=1, seed=31), vae=dict(dim=32, seed=32
             audio_frames=24)
 
 
+# BASELINE config 1: the full Wan-1.3B StableAvatar DiT (30 layers, dim 1536, ffn 8960,
+# text_dim 4096) and the full-width VAE (dim 96) at 256x256, clip 17 (5 latent frames), 5 sampling steps,
+# overlap 2, 24 video frames of audio -> T_lat 6 -> windows (0,5),(3,6) per step
+DIT_FULL = dict(model_type="i2v", dim=1536, ffn_dim=8960, freq_dim=256, text_dim=4096, in_dim=36, out_dim=16,
+                num_heads=12, num_layers=30, text_len=512, eps=1e-6)
+PIPE_C1 = dict(dit=dict(DIT_FULL, seed=41), vae=dict(dim=96, seed=42), height=256, width=256, clip_length=17,
+               steps=5, overlap=2, text_guide=3.0, audio_guide=5.0, neg_len=24, pos_len=31, audio_frames=24)
+PIPE_C1_VIDEO_FRAMES = (0, 4, 9, 16, 20)  # decoded frames stored in the golden (fp16)
+
+
 def pipe_fixed_inputs(P):
     """Seeded inputs of the pipeline golden: 24 video frames of audio @16 kHz -> T_lat 6 -> two
     windows (0,5),(3,6) per step (avoids the reference's single-window hang, App. A.1)."""

@@ -1,0 +1,129 @@
+"""bench.py's multi-process orchestration on CPU (gloo, world 2), with a stand-in workload in place of
+the HIP clip: rank/world handling, the barrier-bracketed timing with the max over ranks, the SP default
+for N > 1 with the extra `replicas` key, the per-row attention-span accounting and the JSON line."""
+import json
+import os
+import socket
+import sys
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+class _Ev:
+    """stands in for a torch.cuda.Event pair: elapsed_time in ms"""
+
+    def __init__(self, ms):
+        self.ms = ms
+
+    def elapsed_time(self, other):
+        return other.ms - self.ms
+
+
+class FakeClip:
+    """CPU stand-in with ClipWorkload's interface: a small all-reduce per step in SP layout (the data
+    path collective), none in replicas layout; attention spans as the per-row SP path records them
+    (three rows of 1/3 each, 2 ms apiece -> 6 ms per whole launch)."""
+
+    def __init__(self, args, dev, rank, world):
+        self.args, self.rank, self.world = args, rank, world
+        self.fpb = (args.frames - 1) // 4 + 1
+        self.h = args.size // 8
+        self.seq_len = self.fpb * (self.h // 2) ** 2
+        self.T = self.fpb
+        self.wins = [(0, self.fpb, self.fpb)]
+        self.out_frames = args.frames
+        self.layout = None
+        self.events = None
+        self.steps_run = 0
+
+    def set_layout(self, layout):
+        self.layout = layout
+
+    def step(self):
+        x = torch.full((4,), float(self.rank + 1))
+        if self.layout == "sp":
+            dist.all_reduce(x)
+        if self.events is not None:
+            for _ in range(3):
+                self.events.append((_Ev(0.0), _Ev(2.0), 1 / 3))
+        self.steps_run += 1
+        return torch.zeros(3, self.out_frames, 8, 8)
+
+    def check(self, video):
+        assert video.shape[1] == self.out_frames
+
+    def start_events(self):
+        self.events = []
+
+    def attention_launch_ms(self):
+        ev, self.events = self.events, None
+        return sum(a.elapsed_time(b) for a, b, _ in ev) / sum(f for _, _, f in ev)
+
+    def n_fwd(self):
+        return self.args.sample_steps * len(self.wins)
+
+
+def _worker(rank, world, port, argv, path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    out = open(path + f".{rank}", "w")
+    sys.stdout = out
+    try:
+        bench.main(argv, work_factory=FakeClip, device="cpu")
+    finally:
+        out.close()
+
+
+def _run(world, argv, tmp_path):
+    path = str(tmp_path / "bench")
+    mp.start_processes(_worker, args=(world, _free_port(), argv, path), nprocs=world, join=True,
+                       start_method="spawn")
+    lines = [open(path + f".{r}").read().strip() for r in range(world)]
+    assert all(not ln for ln in lines[1:]), "only rank 0 prints"
+    return json.loads(lines[0])
+
+
+def test_bench_sp_default_world2(tmp_path):
+    j = _run(2, ["--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-encode"], tmp_path)
+    assert j["n_gpus"] == 2 and j["steps"] == 2 and j["warmup"] == 1
+    assert j["scaling"] == "strong" and j["config"]["parallelism"] == "ulysses2"
+    assert j["config"]["global_batch"] == 3
+    assert j["value"] > 0 and j["ms_per_step"] > 0
+    # one clip of 81 frames per step, over all ranks
+    assert abs(j["value"] * j["ms_per_step"] / 1e3 / 81 - 1) < 0.1  # ms_per_step is rounded to 0.1 ms
+    # per-row spans (3 x 1/3 of the batch, 2 ms each) -> 6 ms per whole launch, flop = this rank's half
+    assert j["roofline"]["launch_ms"] == 6.0
+    assert j["roofline"]["flop_per_launch"] == 4.0 * 3 * 12 * 21504 ** 2 * 128 / 2
+    assert j["replicas"]["scaling"] == "weak" and j["replicas"]["parallelism"] == "replicas2"
+    for k in ("metric", "unit", "higher_is_better", "vs_baseline", "dtype", "data", "config", "roofline",
+              "cpu_baseline"):
+        assert k in j
+
+
+def test_bench_replicas_mode_world2(tmp_path):
+    j = _run(2, ["--gpus", "2", "--steps", "1", "--warmup", "0", "--mode", "replicas", "--no-cpu-baseline",
+                 "--no-encode"], tmp_path)
+    assert j["scaling"] == "weak" and j["config"]["parallelism"] == "replicas2"
+    assert j["config"]["global_batch"] == 6 and "replicas" not in j
+
+
+def test_bench_parse_defaults():
+    a = bench.parse([])
+    assert a.gpus == 1 and a.mode == "sp" and a.steps >= 1
+    assert bench.parse(["--window-dp"]).mode == "window-dp"
+    assert bench.cpu_cores() >= 1 and isinstance(bench.cpu_model(), str)

@@ -50,35 +50,43 @@ def test_gemm_epilogues(M, N, K):
     assert rel(out, res + ref.bfloat16().float() * g_rows) < 2e-3
 
 
-@pytest.mark.parametrize("variant", [3, 4, 5, 9, 10, 11, 14, 15, 16])
+@pytest.mark.parametrize("kernel", [0, 1, 2], ids=["auto", "pingpong", "persistent"])
 @pytest.mark.parametrize("M,N,K", [(300, 520, 256), (257, 130, 128), (1000, 1536, 1536), (600, 300, 2304)])
-def test_gemm_variants(variant, M, N, K):
-    """Every GEMM schedule (sa_gemm_set_variant) on ragged M/N tiles, every epilogue, vs torch fp32."""
+def test_gemm_kernels(kernel, M, N, K):
+    """Both shipped GEMM schedules (per-call selection, sa_gemm_bf16_ex) on ragged M/N tiles, every
+    epilogue, vs torch fp32."""
     from stableavatar_amd import ops
-    from stableavatar_amd._lib import call
-    call("sa_gemm_set_variant", variant)
-    try:
-        x = torch.randn(M, K + 64, device=dev).bfloat16()[:, 32:32 + K]  # strided rows
-        w = (torch.randn(N, K, device=dev) / math.sqrt(K)).bfloat16()
-        b = torch.randn(N, device=dev)
-        ref = x.float() @ w.float().t() + b
-        assert rel(ops.linear(x, w, b, ops.EPI_BF16), ref) < 1e-2
-        assert rel(ops.linear(x, w, b, ops.EPI_F32), ref) < 2e-3
-        assert rel(ops.linear(x, w, b, ops.EPI_GELU_TANH_BF16), torch.nn.functional.gelu(ref, approximate="tanh")) < 1e-2
-        B = 3
-        rpb = (M + B - 1) // B
-        res = torch.randn(M, N, device=dev)
-        gate = torch.randn(B, N, device=dev)
-        out = res.clone()
-        ops.linear(x, w, b, ops.EPI_RES_F32, out=out, residual=out, gate=gate, rows_per_batch=rpb)
-        assert rel(out, res + ref.bfloat16().float() * gate[torch.arange(M, device=dev) // rpb]) < 2e-3
-        a = torch.randn(2, 300, K, device=dev).bfloat16()
-        bb = torch.randn(2, 200, K, device=dev).bfloat16()
-        o = torch.empty(2, 300, 200, device=dev)
-        ops.bmm_nt(a, bb, o)
-        assert rel(o, a.float() @ bb.float().transpose(1, 2)) < 2e-3
-    finally:
-        call("sa_gemm_set_variant", 15)
+    kw = dict(kernel=kernel)
+    x = torch.randn(M, K + 64, device=dev).bfloat16()[:, 32:32 + K]  # strided rows
+    w = (torch.randn(N, K, device=dev) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device=dev)
+    ref = x.float() @ w.float().t() + b
+    assert rel(ops.linear(x, w, b, ops.EPI_BF16, **kw), ref) < 1e-2
+    assert rel(ops.linear(x, w, b, ops.EPI_F32, **kw), ref) < 2e-3
+    assert rel(ops.linear(x, w, b, ops.EPI_GELU_TANH_BF16, **kw), torch.nn.functional.gelu(ref, approximate="tanh")) < 1e-2
+    B = 3
+    rpb = (M + B - 1) // B
+    res = torch.randn(M, N, device=dev)
+    gate = torch.randn(B, N, device=dev)
+    out = res.clone()
+    ops.linear(x, w, b, ops.EPI_RES_F32, out=out, residual=out, gate=gate, rows_per_batch=rpb, **kw)
+    assert rel(out, res + ref.bfloat16().float() * gate[torch.arange(M, device=dev) // rpb]) < 2e-3
+    a = torch.randn(2, 300, K, device=dev).bfloat16()
+    bb = torch.randn(2, 200, K, device=dev).bfloat16()
+    o = torch.empty(2, 300, 200, device=dev)
+    ops.bmm_nt(a, bb, o, kernel=kernel)
+    assert rel(o, a.float() @ bb.float().transpose(1, 2)) < 2e-3
+
+
+def test_gemm_persistent_rejects_k192():
+    """the persistent kernel needs K % 128 == 0: an explicit request is refused, auto falls back"""
+    from stableavatar_amd import ops
+    from stableavatar_amd._lib import KernelError
+    x = torch.randn(64, 192, device=dev).bfloat16()
+    w = torch.randn(64, 192, device=dev).bfloat16()
+    with pytest.raises(KernelError):
+        ops.linear(x, w, None, ops.EPI_F32, kernel=2)
+    assert rel(ops.linear(x, w, None, ops.EPI_F32), x.float() @ w.float().t()) < 2e-3
 
 
 def test_gemm_strided_input_and_batched():
@@ -100,17 +108,8 @@ def _ref_attn(q, k, v, scale):
     return torch.softmax(s, -1) @ v.float()
 
 
-@pytest.fixture(params=[5, 6], ids=["attn_v5", "attn_v6"])
-def attn_variant(request):
-    """run an attention test under each shipped schedule (5 = 32x32x16 MFMA, 6 = 16x16x32 MFMA)"""
-    from stableavatar_amd._lib import call
-    call("sa_attn_set_variant", request.param)
-    yield request.param
-    call("sa_attn_set_variant", 6)
-
-
 @pytest.mark.parametrize("Lq,Lk", [(300, 300), (512, 257), (1024, 17), (64, 512)])
-def test_attention_segments(Lq, Lk, attn_variant):
+def test_attention_segments(Lq, Lk):
     from stableavatar_amd import ops
     B, H, D = 2, 3, 128
     q = torch.randn(B * Lq, H * D + 64, device=dev).bfloat16()[:, :H * D]  # strided rows
@@ -130,7 +129,7 @@ def test_attention_segments(Lq, Lk, attn_variant):
     assert rel(o2, 2 * o.float()) < 1e-2
 
 
-def test_attention_vocal_grouping(attn_variant):
+def test_attention_vocal_grouping():
     """per-frame grouping of 1B:575-586: q rows of frame f attend to that frame's 17 keys"""
     from stableavatar_amd import ops
     B, F, G, Lv, H, D = 2, 3, 64, 17, 2, 128
@@ -147,7 +146,7 @@ def test_attention_vocal_grouping(attn_variant):
             assert rel(o[i * G:(i + 1) * G, sl], ref) < 1e-2
 
 
-def test_attention_spike_rescale(attn_variant):
+def test_attention_spike_rescale():
     """force the online-softmax rescale branch: a late key with a huge score"""
     from stableavatar_amd import ops
     L, D = 512, 128
