@@ -45,7 +45,10 @@ def parse(argv=None):
     p.add_argument("--overlap", type=int, default=15)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-cpu-config1", action="store_true",
-                   help="skip the end-to-end config-1 run of the CPU oracle inside cpu_baseline")
+                   help="skip the config-1 run of the CPU oracle inside cpu_baseline")
+    p.add_argument("--cpu-config1-steps", type=int, default=1,
+                   help="sampling steps of the config-1 CPU oracle run actually executed (1..5; the rest of the 5 "
+                        "are extrapolated from the measured per-step time; 5 = fully end to end)")
     p.add_argument("--no-encode", action="store_true", help="skip the (untimed) VAE encode measurement")
     p.add_argument("--mode", choices=("sp", "replicas", "window-dp"), default=None,
                    help="N>1 layout (default sp); ignored at N=1")
@@ -79,8 +82,12 @@ def launch_workers(args, argv) -> int:
 # ------------------------------------------------------------------------------------------------ CPU baseline
 
 def cpu_cores() -> int:
-    """Cores this process may use: the affinity mask, capped by a cgroup-v2 CPU quota."""
+    """Cores this process may use: the affinity mask, capped by a cgroup-v2 CPU quota and by the
+    OMP_NUM_THREADS share the host sets (the GPU box's per-GPU CPU share)."""
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
     try:
         with open("/sys/fs/cgroup/cpu.max") as f:
             q, per = f.read().split()[:2]
@@ -102,12 +109,13 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(size, frames, sample_steps, n_fwd, out_frames, config1=True):
+def cpu_baseline(size, frames, sample_steps, n_fwd, out_frames, config1=True, config1_steps=1):
     """The CPU oracle (oracle/, fp32 restatement of the reference) on this host's cores:
     (a) config 2, bounded sample: one of the 30 DiT blocks at the full shape + the VAE decoder on one
         latent frame, extrapolated to the clip (n_fwd forwards x 30 blocks + out_frames frames);
-    (b) config 1 (BASELINE.json configs[0]) end to end: 5 sampling steps x 2 windows of the full 30-layer
-        DiT at 256x256 clip 17 + the full VAE decode of the 21-frame video, measured, not extrapolated."""
+    (b) config 1 (BASELINE.json configs[0]): the restated pipeline with the full 30-layer DiT at 256x256
+        clip 17 (2 windows per step) + the full VAE decode of the 21-frame video; config1_steps of its 5
+        sampling steps run (5 = end to end), the others extrapolated at the measured per-step time."""
     from oracle import dit as odit
     from oracle import vae as ovae
     from stableavatar_amd import synthetic
@@ -142,14 +150,16 @@ def cpu_baseline(size, frames, sample_steps, n_fwd, out_frames, config1=True):
                      f"({t_vae_frame:.1f}s), extrapolated to {n_fwd} forwards x 30 blocks + {out_frames} frames "
                      f"= {t_clip:.0f}s per clip"}
     if config1:
-        out["config_1"] = cpu_config1(Pv)
+        out["config_1"] = cpu_config1(Pv, config1_steps)
     return out
 
 
-def cpu_config1(Pv):
-    """BASELINE config 1 end to end on the CPU oracle: the full 30-layer DiT (synthetic weights) through
-    the restated sliding-window loop (oracle/pipeline.py) + the full VAE decode; encoders excluded
-    (once per call).  Returns the measured frames/s."""
+def cpu_config1(Pv, run_steps=5):
+    """BASELINE config 1 on the CPU oracle: the full 30-layer DiT (synthetic weights) through the
+    restated sliding-window loop (oracle/pipeline.py) + the full VAE decode; encoders excluded (once
+    per call).  run_steps of the 5 sampling steps are executed (the denoise loop takes
+    the first run_steps sigmas of the 5-step schedule); the remaining steps cost the measured per-step
+    time."""
     from oracle import dit as odit
     from oracle import pipeline as opipe
     from oracle import vae as ovae
@@ -157,6 +167,7 @@ def cpu_config1(Pv):
     cfg = dict(odit.CONFIG_1_3B)
     Pd = synthetic.fill_state_dict(odit.param_shapes(cfg), 41)
     size, clip_length, steps, overlap, audio_frames = 256, 17, 5, 2, 24
+    run_steps = max(1, min(steps, run_steps))
     T = (audio_frames - 1) // 4 + 1
     lat0 = synthetic.seeded_normal((1, 16, T, size // 8, size // 8), 301)
     y = synthetic.seeded_normal((3, 20, (clip_length - 1) // 4 + 1, size // 8, size // 8), 302)
@@ -174,15 +185,19 @@ def cpu_config1(Pv):
         t0 = time.time()
         lat = opipe.denoise(dit, lat0, y, ctx, clip, audio, enc, num_inference_steps=steps, clip_length=clip_length,
                             num_frames=clip_length, height=size, width=size, overlap=overlap, text_guide_scale=3.0,
-                            audio_guide_scale=5.0)
+                            audio_guide_scale=5.0, max_steps=run_steps)
         t_denoise = time.time() - t0
+        t1 = time.time()
         video = ovae.decode(Pv, lat)
-        dt = time.time() - t0
+        t_decode = time.time() - t1
     n_out = video.shape[2]
-    return {"value": round(n_out / dt, 5), "unit": "frames/s", "seconds": round(dt, 1),
-            "denoise_s": round(t_denoise, 1), "dit_forwards": n_fwd[0], "frames": n_out,
+    total = t_denoise * steps / run_steps + t_decode
+    return {"value": round(n_out / total, 5), "unit": "frames/s", "seconds": round(total, 1),
+            "denoise_s_measured": round(t_denoise, 1), "decode_s": round(t_decode, 1), "steps_run": run_steps,
+            "dit_forwards_run": n_fwd[0], "frames": n_out,
             "workload": f"Wan-1.3B 30 layers {size}x{size}, clip {clip_length}, {audio_frames} frames of audio "
-                        f"(T_lat {T}, 2 windows/step), {steps} steps, fp32, + VAE decode"}
+                        f"(T_lat {T}, 2 windows/step), {steps} steps, fp32, + VAE decode"
+                        + ("" if run_steps == steps else f"; {run_steps} of {steps} steps run, the rest extrapolated")}
 
 
 # ------------------------------------------------------------------------------------------------ GPU workload
@@ -388,7 +403,7 @@ def run(args, world, rank, dev, work_factory=ClipWorkload):
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.size, args.frames, args.sample_steps, n_fwd, work.out_frames,
-                           config1=not args.no_cpu_config1)
+                           config1=not args.no_cpu_config1, config1_steps=args.cpu_config1_steps)
     n_win = len(work.wins)
     out = {"metric": METRIC, "value": round(value, 4), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 1), "higher_is_better": True,

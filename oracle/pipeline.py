@@ -89,6 +89,8 @@ def denoise(dit, latents, y, context, clip_ctx, audio, audio_encoder, *, num_inf
     seq_len = math.ceil((width // 8) * (height // 8) / (patch[1] * patch[2]) * tgt_f)
     wts = overlap_weights(overlap, scheme) if overlap > 0 else None
     for i, t in enumerate(timesteps):
+        if max_steps is not None and i >= max_steps:
+            break
         pred = torch.zeros_like(latents_all)
         for (s, e, pe) in window_schedule(infer_length, frames_per_batch, overlap):
             idx = [ii % latents_all.shape[2] for ii in range(s, e)]

@@ -138,7 +138,6 @@ class _Obj(types.SimpleNamespace):
 
 def gen_pipeline(P=PIPE, name="pipeline_small"):
     import time
-    from PIL import Image
     from wan.pipeline.wan_inference_long_pipeline import WanI2VTalkingInferenceLongPipeline
     from _refstub import FlowMatchEulerDiscreteScheduler
 
@@ -147,41 +146,8 @@ def gen_pipeline(P=PIPE, name="pipeline_small"):
     vae = build_ref_vae(P["vae"])
     fx = pipe_fixed_inputs(P)
 
-    class Tok:
-        def __call__(self, prompt, padding=None, max_length=None, truncation=None, add_special_tokens=None,
-                     return_tensors=None):
-            n = max_length or 8
-            lens = [P["neg_len"] if p == "" else P["pos_len"] for p in prompt]
-            ids = torch.ones(len(prompt), n, dtype=torch.long)
-            mask = torch.zeros(len(prompt), n, dtype=torch.long)
-            for i, ln in enumerate(lens):
-                mask[i, :ln] = 1
-            return types.SimpleNamespace(input_ids=ids, attention_mask=mask)
-
-        def batch_decode(self, *a, **k):
-            return []
-
-    class T5(torch.nn.Module):
-        dtype = torch.float32
-
-        def forward(self, ids, attention_mask=None):
-            ln = int(attention_mask.sum())
-            e = fx["pos_embeds"] if ln == P["pos_len"] else fx["neg_embeds"]
-            full = torch.zeros(1, ids.shape[1], e.shape[1])
-            full[0, :ln] = e
-            return (full,)
-
-    class Clip(torch.nn.Module):
-        def forward(self, imgs):
-            return fx["clip"].clone()
-
-    class Proc:
-        def __call__(self, samples, sampling_rate=None, return_tensors=None):
-            return types.SimpleNamespace(input_values=torch.as_tensor(np.asarray(samples), dtype=torch.float32)[None])
-
-    class W2V(torch.nn.Module):
-        def forward(self, x):
-            return types.SimpleNamespace(last_hidden_state=synthetic.fake_wav2vec_features(x))
+    from golden_cases import fake_encoders, ref_image
+    enc = fake_encoders(P, fx)
 
     calls = []
     orig = dit.forward
@@ -202,13 +168,9 @@ def gen_pipeline(P=PIPE, name="pipeline_small"):
         return vdec(z, return_dict)
 
     vae.decode = tdec
-    img = Image.fromarray((np.random.default_rng(1).random((48, 40, 3)) * 255).astype(np.uint8))
-    path = "/tmp/_sa_golden_ref.png"
-    img.save(path)
-    pipe = WanI2VTalkingInferenceLongPipeline(tokenizer=Tok(), text_encoder=T5(), vae=vae, transformer=dit,
-                                              clip_image_encoder=Clip(),
-                                              scheduler=FlowMatchEulerDiscreteScheduler(1000, shift=5.0),
-                                              wav2vec_processor=Proc(), wav2vec=W2V())
+    path = ref_image()
+    pipe = WanI2VTalkingInferenceLongPipeline(vae=vae, transformer=dit,
+                                              scheduler=FlowMatchEulerDiscreteScheduler(1000, shift=5.0), **enc)
     video = pipe("pos prompt", negative_prompt="", num_frames=P["clip_length"], height=P["height"],
                  width=P["width"], guidance_scale=6.0, num_inference_steps=P["steps"], latents=fx["latents"],
                  text_guide_scale=P["text_guide"], audio_guide_scale=P["audio_guide"],
@@ -235,6 +197,29 @@ def gen_pipeline_c1():
     256x256, clip 17, 5 steps, 2 windows per step (golden_cases.PIPE_C1)."""
     from golden_cases import PIPE_C1
     gen_pipeline(PIPE_C1, "pipeline_c1")
+
+
+def gen_keys():
+    """state_dict key -> shape of the reference modules the checkpoint loaders fill: the 1.3B DiT
+    (WanTransformer3DFantasyModel at the wan_civitai.yaml / Wan2.1-1.3B dims), the full VAE
+    (AutoencoderKLWan, keys as in Wan2.1_VAE.pth, i.e. without the "model." prefix its loader adds)."""
+    import json
+    from golden_cases import DIT_FULL
+    from wan.models.wan_fantasy_transformer3d_1B import WanTransformer3DFantasyModel
+    from wan.models.wan_vae import AutoencoderKLWan
+    cfg = DIT_FULL
+    with torch.device("meta"):
+        m = WanTransformer3DFantasyModel(model_type="i2v", patch_size=(1, 2, 2), text_len=cfg["text_len"],
+                                         in_dim=cfg["in_dim"], dim=cfg["dim"], ffn_dim=cfg["ffn_dim"],
+                                         freq_dim=cfg["freq_dim"], text_dim=cfg["text_dim"], out_dim=cfg["out_dim"],
+                                         num_heads=cfg["num_heads"], num_layers=cfg["num_layers"], qk_norm=True,
+                                         cross_attn_norm=True, eps=1e-6)
+        v = AutoencoderKLWan()
+    out = {"dit_1_3b": {k: list(t.shape) for k, t in m.state_dict().items()},
+           "vae": {k[len("model."):]: list(t.shape) for k, t in v.state_dict().items()}}
+    with open(os.path.join(HERE, "ref_keys.json"), "w") as f:
+        json.dump(out, f, indent=0, sort_keys=True)
+    print("keys", len(out["dit_1_3b"]), len(out["vae"]))
 
 
 def gen_tables():

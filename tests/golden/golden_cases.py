@@ -1,7 +1,9 @@
 """Shared definitions of the golden cases: configs + seeded input builders.  Used by
 gen_golden.py (with the reference, here only) and by the tests (oracle / HIP path)."""
 import math
+import types
 
+import numpy as np
 import torch
 
 from stableavatar_amd import synthetic
@@ -83,3 +85,55 @@ def pipe_fixed_inputs(P):
 TEACACHE = {"identity_thr1.0": ([1.0, 0.0], 1.0), "identity_thr2.5": ([1.0, 0.0], 2.5),
             "wan13b_thr0.1": (None, 0.1)}
 TEACACHE_STEPS = 10
+
+
+# ---- stand-ins for the once-per-call encoders the pipeline's __call__ drives (tokenizer, umT5, CLIP,
+# wav2vec2 processor + model): seeded tensors of the right shapes, shared by gen_golden.py (reference
+# pipeline) and the GPU __call__ tests (drop-in pipeline), so both see identical encoder outputs
+def fake_encoders(P, fx):
+    class Tok:
+        def __call__(self, prompt, padding=None, max_length=None, truncation=None, add_special_tokens=None,
+                     return_tensors=None):
+            n = max_length or 8
+            lens = [P["neg_len"] if p == "" else P["pos_len"] for p in prompt]
+            ids = torch.ones(len(prompt), n, dtype=torch.long)
+            mask = torch.zeros(len(prompt), n, dtype=torch.long)
+            for i, ln in enumerate(lens):
+                mask[i, :ln] = 1
+            return types.SimpleNamespace(input_ids=ids, attention_mask=mask)
+
+        def batch_decode(self, *a, **k):
+            return []
+
+    class T5(torch.nn.Module):
+        dtype = torch.float32
+
+        def forward(self, ids, attention_mask=None):
+            ln = int(attention_mask.sum())
+            e = fx["pos_embeds"] if ln == P["pos_len"] else fx["neg_embeds"]
+            full = torch.zeros(1, ids.shape[1], e.shape[1], device=ids.device)
+            full[0, :ln] = e.to(ids.device)
+            return (full,)
+
+    class Clip(torch.nn.Module):
+        def forward(self, imgs):
+            return fx["clip"].clone().to(imgs[0].device)
+
+    class Proc:
+        def __call__(self, samples, sampling_rate=None, return_tensors=None):
+            return types.SimpleNamespace(input_values=torch.as_tensor(np.asarray(samples), dtype=torch.float32)[None])
+
+    class W2V(torch.nn.Module):
+        def forward(self, x):
+            return types.SimpleNamespace(last_hidden_state=synthetic.fake_wav2vec_features(x))
+
+    return dict(tokenizer=Tok(), text_encoder=T5(), clip_image_encoder=Clip(), wav2vec_processor=Proc(),
+                wav2vec=W2V())
+
+
+def ref_image(path="/tmp/_sa_golden_ref.png"):
+    """the reference frame of the pipeline goldens (48x40 RGB noise, resized by the pipeline)"""
+    from PIL import Image
+    img = Image.fromarray((np.random.default_rng(1).random((48, 40, 3)) * 255).astype(np.uint8))
+    img.save(path)
+    return path
