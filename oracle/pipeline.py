@@ -75,7 +75,7 @@ def audio_window(index_start, index_end, infer_length, audio_token_per_frame, ma
 
 def denoise(dit, latents, y, context, clip_ctx, audio, audio_encoder, *, num_inference_steps, clip_length,
             num_frames, height, width, overlap, text_guide_scale, audio_guide_scale, sr=16000, fps=25,
-            scheme="uniform", shift=5.0, patch=(1, 2, 2)):
+            scheme="uniform", shift=5.0, patch=(1, 2, 2), max_steps=None):
     """Restated loop of pipeline:703-790.  `dit(x, t, context, seq_len, y, clip_fea, vocal, n)` is the
     denoiser; `audio_encoder(samples [n]) -> [1, tokens, 768]`.  Returns latents_all (fp32 holding
     bf16-rounded values like the reference, :771,:776)."""

@@ -6,9 +6,9 @@ mkdir -p gpurun_out
 tag=${1:-x}
 kexpr=${2:-}
 if [ -n "$kexpr" ]; then
-  scripts/gpustep.sh 1500 gpurun_out/t_$tag.log python -u -m pytest tests -m gpu -v --maxfail 3 --timeout 600 --timeout-method thread -k "$kexpr"
+  scripts/gpustep.sh 1500 gpurun_out/t_$tag.log python -u -m pytest tests -m gpu -v -rP --maxfail 3 --timeout 600 --timeout-method thread -k "$kexpr"
 else
-  scripts/gpustep.sh 1500 gpurun_out/t_$tag.log python -u -m pytest tests -m gpu -v --maxfail 3 --timeout 600 --timeout-method thread
+  scripts/gpustep.sh 1500 gpurun_out/t_$tag.log python -u -m pytest tests -m gpu -v -rP --maxfail 3 --timeout 600 --timeout-method thread
 fi
 rc=$?; echo "tests rc=$rc"; tail -5 gpurun_out/t_$tag.log; [ $rc -eq 99 ] && exit $rc
 scripts/gpustep.sh 900 gpurun_out/bench_$tag.log python -u bench.py; rc2=$?; echo "bench rc=$rc2"

@@ -210,6 +210,7 @@ class WanTransformer3DFantasyModel(nn.Module):
         self._segs = _Seg()
         self._split_cache = {}
         self._events = None  # optional list to record (start, end) events around self-attention
+        self._sp_enabled = False
 
     # ------------------------------------------------------------------ loading
 
@@ -300,10 +301,12 @@ class WanTransformer3DFantasyModel(nn.Module):
         self.sp_group = group
         self.sp_world_size = dist.get_world_size(group)
         self.sp_world_rank = dist.get_rank(group)
+        self._sp_enabled = True  # the exchange path runs even at degree 1 (a self all-to-all)
 
     def disable_multi_gpus_inference(self):
         """back to single-GPU forwards (every rank its own clip)"""
         self.sp_group, self.sp_world_size, self.sp_world_rank = None, 1, 0
+        self._sp_enabled = False
 
     # ------------------------------------------------------------------ packing
 
@@ -538,6 +541,7 @@ class WanTransformer3DFantasyModel(nn.Module):
         hp, wp = Hh // 2, Ww // 2
         real = Fw * hp * wp
         NS, rank = self.sp_world_size, self.sp_world_rank
+        SP = self._sp_enabled  # sequence-parallel path (NS ranks; at NS = 1 the exchanges are self-copies)
         Lp = sp.padded_len(int(seq_len), NS)
         assert real <= Lp, "seq_len smaller than the token count"
         Lc = Lp // NS  # tokens of each CFG row held by this rank (all of them without SP)
@@ -548,12 +552,12 @@ class WanTransformer3DFantasyModel(nn.Module):
         cols = torch.empty(B, Lp, pk.kpad, device=dev, dtype=torch.bfloat16)
         ops.patch_im2col(lat, y, B, Fw, Hh, Ww, cols, pk.kpad, Lp, x_frame_offset=frame_offset,
                          x_batch_broadcast=broadcast)
-        xfull = ws.x if NS == 1 else torch.empty(B * Lp, dim, device=dev, dtype=torch.float32)
+        xfull = ws.x if not SP else torch.empty(B * Lp, dim, device=dev, dtype=torch.float32)
         call_gemm_batched(cols, pk.w_pe, pk.b_pe, xfull, B, real, Lp, dim, pk.kpad)
         if real < Lp:
             for b in range(B):
                 ops.fill_(xfull[b * Lp + real:(b + 1) * Lp], 0.0)
-        if NS > 1:
+        if SP:
             ws.x.view(B, Lc, dim).copy_(xfull.view(B, Lp, dim)[:, rank * Lc:(rank + 1) * Lc])
 
         # time embedding (fp32, 1B:986-990)
@@ -609,7 +613,7 @@ class WanTransformer3DFantasyModel(nn.Module):
             vctx = vctx.view(B * Fn * nper, dim)
 
             G = Lp // n_fr
-            if NS > 1:
+            if SP:
                 plan = sp.make_plan(NS, rank, H_)
                 exch = sp.UlyssesExchange(plan, self.sp_group)
                 Lq, hg = plan.G * Lc, plan.hg
@@ -646,7 +650,7 @@ class WanTransformer3DFantasyModel(nn.Module):
                 ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 0], scale=em[:, 1], rows_per_batch=Lc)
                 rope_kw = dict(rope=pk.rope, rows_per_batch=Lc, tok_offset=rank * Lc, grid=grid, head_dim=self.d,
                                n_frame_pairs=self.d // 2 - 2 * (self.d // 6), n_height_pairs=self.d // 6)
-                if NS > 1 and sp_rows:
+                if SP and sp_rows:
                     # Ulysses pipelined over the CFG rows: row b's Q/K/V exchange is issued right after its
                     # QKV GEMM + norm/RoPE (so it travels under rows b+1..'s GEMMs), row b's attention waits
                     # only on it, and row b's output exchange travels under the next rows' attention and
@@ -673,7 +677,7 @@ class WanTransformer3DFantasyModel(nn.Module):
                 else:
                     ops.linear(ws.mod, L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv)
                     ops.qk_rmsnorm_rope(ws.qkv, 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
-                    if NS > 1:  # Ulysses: tokens -> heads, full-sequence attention, heads -> tokens
+                    if SP:  # Ulysses: tokens -> heads, full-sequence attention, heads -> tokens
                         q_sp, kv_sp = exch.to_heads(ws.qkv, B, Lc, self.d)
                         args_ = (q_sp, kv_sp[:, :hg * self.d], kv_sp[:, hg * self.d:], o_sp, segs_self, B, Lq, hg)
                     else:
@@ -682,7 +686,7 @@ class WanTransformer3DFantasyModel(nn.Module):
                     ev0 = self._record_event()
                     ops.attention(*args_, kernel=self.attn_kernel)
                     self._record_span(ev0, rows=B, batch=B)
-                    if NS > 1:
+                    if SP:
                         exch.to_tokens(o_sp, B, Lc, self.d, ws.att)
                     ops.linear(ws.att, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2],
                                rows_per_batch=Lc)
@@ -715,7 +719,7 @@ class WanTransformer3DFantasyModel(nn.Module):
         hm = hmod[0]
         ops.layernorm_mod(x, ws.mod, self.eps, shift=hm[:, 0], scale=hm[:, 1], rows_per_batch=Lc)
         ho = ops.linear(ws.mod, pk.w_head, pk.b_head, ops.EPI_BF16)
-        if NS > 1:  # every rank gets the whole prediction (1B:1150-1152)
+        if SP:  # every rank gets the whole prediction (1B:1150-1152)
             ho = sp.gather_tokens(ho, B, Lc, NS, self.sp_group)
         if out is None:
             out = torch.empty(B, self.out_dim, Fw, Hh, Ww, device=dev, dtype=torch.bfloat16)

@@ -59,3 +59,40 @@ def test_sp2_matches_single_gpu(case, overlap):
         assert p.exitcode == 0
     for rank, err, finite in res:
         assert finite and err < 1e-3, (rank, err)
+
+
+def _rccl_worker(port, overlap, qret):
+    """RCCL (backend "nccl") process group of ONE rank with the SP path forced on: every Ulysses
+    exchange is a real async all_to_all_single on ProcessGroupNCCL's stream (a self-copy at degree 1)
+    with the deferred unpack (sp.Pending), and the head output goes through all_gather_into_tensor -
+    the code that runs over xGMI at N = 2/4/8, here on the one GPU of the box."""
+    os.environ["SA_SP_OVERLAP"] = overlap
+    import torch.distributed as dist
+    sys.path.insert(0, HERE)
+    from test_gpu_dit import make_model, run
+    from golden_cases import DIT_SMALL, dit_inputs
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda:0"))
+    try:
+        m = make_model(DIT_SMALL)
+        inp = dit_inputs(DIT_SMALL, "full")
+        single = run(m, inp)
+        m.enable_multi_gpus_inference()
+        assert dist.get_backend() == "nccl" and m._sp_enabled
+        par = run(m, inp)
+        qret.put((torch.equal(par, single), ((par - single).norm() / single.norm()).item()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("overlap", ["0", "2"], ids=["batched", "per_row_async"])
+def test_sp_rccl_path_degree1(overlap):
+    ctx = mp.get_context("spawn")
+    qret = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), overlap, qret))
+    p.start()
+    same, err = qret.get(timeout=300)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert same, err
