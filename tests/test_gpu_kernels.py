@@ -355,3 +355,25 @@ def test_flow_step_blend():
     x[:, :, :ov] = x[:, :, :ov] * wb + pred0[:, :, start:start + ov].float() * (1 - wb)
     assert rel(pred[:, :, start:start + Fw], x) < 1e-2
     assert torch.equal(pred[:, :, :start], pred0[:, :, :start])
+
+
+@pytest.mark.parametrize("B,Lq,Lk,N,D", [(2, 300, 300, 3, 128), (1, 1024, 257, 12, 128), (3, 40, 17, 8, 192),
+                                         (2, 64, 100, 4, 64)])
+def test_attention_op_seam_drop_in(B, Lq, Lk, N, D):
+    """stableavatar_amd.attention.attention == the reference's SDPA branch (1B:158-207): q/k/v
+    [B, L, N, D] bf16, scale 1/sqrt(D) whatever softmax_scale says, q_lens/k_lens only warn."""
+    import warnings
+    from stableavatar_amd.attention import attention
+    q = torch.randn(B, Lq, N, D, device=dev).bfloat16()
+    k = torch.randn(B, Lk, N, D, device=dev).bfloat16()
+    v = torch.randn(B, Lk, N, D, device=dev).bfloat16()
+    ref = torch.nn.functional.scaled_dot_product_attention(q.float().transpose(1, 2), k.float().transpose(1, 2),
+                                                           v.float().transpose(1, 2)).transpose(1, 2)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        out = attention(q, k, v, q_lens=torch.full((B,), Lq), k_lens=None, softmax_scale=0.5)
+    assert any("Padding mask" in str(x.message) for x in w)
+    assert out.shape == (B, Lq, N, D) and out.dtype == torch.bfloat16
+    assert rel(out, ref) < 1e-2
+    with pytest.raises(NotImplementedError):
+        attention(q, k, v, causal=True)
