@@ -171,6 +171,34 @@ int sa_softmax_rows(const float* s, int64_t ld_s, void* p, int64_t ld_p, int64_t
 int sa_transpose_bf16(const void* in, int64_t ld_in, int64_t stride_in, void* out, int64_t ld_out,
                       int64_t stride_out, int rows, int cols, int batch, void* stream);
 
+/* ---- once-per-call encoders: umT5 (wan/models/wan_text_encoder.py) and the
+ * CLIP ViT-H/14 visual tower (wan/models/wan_image_encoder.py); their GEMMs are sa_gemm_bf16(_ex) ---- */
+
+/* T5LayerNorm: y(bf16) = bf16(w) * bf16(x * rsqrt(mean(x^2) + eps)); x f32 (in_f32 != 0) or bf16 rows. */
+int sa_t5_rmsnorm(const void* x, int64_t ldx, int in_f32, void* y, int64_t ldy, const float* weight, int M, int C,
+                  float eps, void* stream);
+
+/* T5Attention softmax: score rows r = (b*heads + h)*rows_per_head + i of s (fp32, unscaled QK^T) get
+ * bf16(bf16(s) + bias) with bias = emb[bucket[i][j]][h] (bf16 [num_buckets][heads] relative-position
+ * embedding; bucket int32 [rows_per_head][n]; both null = no bias) or finfo(bf16).min where
+ * key_mask[b][j] == 0 (int32, null = no mask); fp32 softmax over j < n (<= 2048) -> bf16 p. */
+int sa_t5_softmax_bias(const float* s, int64_t ld_s, void* p, int64_t ld_p, int batch, int heads, int rows_per_head,
+                       int n, const int32_t* bucket, const void* emb, const int32_t* key_mask, void* stream);
+
+/* T5FeedForward gate: out[m][c] = bf16(fc1 * GELU(gate)) with in = [gate | fc1] bf16 [M][2N] and the
+ * reference GELU's per-op bf16 rounding. */
+int sa_t5_geglu(const void* in, int64_t ld_in, void* out, int64_t ld_out, int64_t M, int N, void* stream);
+
+/* CLIPModel.forward preprocessing: bicubic (a = -0.75, align_corners False) resize of fp32 planes
+ * [C][H][W] in [-1, 1] to [C][S][S], then (x*0.5 + 0.5 - mean[c]) / std[c]. */
+int sa_clip_preprocess(const float* in, int C, int H, int W, float* out, int S, const float* mean, const float* stdv,
+                       void* stream);
+
+/* Conv2d(C, dim, k = s = P) im2col: fp32 [C][S][S] -> bf16 [1 + (S/P)^2][Kpad], row 0 (class token) zero. */
+int sa_clip_patch_im2col(const float* img, int C, int S, int P, void* cols, int Kpad, void* stream);
+
+int sa_cast_bf16_f32(const void* in, float* out, int64_t n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -40,6 +40,12 @@ SIGNATURES = {
     "sa_vae_latent_out": "piilpppp",
     "sa_softmax_rows": "plpllifp",
     "sa_transpose_bf16": "pllplliiip",
+    "sa_t5_rmsnorm": "pliplpiifp",
+    "sa_t5_softmax_bias": "plpliiiipppp",
+    "sa_t5_geglu": "plpllip",
+    "sa_clip_preprocess": "piiipippp",
+    "sa_clip_patch_im2col": "piiipip",
+    "sa_cast_bf16_f32": "pplp",
 }
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int32, "l": ctypes.c_int64, "f": ctypes.c_float}
 

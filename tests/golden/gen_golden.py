@@ -215,11 +215,61 @@ def gen_keys():
                                          num_heads=cfg["num_heads"], num_layers=cfg["num_layers"], qk_norm=True,
                                          cross_attn_norm=True, eps=1e-6)
         v = AutoencoderKLWan()
+    from golden_cases import CLIP_SMALL, T5_SMALL
+    from wan.models.wan_text_encoder import WanT5EncoderModel
+    with torch.device("meta"):
+        t5 = WanT5EncoderModel(vocab=256384, dim=4096, dim_attn=4096, dim_ffn=10240, num_heads=64, num_layers=24,
+                               num_buckets=32, shared_pos=False, dropout=0.0)  # wan_civitai.yaml:14-26
+    clip = build_ref_clip_visual(dict(CLIP_SMALL, dim=1280, num_heads=16, num_layers=32))  # ViT-H/14
     out = {"dit_1_3b": {k: list(t.shape) for k, t in m.state_dict().items()},
-           "vae": {k[len("model."):]: list(t.shape) for k, t in v.state_dict().items()}}
+           "vae": {k[len("model."):]: list(t.shape) for k, t in v.state_dict().items()},
+           "umt5_xxl": {k: list(t.shape) for k, t in t5.state_dict().items()},
+           "clip_visual_vit_h14": {"model.visual." + k: list(t.shape) for k, t in clip.state_dict().items()}}
     with open(os.path.join(HERE, "ref_keys.json"), "w") as f:
         json.dump(out, f, indent=0, sort_keys=True)
     print("keys", len(out["dit_1_3b"]), len(out["vae"]))
+
+
+def build_ref_t5(cfg):
+    from wan.models.wan_text_encoder import WanT5EncoderModel
+    m = WanT5EncoderModel(vocab=cfg["vocab"], dim=cfg["dim"], dim_attn=cfg["dim_attn"], dim_ffn=cfg["dim_ffn"],
+                          num_heads=cfg["num_heads"], num_layers=cfg["num_layers"], num_buckets=cfg["num_buckets"],
+                          shared_pos=cfg["shared_pos"], dropout=0.0)
+    return load_synthetic(m.eval(), cfg["seed"])
+
+
+def build_ref_clip_visual(cfg):
+    from wan.models.wan_image_encoder import VisionTransformer
+    v = VisionTransformer(image_size=cfg["image_size"], patch_size=cfg["patch"], dim=cfg["dim"], mlp_ratio=4,
+                          out_dim=1024, num_heads=cfg["num_heads"], num_layers=cfg["num_layers"], pool_type="token",
+                          pre_norm=True, post_norm=False, activation="gelu")
+    wrap = torch.nn.Module()
+    wrap.model = torch.nn.Module()
+    wrap.model.visual = v  # CLIPModel's key prefix: model.visual.*
+    load_synthetic(wrap.eval(), cfg["seed"])
+    return v
+
+
+def gen_encoders():
+    """umT5 (WanT5EncoderModel.forward) and the CLIP visual tower as CLIPModel.forward runs it
+    (F.interpolate bicubic to 224, *0.5+0.5, Normalize(mean, std) -- the torchvision Normalize is written
+    out here because torchvision is stubbed -- then visual(x, use_31_block=True)), at reduced sizes."""
+    import torch.nn.functional as F
+    from golden_cases import CLIP_SMALL, T5_SMALL, clip_image, t5_inputs
+    out = {}
+    m = build_ref_t5(T5_SMALL)
+    ids, mask = t5_inputs(T5_SMALL)
+    out["t5_out"] = m(ids, attention_mask=mask)[0].numpy()
+    v = build_ref_clip_visual(CLIP_SMALL)
+    img = clip_image(CLIP_SMALL)
+    x = F.interpolate(img.transpose(0, 1), size=(224, 224), mode="bicubic", align_corners=False)
+    x = x.mul_(0.5).add_(0.5)
+    mean = torch.tensor([0.48145466, 0.4578275, 0.40821073]).view(1, 3, 1, 1)
+    std = torch.tensor([0.26862954, 0.26130258, 0.27577711]).view(1, 3, 1, 1)
+    out["clip_pre"] = ((x - mean) / std).numpy()
+    out["clip_out"] = v((x - mean) / std, use_31_block=True).numpy()
+    print("encoders", out["t5_out"].shape, out["clip_out"].shape)
+    np.savez_compressed(os.path.join(HERE, "encoders_small.npz"), **out)
 
 
 def gen_tables():

@@ -137,3 +137,26 @@ def ref_image(path="/tmp/_sa_golden_ref.png"):
     img = Image.fromarray((np.random.default_rng(1).random((48, 40, 3)) * 255).astype(np.uint8))
     img.save(path)
     return path
+
+
+# once-per-call encoders, reduced sizes for the reference goldens: umT5 with its
+# per-block relative position embedding (shared_pos False as wan_civitai.yaml:14-26) and 64-wide heads; the
+# CLIP ViT visual tower with 80-wide heads (ViT-H/14: 1280 / 16) on a 224 image (257 tokens)
+T5_SMALL = dict(vocab=1000, dim=512, dim_attn=512, dim_ffn=1024, num_heads=8, num_layers=2, num_buckets=32,
+                shared_pos=False, seed=61, text_len=512, valid=37)
+T5_FULL_WIDTH = dict(T5_SMALL, dim=4096, dim_attn=4096, dim_ffn=10240, num_heads=64, seed=62, valid=53)
+CLIP_SMALL = dict(dim=320, num_heads=4, num_layers=3, patch=14, image_size=224, seed=63, img_hw=(512, 448))
+CLIP_FULL_WIDTH = dict(CLIP_SMALL, dim=1280, num_heads=16, seed=64)
+
+
+def t5_inputs(cfg):
+    ids = torch.from_numpy(np.random.default_rng(cfg["seed"]).integers(2, cfg["vocab"], size=(1, cfg["text_len"])))
+    mask = torch.zeros(1, cfg["text_len"], dtype=torch.long)
+    mask[:, :cfg["valid"]] = 1
+    return ids.masked_fill(mask == 0, 0), mask
+
+
+def clip_image(cfg):
+    """the reference frame as the pipeline hands it to CLIP: [C, 1, H, W] in [-1, 1]"""
+    H, W = cfg["img_hw"]
+    return synthetic.seeded_normal((3, 1, H, W), 700 + cfg["seed"], 0.5).clamp(-1, 1)

@@ -148,3 +148,37 @@ def test_riflex_rope_table_vs_reference():
     assert np.allclose(tab[:, :nf, 1].numpy(), g["riflex_frame_sin"], atol=1e-6)
     plain = rope_table(128)
     assert torch.equal(plain[:, nf:], tab[:, nf:]) and not torch.equal(plain[:, :nf], tab[:, :nf])
+
+
+def test_encoders_vs_reference():
+    """oracle/encoders.py (umT5, CLIP visual tower + CLIPModel preprocessing) vs the reference modules."""
+    from golden_cases import CLIP_SMALL, T5_SMALL, clip_image, t5_inputs
+    from oracle import encoders as oenc
+    g = G("encoders_small.npz")
+    c = T5_SMALL
+    P = synthetic.fill_state_dict(oenc.t5_param_shapes(c["vocab"], c["dim"], c["dim_attn"], c["dim_ffn"],
+                                                       c["num_heads"], c["num_layers"], c["num_buckets"],
+                                                       c["shared_pos"]), c["seed"])
+    ids, mask = t5_inputs(c)
+    with torch.no_grad():
+        y = oenc.t5_forward(P, ids, mask, c["num_heads"], c["num_layers"], c["num_buckets"], c["shared_pos"])
+    assert rel(y, g["t5_out"]) < 1e-5
+    c = CLIP_SMALL
+    P = synthetic.fill_state_dict(oenc.clip_param_shapes(c["dim"], c["num_layers"], c["patch"], c["image_size"]),
+                                  c["seed"])
+    with torch.no_grad():
+        pre = oenc.clip_preprocess(clip_image(c), c["image_size"])
+        y = oenc.clip_visual(P, pre, c["num_heads"], c["num_layers"], c["patch"])
+    assert rel(pre, g["clip_pre"]) < 1e-6
+    assert rel(y, g["clip_out"]) < 1e-5
+
+
+def test_encoder_keys_match_reference():
+    """the oracle / HIP key layouts == the reference umT5-XXL (wan_civitai.yaml dims) and ViT-H/14 state_dicts"""
+    import json
+    from oracle import encoders as oenc
+    with open(os.path.join(HERE, "golden", "ref_keys.json")) as f:
+        ref = json.load(f)
+    t5 = oenc.t5_param_shapes(256384, 4096, 4096, 10240, 64, 24, 32, shared_pos=False)
+    assert {k: list(v) for k, v in t5.items()} == ref["umt5_xxl"]
+    assert {k: list(v) for k, v in oenc.clip_param_shapes().items()} == ref["clip_visual_vit_h14"]
