@@ -256,10 +256,21 @@ def gen_encoders():
     out here because torchvision is stubbed -- then visual(x, use_31_block=True)), at reduced sizes."""
     import torch.nn.functional as F
     from golden_cases import CLIP_SMALL, T5_SMALL, clip_image, t5_inputs
+    from golden_cases import T5_FULL_WIDTH
     out = {}
     m = build_ref_t5(T5_SMALL)
     ids, mask = t5_inputs(T5_SMALL)
     out["t5_out"] = m(ids, attention_mask=mask)[0].numpy()
+    # the reference loads umT5 with torch_dtype=bf16 (inference.py:464-469): its bf16 run is the deployed
+    # semantics (unscaled T5 logits rounded to bf16 move the output by several %); both are stored
+    out["t5_out_bf16"] = m.to(torch.bfloat16)(ids, attention_mask=mask)[0].float().numpy()
+    for L, valid in ((512, T5_FULL_WIDTH["valid"]), (100, 100)):
+        c = dict(T5_FULL_WIDTH, text_len=L, valid=valid)
+        mf = build_ref_t5(c)
+        ids, mask = t5_inputs(c)
+        out[f"t5_full_L{L}"] = mf(ids, attention_mask=mask)[0][:, :valid].numpy().astype(np.float16)
+        out[f"t5_full_L{L}_bf16"] = mf.to(torch.bfloat16)(ids, attention_mask=mask)[0][:, :valid].float().numpy().astype(np.float16)
+        del mf
     v = build_ref_clip_visual(CLIP_SMALL)
     img = clip_image(CLIP_SMALL)
     x = F.interpolate(img.transpose(0, 1), size=(224, 224), mode="bicubic", align_corners=False)

@@ -48,31 +48,38 @@ def _clip(c):
 
 
 def test_t5_vs_reference_golden():
+    """The reference runs umT5 in bf16 (inference.py:464-469); T5's unscaled logits rounded to bf16 move its
+    output several % from its own fp32 run.  Contract: no further from the reference's bf16 output, nor from
+    its fp32 output, than 1.5x the reference's own bf16-vs-fp32 drift."""
     m, _, _ = _t5(T5_SMALL)
     ids, mask = t5_inputs(T5_SMALL)
     with torch.no_grad():
         out = m(ids.cuda(), attention_mask=mask.cuda())[0]
     torch.cuda.synchronize()
     assert out.dtype == torch.bfloat16 and tuple(out.shape) == (1, 512, T5_SMALL["dim"])
-    e = rel(out, G("encoders_small.npz")["t5_out"])
-    print(f"t5 small vs reference: rel-L2 {e:.2e}")
-    assert e < 2e-2, e
+    g = G("encoders_small.npz")
+    e_bf, e_32, drift = rel(out, g["t5_out_bf16"]), rel(out, g["t5_out"]), rel(g["t5_out_bf16"], g["t5_out"])
+    print(f"t5 small: vs reference bf16 {e_bf:.2e}, vs reference fp32 {e_32:.2e} (reference bf16 drift {drift:.2e})")
+    assert e_bf < 1.5 * drift and e_32 < 1.5 * drift, (e_bf, e_32, drift)
 
 
 @pytest.mark.parametrize("L,valid", [(512, 53), (100, 100)])
-def test_t5_full_width_vs_oracle(L, valid):
-    """umT5-XXL widths; L = 100 is padded to 128 keys inside (masked) and trimmed back."""
-    from oracle import encoders as oenc
+def test_t5_full_width_vs_reference(L, valid):
+    """umT5-XXL widths (2 layers, small vocabulary), the reference's bf16 and fp32 outputs on the valid
+    rows; L = 100 is padded to 128 keys inside (masked) and trimmed back."""
     c = dict(T5_FULL_WIDTH, text_len=L, valid=valid)
-    m, P, kw = _t5(c)
+    m, _, _ = _t5(c)
     ids, mask = t5_inputs(c)
     with torch.no_grad():
         out = m(ids.cuda(), attention_mask=mask.cuda())[0]
-        ref = oenc.t5_forward(P, ids, mask, kw["num_heads"], kw["num_layers"], kw["num_buckets"], kw["shared_pos"])
-    e = rel(out[0, :valid], ref[0, :valid])
-    print(f"t5 full width L={L}: rel-L2 {e:.2e}")
+    torch.cuda.synchronize()
     assert tuple(out.shape) == (1, L, 4096)
-    assert e < 2e-2, e
+    g = G("encoders_small.npz")
+    rb, r32 = g[f"t5_full_L{L}_bf16"].astype(np.float32), g[f"t5_full_L{L}"].astype(np.float32)
+    o = out[:, :valid].float()
+    e_bf, e_32, drift = rel(o, rb), rel(o, r32), rel(rb, r32)
+    print(f"t5 full width L={L}: vs reference bf16 {e_bf:.2e}, vs fp32 {e_32:.2e} (reference drift {drift:.2e})")
+    assert e_bf < 1.5 * drift and e_32 < 1.5 * drift, (e_bf, e_32, drift)
 
 
 def test_clip_vs_reference_golden():
