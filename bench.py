@@ -255,9 +255,10 @@ class ClipWorkload:
         self.layout = layout
         self.dit.disable_multi_gpus_inference()
         self.pipe.disable_window_parallel()
-        if layout == "sp":
+        if layout == "sp":  # Ulysses DiT + the VAE decode split over the ranks
             self.dit.enable_multi_gpus_inference()
-        elif layout == "window-dp":
+            self.pipe._decode_group_sync()
+        elif layout == "window-dp":  # windows + the VAE decode split over the ranks
             self.pipe.enable_window_parallel()
         shared = layout in ("sp", "window-dp")  # one clip over all ranks
         a = self.args

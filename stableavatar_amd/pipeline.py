@@ -90,11 +90,28 @@ class WanI2VTalkingInferenceLongPipeline:
         import torch.distributed as dist
         self._check_window_parallel(self.transformer)
         self.window_group = group if group is not None else dist.group.WORLD
+        if self.vae is not None and hasattr(self.vae, "enable_multi_gpus_inference"):
+            self.vae.enable_multi_gpus_inference(self.window_group)  # each rank decodes its share of frames
         return self
 
     def disable_window_parallel(self):
         self.window_group = None
+        if self.vae is not None and hasattr(self.vae, "disable_multi_gpus_inference"):
+            self.vae.disable_multi_gpus_inference()
         return self
+
+    def _decode_group_sync(self):
+        """the VAE decodes over the ranks the transformer runs sequence parallel on (the reference decodes the
+        whole clip on every rank, :793-796): same result, 1/N of the frames per rank + one gather"""
+        t = self.transformer
+        if self.vae is None or self.window_group is not None or not hasattr(self.vae, "decode_group"):
+            return
+        if getattr(t, "_sp_enabled", False):
+            if self.vae.decode_group is None:
+                import torch.distributed as dist
+                self.vae.enable_multi_gpus_inference(t.sp_group if t.sp_group is not None else dist.group.WORLD)
+        elif self.vae.decode_group is not None:
+            self.vae.disable_multi_gpus_inference()
 
     @staticmethod
     def _check_window_parallel(transformer):
@@ -286,5 +303,6 @@ class WanI2VTalkingInferenceLongPipeline:
         if output_type == "latent":
             video = lat.float()
         else:
+            self._decode_group_sync()
             video = torch.stack([self.vae.decode_clip(u.float(), post=True) for u in lat]).cpu()
         return WanI2VPipelineTalkingInferenceLongOutput(videos=video)

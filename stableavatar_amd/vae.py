@@ -163,6 +163,103 @@ def _pack_conv(w, b, cin_pad=None, cout_store=None):
                            kt=kt, kh=kh, kw=kw)
 
 
+class _SeqState:
+    """causal caches of a chunk-by-chunk decode in one process"""
+
+    def __init__(self):
+        self.d = {}
+
+    def get(self, key, like):
+        return self.d.get(key)
+
+    def put(self, key, val):
+        self.d[key] = val
+
+    def skip(self, key, like):
+        pass
+
+
+def _world(group):
+    import torch.distributed as dist
+    return dist.get_world_size(group)
+
+
+def _gloo(group):
+    import torch.distributed as dist
+    return dist.get_backend(group) == "gloo"
+
+
+class _ChainState:
+    """causal caches of the multi-rank decode: rank r's chunk takes every cache from rank r-1 and passes its
+    updated cache to rank r+1, in the (identical) order of the cache points.  RCCL: async P2P on the
+    collective stream (the receiver's stream waits, no host sync); gloo (ranks sharing one GPU in tests):
+    host-staged."""
+
+    def __init__(self, group, rank, n):
+        import torch.distributed as dist
+        self.group, self.rank, self.n = group, rank, n
+        self.prev_g = dist.get_global_rank(group, rank - 1) if rank > 0 else None
+        self.next_g = dist.get_global_rank(group, rank + 1) if rank + 1 < n else None
+        self.sends = []
+        self.local = {}
+        self.first_sub, self.last_sub = True, True
+
+    def begin(self, first_sub, last_sub):
+        """a rank decodes its run in sub-chunks: only the first takes its caches from rank r-1 and only the
+        last hands them to rank r+1; in between they stay local"""
+        self.first_sub, self.last_sub = first_sub, last_sub
+
+    def get(self, key, like):
+        import torch.distributed as dist
+        if not self.first_sub:
+            return self.local.get(key)
+        if self.prev_g is None:
+            return None
+        shape = (2,) + tuple(like.shape[1:])
+        if _gloo(self.group) and like.is_cuda:
+            h = torch.empty(shape, dtype=like.dtype)
+            dist.recv(h, self.prev_g, group=self.group)
+            return h.to(like.device)
+        t = torch.empty(shape, dtype=like.dtype, device=like.device)
+        dist.irecv(t, self.prev_g, group=self.group).wait()
+        return t
+
+    def put(self, key, val):
+        import torch.distributed as dist
+        if not self.last_sub:
+            self.local[key] = val
+            return
+        if self.next_g is None:
+            return
+        if _gloo(self.group) and val.is_cuda:
+            h = val.cpu()
+            self.sends.append((dist.isend(h, self.next_g, group=self.group), h))
+        else:
+            self.sends.append((dist.isend(val, self.next_g, group=self.group), val))
+
+    def skip(self, key, like):
+        prev = self.get(key, like)
+        if prev is None:
+            prev = torch.zeros((2,) + tuple(like.shape[1:]), device=like.device, dtype=like.dtype)
+        self.put(key, prev)
+
+    def finish(self):
+        for w, _ in self.sends:
+            w.wait()
+        self.sends = []
+
+
+def _all_gather(buf, N, group):
+    import torch.distributed as dist
+    if _gloo(group) and buf.is_cuda:
+        out = torch.empty((N,) + tuple(buf.shape), dtype=buf.dtype)
+        dist.all_gather_into_tensor(out, buf.cpu(), group=group)
+        return out.to(buf.device)
+    out = torch.empty((N,) + tuple(buf.shape), dtype=buf.dtype, device=buf.device)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    return out
+
+
 class DecoderOutput:
     def __init__(self, sample):
         self.sample = sample
@@ -216,6 +313,7 @@ class AutoencoderKLWan(nn.Module):
             mod.register_parameter(leaf, nn.Parameter(torch.empty(shp), requires_grad=False))
         self._packed = None
         self._packed_enc = None
+        self.decode_group = None  # enable_multi_gpus_inference(): decode over several ranks
 
     @property
     def dtype(self):
@@ -343,11 +441,18 @@ class AutoencoderKLWan(nn.Module):
         cache_x (wan_vae.py:27-36): the last 2 input frames seen so far, zeros before the clip."""
         if state is None:
             return None
-        prev = state.get(key)
+        prev = state.get(key, x)
         if prev is None:
             prev = torch.zeros((2,) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
-        state[key] = torch.cat([prev, x])[-2:].clone() if x.shape[0] < 2 else x[-2:].clone()
+        state.put(key, torch.cat([prev, x])[-2:].clone() if x.shape[0] < 2 else x[-2:].clone())
         return prev
+
+    @staticmethod
+    def _cache_skip(state, key, x):
+        """a cache point this chunk does not reach (the first chunk's up3d time_conv with one frame): the
+        cache stays as it was (zeros before the clip)"""
+        if state is not None:
+            state.skip(key, x)
 
     @staticmethod
     def _rms(x, gamma, silu):
@@ -398,6 +503,8 @@ class AutoencoderKLWan(nn.Module):
             u[0].copy_(x[0])
             self._conv(x[1:], T - 1, H, W, e.tc, out=u[1:], interleave=C, prev=self._cache(state, id(e), x[1:]))
             x, T = u, 1 + 2 * (T - 1)
+        elif e.kind == "up3d":
+            self._cache_skip(state, id(e), x)
         return self._conv(x, T, 2 * H, 2 * W, e.rs, upsample=True), T, 2 * H, 2 * W
 
     @staticmethod
@@ -471,15 +578,58 @@ class AutoencoderKLWan(nn.Module):
         dev = pk.mean.device
         Cz, T, H, W = z.shape
         chunk = chunk or self.decode_chunk
+        if self.decode_group is not None and _world(self.decode_group) > 1:
+            return self._decode_parallel(pk, z, post, chunk)
         if T <= chunk:
             return self._decode_chunk(pk, z, True, None, post)
         out = torch.empty(3, 1 + 4 * (T - 1), 8 * H, 8 * W, device=dev, dtype=torch.float32)
-        state = {}
+        state = _SeqState()
         for c0 in range(0, T, chunk):
             c1 = min(c0 + chunk, T)
             y = self._decode_chunk(pk, z[:, c0:c1], c0 == 0, state, post)
             o0 = 0 if c0 == 0 else 1 + 4 * (c0 - 1)
             out[:, o0:o0 + y.shape[1]].copy_(y)
+        return out
+
+    def enable_multi_gpus_inference(self, group=None):
+        """Decode over the ranks of `group` (default: the torch.distributed world): rank r decodes the r-th
+        contiguous run of latent frames, taking each causal conv's 2-frame cache from rank r-1 and handing
+        its own to rank r+1 (P2P, one send per cache point: a wavefront over the ranks), then one gather.
+        Bit-identical to the single-GPU decode (the chunked decode == whole-clip decode)."""
+        import torch.distributed as dist
+        self.decode_group = group if group is not None else dist.group.WORLD
+        return self
+
+    def disable_multi_gpus_inference(self):
+        self.decode_group = None
+        return self
+
+    def _decode_parallel(self, pk, z, post, chunk):
+        import torch.distributed as dist
+        grp = self.decode_group
+        N, r = _world(grp), dist.get_rank(grp)
+        dev = pk.mean.device
+        Cz, T, H, W = z.shape
+        n = min(N, T)
+        bounds = [round(i * T / n) for i in range(n + 1)]  # contiguous runs of latent frames
+        frames = lambda i: (1 + 4 * (bounds[1] - 1)) if i == 0 else 4 * (bounds[i + 1] - bounds[i])  # noqa: E731
+        fmax = max(frames(i) for i in range(n))
+        buf = torch.zeros(fmax, 3, 8 * H, 8 * W, device=dev, dtype=torch.float32)
+        if r < n:
+            state = _ChainState(grp, r, n)
+            o = 0
+            subs = list(range(bounds[r], bounds[r + 1], chunk))
+            for j, c0 in enumerate(subs):  # sub-chunks of <= `chunk` latent frames bound the activations
+                c1 = min(c0 + chunk, bounds[r + 1])
+                state.begin(j == 0, j == len(subs) - 1)
+                y = self._decode_chunk(pk, z[:, c0:c1], c0 == 0, state, post)  # [3, F, 8H, 8W]
+                buf[o:o + y.shape[1]].copy_(y.transpose(0, 1))
+                o += y.shape[1]
+            state.finish()
+            assert o == frames(r)
+        allb = _all_gather(buf, N, grp)  # [N, fmax, 3, 8H, 8W]
+        out = torch.cat([allb[i, :frames(i)] for i in range(n)]).transpose(0, 1).contiguous()
+        assert out.shape[1] == 1 + 4 * (T - 1)
         return out
 
     def _decode_chunk(self, pk, z, first, state, post):
