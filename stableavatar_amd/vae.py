@@ -250,14 +250,17 @@ class _ChainState:
 
 
 def _all_gather(buf, N, group):
+    """[N, *buf.shape]: every rank's buf (gathered as the concatenation along dim 0)"""
     import torch.distributed as dist
+    shape = (N * buf.shape[0],) + tuple(buf.shape[1:])
     if _gloo(group) and buf.is_cuda:
-        out = torch.empty((N,) + tuple(buf.shape), dtype=buf.dtype)
+        out = torch.empty(shape, dtype=buf.dtype)
         dist.all_gather_into_tensor(out, buf.cpu(), group=group)
-        return out.to(buf.device)
-    out = torch.empty((N,) + tuple(buf.shape), dtype=buf.dtype, device=buf.device)
-    dist.all_gather_into_tensor(out, buf, group=group)
-    return out
+        out = out.to(buf.device)
+    else:
+        out = torch.empty(shape, dtype=buf.dtype, device=buf.device)
+        dist.all_gather_into_tensor(out, buf.contiguous(), group=group)
+    return out.view((N,) + tuple(buf.shape))
 
 
 class DecoderOutput:

@@ -12,6 +12,9 @@ import torch.multiprocessing as mp
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "golden"))
 
+sys.path.insert(0, HERE)
+from mp_util import collect  # noqa: E402
+
 pytestmark = pytest.mark.gpu
 
 
@@ -53,7 +56,7 @@ def test_sp2_matches_single_gpu(case, overlap):
     procs = [ctx.Process(target=_worker, args=(r, world, port, case, overlap, qret)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [qret.get(timeout=300) for _ in range(world)]
+    res = collect(procs, qret, world)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -92,7 +95,7 @@ def test_sp_rccl_path_degree1(overlap):
     qret = ctx.Queue()
     p = ctx.Process(target=_rccl_worker, args=(_free_port(), overlap, qret))
     p.start()
-    same, err = qret.get(timeout=300)
+    same, err = collect([p], qret, 1)[0]
     p.join(timeout=120)
     assert p.exitcode == 0
     assert same, err

@@ -14,6 +14,9 @@ import torch.multiprocessing as mp
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "golden"))
 
+sys.path.insert(0, HERE)
+from mp_util import collect  # noqa: E402
+
 pytestmark = pytest.mark.gpu
 
 
@@ -86,7 +89,7 @@ def test_window_parallel_bit_exact():
     procs = [ctx.Process(target=_worker, args=(r, world, port, qret)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [qret.get(timeout=300) for _ in range(world)]
+    res = collect(procs, qret, world)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
