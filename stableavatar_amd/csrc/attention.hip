@@ -754,272 +754,7 @@ __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) {
   }
 }
 
-// ---- v7: v6's block math with the two wave groups of each SIMD staggered by half a block (FA3-style
-// ping-pong between the waves sharing a SIMD, MI355X_MICROARCH.md "Two waves per SIMD" item 9).  In v6
-// all 8 waves pass each block barrier together, so each SIMD's two waves run their QK^T MFMAs, their
-// softmax VALU and their PV MFMAs at the same time and the matrix pipe idles through the softmax.  Here
-// both groups run the same per-block instruction stream QK^T(j) -> softmax(j) -> PV(j), but waves 0-3
-// (group A) take the block barrier before QK^T(j) while waves 4-7 (group B, their SIMD partners) take it
-// between softmax(j) and PV(j): B's segment between barriers is PV(j-1) QK^T(j) softmax(j), so A's softmax
-// meets B's QK^T MFMAs and B's softmax meets A's PV MFMAs.  Each wave issues its DMA pieces of block j+1
-// right after barrier #j; B reads V(j) after barrier #(j+1), so the V ring is 3 stages deep (K too, for
-// static slot indices: K ring [0, 48K), V ring [48K, 96K), every ds_read offset inside the 16-bit
-// immediate).  Rescale safety (T13): PV(j-1) is always complete before softmax(j) decides a rescale.
-constexpr int V7_STAGE = 16384;       // one 64-key K (or V) tile
-constexpr int V7_V0 = 3 * V7_STAGE;   // V ring base
-constexpr int V7_LDS = 6 * V7_STAGE;  // 96 KB
-
-template <int S, int KT>
-__device__ __forceinline__ void v7_read_k(u32x4* f, const uint32_t* ka) {
-  constexpr int base = S * V7_STAGE + KT * 4096;
-  ds_b128<base>(f[0], ka[0]);
-  ds_b128<base>(f[1], ka[1]);
-  ds_b128<base>(f[2], ka[2]);
-  ds_b128<base>(f[3], ka[3]);
-}
-// V^T fragments of key chunk C for d tiles DT0..DT0+3 of stage S (va already points into the V ring)
-template <int S, int C, int DT0>
-__device__ __forceinline__ void v7_read_v(u32x2* f, const uint32_t* va) {
-  constexpr int base = S * V7_STAGE + C * 8192;
-  ds_tr64<base>(f[0], va[DT0 + 0]); ds_tr64<base + 4096>(f[1], va[DT0 + 0]);
-  ds_tr64<base>(f[2], va[DT0 + 1]); ds_tr64<base + 4096>(f[3], va[DT0 + 1]);
-  ds_tr64<base>(f[4], va[DT0 + 2]); ds_tr64<base + 4096>(f[5], va[DT0 + 2]);
-  ds_tr64<base>(f[6], va[DT0 + 3]); ds_tr64<base + 4096>(f[7], va[DT0 + 3]);
-}
-
-// one block kb in stage S, with the group-dependent barrier (see above); the caller's `stage(kb, slot)`
-// issues this wave's DMA pieces
-template <int S, class Stage>
-__device__ __forceinline__ void v7_block(V6State& st, const bf16x8 (&qf)[2][4], const uint32_t* ka,
-                                         const uint32_t* va, int kb, int nkb, int kv_len, int g, bool grpB,
-                                         Stage& stage) {
-  if (!grpB) {
-    if (kb > 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-    if (kb + 1 < nkb) stage(kb + 1, (S + 1) % 3);
-  }
-  f32x4 Sa[4][2];
-#pragma unroll
-  for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) Sa[kt][qt] = (f32x4){st.negm[qt], st.negm[qt], st.negm[qt], st.negm[qt]};
-  u32x4 k0[4], k1[4];
-  v7_read_k<S, 0>(k0, ka);
-  v7_read_k<S, 1>(k1, ka);
-  wait_k4<4>(k0);
-  v6_mma_k(Sa, 0, k0, qf);
-  v7_read_k<S, 2>(k0, ka);
-  wait_k4<4>(k1);
-  v6_mma_k(Sa, 1, k1, qf);
-  v7_read_k<S, 3>(k1, ka);
-  wait_k4<4>(k0);
-  v6_mma_k(Sa, 2, k0, qf);
-  wait_k4<0>(k1);
-  v6_mma_k(Sa, 3, k1, qf);
-  u32x2 v0[8], v1[8];
-  v7_read_v<S, 0, 0>(v0, va);  // first V^T fragments under the softmax
-  v7_read_v<S, 0, 4>(v1, va);
-  if (kb * KVB + KVB > kv_len) {
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (kb * KVB + kt * 16 + 4 * g + i >= kv_len) { Sa[kt][0][i] = -INFINITY; Sa[kt][1][i] = -INFINITY; }
-  }
-  float mx[2];
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    float m = Sa[0][qt][0];
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) m = fmaxf(m, Sa[kt][qt][i]);
-    mx[qt] = max16x2(m);
-  }
-  const bool first = kb == 0;
-  if (first || !__all(mx[0] <= RESCALE_THR && mx[1] <= RESCALE_THR)) {  // wave-uniform
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const float delta = first ? mx[qt] : fmaxf(mx[qt], 0.f);
-      const float alpha = __builtin_amdgcn_exp2f(-delta);
-      st.L[qt] *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) st.O[dt][qt][i] *= alpha;
-      st.negm[qt] -= delta;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) Sa[kt][qt][i] -= delta;
-    }
-  }
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) Sa[kt][qt][i] = __builtin_amdgcn_exp2f(Sa[kt][qt][i]);
-  bf16x8 pb[2][2];
-#pragma unroll
-  for (int c = 0; c < 2; ++c)
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        pb[c][qt][j] = f2bf(Sa[2 * c][qt][j]);
-        pb[c][qt][4 + j] = f2bf(Sa[2 * c + 1][qt][j]);
-      }
-  if (grpB) {  // B's barrier sits here: its segment continues with PV(kb) and the next block's QK^T
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kb + 2 < nkb) stage(kb + 2, (S + 2) % 3);
-  }
-  bf16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    st.L[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[c][0], st.L[0], 0, 0, 0);
-    st.L[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[c][1], st.L[1], 0, 0, 0);
-    if (c == 0) {
-      wait_v<8>(v0);
-      v6_mma_v(st.O, 0, v0, pb[0]);
-      v7_read_v<S, 1, 0>(v0, va);
-      wait_v<8>(v1);
-      v6_mma_v(st.O, 4, v1, pb[0]);
-      v7_read_v<S, 1, 4>(v1, va);
-    } else {
-      wait_v<8>(v0);
-      v6_mma_v(st.O, 0, v0, pb[1]);
-      wait_v<0>(v1);
-      v6_mma_v(st.O, 4, v1, pb[1]);
-    }
-  }
-}
-
-__global__ __launch_bounds__(512) void attn_fwd_v7_kernel(AttnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nx = gridDim.x, ny = gridDim.y;
-  const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
-  const int qb = flat % nx, h = (flat / nx) % ny, seg = flat / (nx * ny);
-  const int* sg = a.segs + seg * 4;
-  const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
-  if (qb * QB >= q_len || kv_len <= 0) return;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, r16 = lane & 15;
-  const bool grpB = wave >= 4;  // waves w and w+4 share a SIMD
-
-  bf16x8 qf[2][4];
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int qc = min(qb * QB + wave * 32 + qt * 16 + r16, q_len - 1);
-    const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * g;
-#pragma unroll
-    for (int dc = 0; dc < 4; ++dc) {
-      qf[qt][dc] = *(const bf16x8*)(qp + 32 * dc);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[qt][dc][j] = f2bf(bf2f(qf[qt][dc][j]) * a.c);
-    }
-  }
-
-  // K/V pieces by buffer_load...lds from the segment's rows: SGPR descriptors over exactly kv_len rows (rows
-  // past the segment read as zeros, and are masked), per-lane 32-bit row/chunk offsets, the block in soffset
-  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.k + (long)kv_row0 * a.ks + h * D), (short)0, (int)(((long)kv_len - 1) * a.ks * 2 + 256), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.v + (long)kv_row0 * a.vs + h * D), (short)0, (int)(((long)kv_len - 1) * a.vs * 2 + 256), 0x00020000);
-  int koff[2], voff[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int srow = (wave * 2 + i) * 4 + (lane >> 4);
-    koff[i] = srow * (int)a.ks * 2 + ((r16 ^ (srow & 15)) << 4);
-    voff[i] = srow * (int)a.vs * 2 + ((r16 ^ ((srow & 7) << 1)) << 4);
-  }
-  const uint32_t lds_dma = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + wave * 2048);
-  auto stage = [&](int kb, int buf) {
-    const int ks_off = kb * KVB * (int)a.ks * 2, vs_off = kb * KVB * (int)a.vs * 2;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, LDS_PTR((uintptr_t)(lds_dma + buf * V7_STAGE + i * 1024)), 16,
-                                               koff[i], ks_off, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, LDS_PTR((uintptr_t)(lds_dma + V7_V0 + buf * V7_STAGE + i * 1024)),
-                                               16, voff[i], vs_off, 0, 0);
-    }
-  };
-
-  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
-  uint32_t ka[4], va[8];
-#pragma unroll
-  for (int dc = 0; dc < 4; ++dc) ka[dc] = lds0 + r16 * 256 + (((dc * 4 + g) ^ r16) << 4);
-  {
-    const int q = r16 >> 2, p = r16 & 3;
-    const int row = 4 * g + q;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      const int ch = 2 * dt + (p >> 1);
-      va[dt] = lds0 + V7_V0 + row * 256 + ((ch ^ ((row & 7) << 1)) << 4) + 8 * (p & 1);
-    }
-  }
-
-  V6State st;
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) st.O[dt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  st.L[0] = st.L[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  st.negm[0] = st.negm[1] = 0.f;
-
-  const int nkb = (kv_len + KVB - 1) / KVB;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // barrier #0: block 0 landed
-  if (grpB) {
-    __builtin_amdgcn_s_setprio(1);
-    if (nkb > 1) stage(1, 1);  // B's pieces of block 1 (A issues its own in block 0)
-  }
-  for (int kb = 0; kb < nkb; kb += 3) {
-    v7_block<0>(st, qf, ka, va, kb, nkb, kv_len, g, grpB, stage);
-    if (kb + 1 >= nkb) break;
-    v7_block<1>(st, qf, ka, va, kb + 1, nkb, kv_len, g, grpB, stage);
-    if (kb + 2 >= nkb) break;
-    v7_block<2>(st, qf, ka, va, kb + 2, nkb, kv_len, g, grpB, stage);
-  }
-  if (!grpB) __syncthreads();  // balance B's extra barrier (B passed one per block after #0)
-
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const float inv = 1.0f / st.L[qt][0];
-    const int qi = qb * QB + wave * 32 + qt * 16 + r16;
-    bf16* op = a.o + (long)(q_row0 + min(qi, q_len - 1)) * a.os + h * D + 4 * (g & ~1) + 16 * (g & 1);
-#pragma unroll
-    for (int dt = 0; dt < 8; dt += 2) {
-      const f32x4& A = st.O[dt][qt];
-      const f32x4& B = st.O[dt + 1][qt];
-      const bf16x4 pa = {f2bf(A[0] * inv), f2bf(A[1] * inv), f2bf(A[2] * inv), f2bf(A[3] * inv)};
-      const bf16x4 pq = {f2bf(B[0] * inv), f2bf(B[1] * inv), f2bf(B[2] * inv), f2bf(B[3] * inv)};
-      const u32x2 ga = __builtin_bit_cast(u32x2, pa), gb = __builtin_bit_cast(u32x2, pq);
-      const auto rx = __builtin_amdgcn_permlane16_swap(ga[0], gb[0], false, false);
-      const auto ry = __builtin_amdgcn_permlane16_swap(ga[1], gb[1], false, false);
-      u32x4 out = {rx[0], ry[0], rx[1], ry[1]};
-      bf16* p = op + dt * 16;
-      if (a.accumulate) {
-        const bf16x8 ov = *(const bf16x8*)p;
-        bf16x8 nv = __builtin_bit_cast(bf16x8, out);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) nv[j] = f2bf(bf2f(ov[j]) + bf2f(nv[j]));
-        out = __builtin_bit_cast(u32x4, nv);
-      }
-      if (qi < q_len) *(u32x4*)p = out;
-    }
-  }
-}
-
-// kernel: 0 = auto, 1 = attn_fwd_v6_kernel (8 waves x 32 queries, mfma_f32_16x16x32_bf16), 2 = attn_fwd_v7_kernel
-// (v6 with the two wave groups of each SIMD staggered by half a block, 3-stage K/V ring)
+// kernel: 0 = auto, 1 = attn_fwd_v6_kernel (8 waves x 32 queries, mfma_f32_16x16x32_bf16)
 extern "C" int sa_attn_fwd_ex(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
                               int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride,
                               int64_t v_stride, int64_t o_stride, float scale, int accumulate, int kernel,
@@ -1028,20 +763,16 @@ extern "C" int sa_attn_fwd_ex(const void* q, const void* k, const void* v, void*
   if (head_dim != D) return SA_ERR_ARG;
   if ((q_stride | k_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
   if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)o)) & 15) return SA_ERR_ARG;
-  if (kernel < 0 || kernel > 2) return SA_ERR_ARG;
+  if (kernel < 0 || kernel > 1) return SA_ERR_ARG;
   static const bool attr = [] {  // one-time, thread-safe
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_v7_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, V7_LDS);
     return true;
   }();
   (void)attr;
   AttnArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, segs,
              q_stride, k_stride, v_stride, o_stride, scale * 1.4426950408889634f, accumulate};
   dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
-  if (kernel == 2)
-    hipLaunchKernelGGL(attn_fwd_v7_kernel, grid, dim3(512), V7_LDS, (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL(attn_fwd_v6_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(attn_fwd_v6_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
   SA_LAUNCH_CHECK();
   return SA_OK;
 }
