@@ -109,7 +109,8 @@ def _ref_attn(q, k, v, scale):
 
 
 @pytest.mark.parametrize("Lq,Lk", [(300, 300), (512, 257), (1024, 17), (64, 512)])
-def test_attention_segments(Lq, Lk):
+@pytest.mark.parametrize("kernel", [1, 2], ids=["v6", "v6opt"])
+def test_attention_segments(Lq, Lk, kernel):
     from stableavatar_amd import ops
     B, H, D = 2, 3, 128
     q = torch.randn(B * Lq, H * D + 64, device=dev).bfloat16()[:, :H * D]  # strided rows
@@ -117,7 +118,7 @@ def test_attention_segments(Lq, Lk):
     v = torch.randn(B * Lk, H * D, device=dev).bfloat16()
     o = torch.empty(B * Lq, H * D, device=dev, dtype=torch.bfloat16)
     segs = torch.tensor([[b * Lq, Lq, b * Lk, Lk] for b in range(B)], dtype=torch.int32, device=dev)
-    ops.attention(q, k, v, o, segs, B, Lq, H)
+    ops.attention(q, k, v, o, segs, B, Lq, H, kernel=kernel)
     for b in range(B):
         for h in range(H):
             ref = _ref_attn(q[b * Lq:(b + 1) * Lq, h * D:(h + 1) * D], k[b * Lk:(b + 1) * Lk, h * D:(h + 1) * D],
@@ -125,11 +126,12 @@ def test_attention_segments(Lq, Lk):
             assert rel(o[b * Lq:(b + 1) * Lq, h * D:(h + 1) * D], ref) < 1e-2, (b, h)
     # accumulate mode adds onto the existing output
     o2 = o.clone()
-    ops.attention(q, k, v, o2, segs, B, Lq, H, accumulate=True)
+    ops.attention(q, k, v, o2, segs, B, Lq, H, accumulate=True, kernel=kernel)
     assert rel(o2, 2 * o.float()) < 1e-2
 
 
-def test_attention_vocal_grouping():
+@pytest.mark.parametrize("kernel", [1, 2], ids=["v6", "v6opt"])
+def test_attention_vocal_grouping(kernel):
     """per-frame grouping of 1B:575-586: q rows of frame f attend to that frame's 17 keys"""
     from stableavatar_amd import ops
     B, F, G, Lv, H, D = 2, 3, 64, 17, 2, 128
@@ -138,7 +140,7 @@ def test_attention_vocal_grouping():
     v = torch.randn(B * F * Lv, H * D, device=dev).bfloat16()
     o = torch.empty_like(q)
     segs = torch.tensor([[i * G, G, i * Lv, Lv] for i in range(B * F)], dtype=torch.int32, device=dev)
-    ops.attention(q, k, v, o, segs, B * F, G, H)
+    ops.attention(q, k, v, o, segs, B * F, G, H, kernel=kernel)
     for i in range(B * F):
         for h in range(H):
             sl = slice(h * D, (h + 1) * D)
@@ -146,7 +148,8 @@ def test_attention_vocal_grouping():
             assert rel(o[i * G:(i + 1) * G, sl], ref) < 1e-2
 
 
-def test_attention_spike_rescale():
+@pytest.mark.parametrize("kernel", [1, 2], ids=["v6", "v6opt"])
+def test_attention_spike_rescale(kernel):
     """force the online-softmax rescale branch: a late key with a huge score"""
     from stableavatar_amd import ops
     L, D = 512, 128
@@ -156,7 +159,7 @@ def test_attention_spike_rescale():
     v = torch.randn(L, D, device=dev).bfloat16()
     o = torch.empty_like(q)
     segs = torch.tensor([[0, L, 0, L]], dtype=torch.int32, device=dev)
-    ops.attention(q, k, v, o, segs, 1, L, 1)
+    ops.attention(q, k, v, o, segs, 1, L, 1, kernel=kernel)
     assert rel(o, _ref_attn(q, k, v, D ** -0.5)) < 1e-2
 
 
