@@ -525,7 +525,7 @@ struct V6State {
   f32x4 O[8][2];
   f32x4 L[2];     // row sums of the bf16 P (every element equal), from a ones x P^T MFMA
   float negm[2];  // -m per query tile (this lane's query)
-  f32x4 negm4[2];  // the same as the QK^T chains' initial accumulator (OPT: refreshed only on a rescale)
+  f32x4 negm4[2];  // the same as the QK^T chains' initial accumulator (refreshed only on a rescale)
 };
 
 // non-canonicalising f32 max (MFMA outputs are never signalling NaNs): fmaxf makes hipcc insert a
@@ -556,7 +556,7 @@ __device__ __forceinline__ float rowmax64(const f32x4 (&S)[4][2], int qt) {
   return vmax2(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 
-template <int BUF, bool OPT>
+template <int BUF>
 __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2][4], const uint32_t* ka,
                                               const uint32_t* va, int kb, int kv_len, int g) {
   f32x4 S[4][2];
@@ -564,7 +564,7 @@ __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2]
   for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt)
-      S[kt][qt] = OPT ? st.negm4[qt] : (f32x4){st.negm[qt], st.negm[qt], st.negm[qt], st.negm[qt]};
+      S[kt][qt] = st.negm4[qt];
   // S'^T = c K Q^T - m, K fragments two key tiles ahead
   u32x4 k0[4], k1[4];
   v6_read_k<BUF, 0>(k0, ka);
@@ -594,16 +594,7 @@ __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2]
   float mx[2];
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
-    if constexpr (OPT) {
-      mx[qt] = rowmax64(S, qt);
-    } else {
-      float m = S[0][qt][0];
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) m = fmaxf(m, S[kt][qt][i]);
-      mx[qt] = max16x2(m);  // max of c S - m over the block's 64 keys
-    }
+    mx[qt] = rowmax64(S, qt);  // max of c S - m over the block's 64 keys
   }
   const bool first = kb == 0;
   if (first || !__all(mx[0] <= RESCALE_THR && mx[1] <= RESCALE_THR)) {  // wave-uniform
@@ -664,7 +655,6 @@ __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2]
   }
 }
 
-template <bool OPT>
 __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nx = gridDim.x, ny = gridDim.y;
@@ -694,60 +684,29 @@ __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) {
   // staging: each wave moves 2 x 1-KB pieces (4 rows each) of K and of V per block; lane -> row
   // (lane / 16), stored position lane % 16 holding source chunk (lane % 16) ^ swizzle(row)
   // K/V pieces: each wave moves 2 x 1-KB pieces (4 rows each) of K and of V per block; lane -> row
-  // (lane / 16), stored position lane % 16 holding source chunk (lane % 16) ^ swizzle(row).  OPT: by
+  // (lane / 16), stored position lane % 16 holding source chunk (lane % 16) ^ swizzle(row).  By
   // buffer_load...lds from SGPR descriptors over exactly the segment's kv_len rows (rows past it read as
   // zeros and are masked), per-lane 32-bit offsets and the block in soffset: no 64-bit address VALU
-  const bf16* kbase = a.k + h * D;
-  const bf16* vbase = a.v + h * D;
-  int srow[2];
-  const bf16 *kp[2], *vp[2];
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.k + (long)kv_row0 * a.ks + h * D), (short)0, (int)(((long)kv_len - 1) * a.ks * 2 + 256), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.v + (long)kv_row0 * a.vs + h * D), (short)0, (int)(((long)kv_len - 1) * a.vs * 2 + 256), 0x00020000);
   int koff[2], voff[2];
-  __amdgpu_buffer_rsrc_t rk, rv;
-  if constexpr (OPT) {
-    rk = __builtin_amdgcn_make_buffer_rsrc((void*)(a.k + (long)kv_row0 * a.ks + h * D), (short)0,
-                                           (int)(((long)kv_len - 1) * a.ks * 2 + 256), 0x00020000);
-    rv = __builtin_amdgcn_make_buffer_rsrc((void*)(a.v + (long)kv_row0 * a.vs + h * D), (short)0,
-                                           (int)(((long)kv_len - 1) * a.vs * 2 + 256), 0x00020000);
-  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    srow[i] = (wave * 2 + i) * 4 + (lane >> 4);
-    if constexpr (OPT) {
-      koff[i] = srow[i] * (int)a.ks * 2 + ((r16 ^ (srow[i] & 15)) << 4);
-      voff[i] = srow[i] * (int)a.vs * 2 + ((r16 ^ ((srow[i] & 7) << 1)) << 4);
-    } else {
-      const long key = kv_row0 + min(srow[i], kv_len - 1);
-      kp[i] = kbase + key * a.ks + ((r16 ^ (srow[i] & 15)) * 8);
-      vp[i] = vbase + key * a.vs + ((r16 ^ ((srow[i] & 7) << 1)) * 8);
-    }
+    const int srow = (wave * 2 + i) * 4 + (lane >> 4);
+    koff[i] = srow * (int)a.ks * 2 + ((r16 ^ (srow & 15)) << 4);
+    voff[i] = srow * (int)a.vs * 2 + ((r16 ^ ((srow & 7) << 1)) << 4);
   }
   const uint32_t lds_dma = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + wave * 2048);
   auto stage = [&](int kb, int buf) {
-    if constexpr (OPT) {
-      const int ks_off = kb * KVB * (int)a.ks * 2, vs_off = kb * KVB * (int)a.vs * 2;
+    const int ks_off = kb * KVB * (int)a.ks * 2, vs_off = kb * KVB * (int)a.vs * 2;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, LDS_PTR((uintptr_t)(lds_dma + buf * STAGE_BYTES + i * 1024)), 16,
-                                                 koff[i], ks_off, 0, 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rv, LDS_PTR((uintptr_t)(lds_dma + buf * STAGE_BYTES + TILE_BYTES + i * 1024)), 16, voff[i], vs_off, 0, 0);
-      }
-    } else {
-      char* base = smem + buf * STAGE_BYTES;
-      const bool full = kb * KVB + KVB <= kv_len;  // wave-uniform
-      const long ko = (long)kb * KVB * a.ks, vo = (long)kb * KVB * a.vs;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const bf16 *ksrc = kp[i] + ko, *vsrc = vp[i] + vo;
-        if (!full) {
-          const long key = kv_row0 + min(kb * KVB + srow[i], kv_len - 1);
-          ksrc = kbase + key * a.ks + ((r16 ^ (srow[i] & 15)) * 8);
-          vsrc = vbase + key * a.vs + ((r16 ^ ((srow[i] & 7) << 1)) * 8);
-        }
-        __builtin_amdgcn_global_load_lds((const void*)ksrc, LDS_PTR(base + (wave * 2 + i) * 1024), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)vsrc, LDS_PTR(base + TILE_BYTES + (wave * 2 + i) * 1024), 16,
-                                         0, 0);
-      }
+    for (int i = 0; i < 2; ++i) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, LDS_PTR((uintptr_t)(lds_dma + buf * STAGE_BYTES + i * 1024)), 16,
+                                               koff[i], ks_off, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rv, LDS_PTR((uintptr_t)(lds_dma + buf * STAGE_BYTES + TILE_BYTES + i * 1024)), 16, voff[i], vs_off, 0, 0);
     }
   };
 
@@ -782,12 +741,12 @@ __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (kb + 1 < nkb) stage(kb + 1, 1);
-    attn_v6_block<0, OPT>(st, qf, ka, va, kb, kv_len, g);
+    attn_v6_block<0>(st, qf, ka, va, kb, kv_len, g);
     if (kb + 1 >= nkb) break;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (kb + 2 < nkb) stage(kb + 2, 0);
-    attn_v6_block<1, OPT>(st, qf, ka, va, kb + 1, kv_len, g);
+    attn_v6_block<1>(st, qf, ka, va, kb + 1, kv_len, g);
   }
 
   // lane rows g and g^1 (lanes l, l^16) hold adjacent 4-column groups of one query row: one
@@ -820,9 +779,7 @@ __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) {
   }
 }
 
-// kernel: 0 = auto, 1 = attn_fwd_v6_kernel<false> (8 waves x 32 queries, mfma_f32_16x16x32_bf16),
-// 2 = attn_fwd_v6_kernel<true> (non-canonicalising max3 row max, -m splat kept across blocks, buffer-descriptor
-// K/V staging)
+// kernel: 0 = auto, 1 = attn_fwd_v6_kernel (8 waves x 32 queries, mfma_f32_16x16x32_bf16)
 extern "C" int sa_attn_fwd_ex(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
                               int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride,
                               int64_t v_stride, int64_t o_stride, float scale, int accumulate, int kernel,
@@ -831,22 +788,16 @@ extern "C" int sa_attn_fwd_ex(const void* q, const void* k, const void* v, void*
   if (head_dim != D) return SA_ERR_ARG;
   if ((q_stride | k_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
   if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)o)) & 15) return SA_ERR_ARG;
-  if (kernel < 0 || kernel > 2) return SA_ERR_ARG;
+  if (kernel < 0 || kernel > 1) return SA_ERR_ARG;
   static const bool attr = [] {  // one-time, thread-safe
-    (void)hipFuncSetAttribute((const void*)attn_fwd_v6_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_v6_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     return true;
   }();
   (void)attr;
   AttnArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, segs,
              q_stride, k_stride, v_stride, o_stride, scale * 1.4426950408889634f, accumulate};
   dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
-  if (kernel == 2)
-    hipLaunchKernelGGL(attn_fwd_v6_kernel<true>, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL(attn_fwd_v6_kernel<false>, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(attn_fwd_v6_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
   SA_LAUNCH_CHECK();
   return SA_OK;
 }

@@ -64,8 +64,7 @@ def _attn_errors(q, k, v, o, rows, heads, chunk=4096):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("kernel", [1, 2], ids=["v6", "v6opt"])
-def test_self_attention_fullsize(kernel):
+def test_self_attention_fullsize():
     """B=3, L=21504, H=12: every head within rel-L2 1e-2 of fp32 (includes the bf16 rounding of the
     prescaled q*scale*log2(e) the kernel feeds the MFMA and the bf16 P of the PV product)."""
     from stableavatar_amd import ops
@@ -74,7 +73,7 @@ def test_self_attention_fullsize(kernel):
     q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
     o = torch.empty(M, H * D, device=dev, dtype=torch.bfloat16)
     segs = torch.tensor([[b * L, L, b * L, L] for b in range(B)], dtype=torch.int32, device=dev)
-    ops.attention(q, k, v, o, segs, B, L, H, kernel=kernel)
+    ops.attention(q, k, v, o, segs, B, L, H)
     torch.cuda.synchronize()
     errs, mx = _attn_errors(q, k, v, o, range(B), range(H))
     print(f"attention L={L}: rel-L2 max {max(errs):.2e} mean {sum(errs) / len(errs):.2e}, max|d| {mx:.2e}")
@@ -82,8 +81,7 @@ def test_self_attention_fullsize(kernel):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("kernel", [1, 2], ids=["v6", "v6opt"])
-def test_self_attention_fullsize_peaked_scores(kernel):
+def test_self_attention_fullsize_peaked_scores():
     """Same launch with q scaled x4 (score std ~4: peaked softmax rows, the running max grows across
     many of the 336 key blocks, so the deferred-rescale branch fires): rel-L2 1e-2 on batch row 1."""
     from stableavatar_amd import ops
@@ -94,7 +92,7 @@ def test_self_attention_fullsize_peaked_scores(kernel):
     q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
     o = torch.empty(M, H * D, device=dev, dtype=torch.bfloat16)
     segs = torch.tensor([[b * L, L, b * L, L] for b in range(B)], dtype=torch.int32, device=dev)
-    ops.attention(q, k, v, o, segs, B, L, H, kernel=kernel)
+    ops.attention(q, k, v, o, segs, B, L, H)
     torch.cuda.synchronize()
     errs, mx = _attn_errors(q, k, v, o, [1], range(H))
     print(f"attention peaked: rel-L2 max {max(errs):.2e}, max|d| {mx:.2e}")

@@ -74,7 +74,7 @@ def test_gemm_kernels(kernel, M, N, K):
     a = torch.randn(2, 300, K, device=dev).bfloat16()
     bb = torch.randn(2, 200, K, device=dev).bfloat16()
     o = torch.empty(2, 300, 200, device=dev)
-    ops.bmm_nt(a, bb, o, kernel=kernel)
+    ops.bmm_nt(a, bb, o)
     assert rel(o, a.float() @ bb.float().transpose(1, 2)) < 2e-3
 
 
@@ -109,8 +109,7 @@ def _ref_attn(q, k, v, scale):
 
 
 @pytest.mark.parametrize("Lq,Lk", [(300, 300), (512, 257), (1024, 17), (64, 512)])
-@pytest.mark.parametrize("kernel", [1, 2], ids=["v6", "v6opt"])
-def test_attention_segments(Lq, Lk, kernel):
+def test_attention_segments(Lq, Lk):
     from stableavatar_amd import ops
     B, H, D = 2, 3, 128
     q = torch.randn(B * Lq, H * D + 64, device=dev).bfloat16()[:, :H * D]  # strided rows
@@ -118,7 +117,7 @@ def test_attention_segments(Lq, Lk, kernel):
     v = torch.randn(B * Lk, H * D, device=dev).bfloat16()
     o = torch.empty(B * Lq, H * D, device=dev, dtype=torch.bfloat16)
     segs = torch.tensor([[b * Lq, Lq, b * Lk, Lk] for b in range(B)], dtype=torch.int32, device=dev)
-    ops.attention(q, k, v, o, segs, B, Lq, H, kernel=kernel)
+    ops.attention(q, k, v, o, segs, B, Lq, H)
     for b in range(B):
         for h in range(H):
             ref = _ref_attn(q[b * Lq:(b + 1) * Lq, h * D:(h + 1) * D], k[b * Lk:(b + 1) * Lk, h * D:(h + 1) * D],
@@ -126,12 +125,11 @@ def test_attention_segments(Lq, Lk, kernel):
             assert rel(o[b * Lq:(b + 1) * Lq, h * D:(h + 1) * D], ref) < 1e-2, (b, h)
     # accumulate mode adds onto the existing output
     o2 = o.clone()
-    ops.attention(q, k, v, o2, segs, B, Lq, H, accumulate=True, kernel=kernel)
+    ops.attention(q, k, v, o2, segs, B, Lq, H, accumulate=True)
     assert rel(o2, 2 * o.float()) < 1e-2
 
 
-@pytest.mark.parametrize("kernel", [1, 2], ids=["v6", "v6opt"])
-def test_attention_vocal_grouping(kernel):
+def test_attention_vocal_grouping():
     """per-frame grouping of 1B:575-586: q rows of frame f attend to that frame's 17 keys"""
     from stableavatar_amd import ops
     B, F, G, Lv, H, D = 2, 3, 64, 17, 2, 128
@@ -140,7 +138,7 @@ def test_attention_vocal_grouping(kernel):
     v = torch.randn(B * F * Lv, H * D, device=dev).bfloat16()
     o = torch.empty_like(q)
     segs = torch.tensor([[i * G, G, i * Lv, Lv] for i in range(B * F)], dtype=torch.int32, device=dev)
-    ops.attention(q, k, v, o, segs, B * F, G, H, kernel=kernel)
+    ops.attention(q, k, v, o, segs, B * F, G, H)
     for i in range(B * F):
         for h in range(H):
             sl = slice(h * D, (h + 1) * D)
@@ -148,8 +146,7 @@ def test_attention_vocal_grouping(kernel):
             assert rel(o[i * G:(i + 1) * G, sl], ref) < 1e-2
 
 
-@pytest.mark.parametrize("kernel", [1, 2], ids=["v6", "v6opt"])
-def test_attention_spike_rescale(kernel):
+def test_attention_spike_rescale():
     """force the online-softmax rescale branch: a late key with a huge score"""
     from stableavatar_amd import ops
     L, D = 512, 128
@@ -159,7 +156,7 @@ def test_attention_spike_rescale(kernel):
     v = torch.randn(L, D, device=dev).bfloat16()
     o = torch.empty_like(q)
     segs = torch.tensor([[0, L, 0, L]], dtype=torch.int32, device=dev)
-    ops.attention(q, k, v, o, segs, 1, L, 1, kernel=kernel)
+    ops.attention(q, k, v, o, segs, 1, L, 1)
     assert rel(o, _ref_attn(q, k, v, D ** -0.5)) < 1e-2
 
 
