@@ -199,6 +199,24 @@ int sa_clip_patch_im2col(const float* img, int C, int S, int P, void* cols, int 
 
 int sa_cast_bf16_f32(const void* in, float* out, int64_t n, void* stream);
 
+/* ---- wav2vec2 audio encoder: replaces transformers' Wav2Vec2Model called per
+ * window at wan_inference_long_pipeline.py:727-729 (loaded at inference.py:475-476).  Transformer layers and
+ * the 1-D convs 1-6 run on sa_gemm_bf16 / sa_attn_small; these are the pieces around them. */
+
+/* Feature-encoder conv 0 (Wav2Vec2GroupNormConvLayer: Conv1d(1, C, k, stride, bias=False) -> GroupNorm(C, C)
+ * -> GELU) on the fp32 normalised waveform; statistics over all T outputs per channel; bf16 [T][C] out. */
+int sa_w2v_conv0_gn_gelu(const float* audio, int n_samples, const float* weight, int C, int k, int stride,
+                         const float* gn_weight, const float* gn_bias, float eps, void* out, int T, void* stream);
+
+/* 1-D im2col of a channels-last bf16 [T_in][ldx] tensor for `groups` groups of `cg` channels starting at
+ * column col0: out[g][t][j*cg + c] = x[t*stride + j - pad][col0 + g*cg + c] (zero outside the input and for
+ * columns >= k*cg up to Kpad).  Wav2Vec2NoLayerNormConvLayer (:conv) and Wav2Vec2PositionalConvEmbedding. */
+int sa_conv1d_im2col(const void* x, int64_t ldx, int T_in, int col0, int groups, int cg, int k, int stride, int pad,
+                     void* out, int T_out, int Kpad, void* stream);
+
+/* x (f32 [M][ldx]) += y (bf16 [M][ldy]): hidden_states + position_embeddings (Wav2Vec2Encoder.forward). */
+int sa_add_f32_bf16(float* x, int64_t ldx, const void* y, int64_t ldy, int M, int N, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -46,6 +46,9 @@ SIGNATURES = {
     "sa_clip_preprocess": "piiipippp",
     "sa_clip_patch_im2col": "piiipip",
     "sa_cast_bf16_f32": "pplp",
+    "sa_w2v_conv0_gn_gelu": "pipiiippfpip",
+    "sa_conv1d_im2col": "pliiiiiiipiip",
+    "sa_add_f32_bf16": "plpliip",
 }
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int32, "l": ctypes.c_int64, "f": ctypes.c_float}
 

@@ -3,8 +3,9 @@
 Same flags and defaults, plus ``--device`` / ``--dtype``; the components are this package's HIP modules:
 ``WanT5EncoderModel`` and ``CLIPModel`` (encoders.py), ``AutoencoderKLWan`` (vae.py),
 ``WanTransformer3DFantasyModel`` (transformer.py), ``FlowMatchEulerDiscreteScheduler`` (scheduler.py) and
-``WanI2VTalkingInferenceLongPipeline`` (pipeline.py); tokenizer and wav2vec2 come from ``transformers`` as in
-the reference (wav2vec2 runs on the GPU through PyTorch; its features are computed once per window).
+``WanI2VTalkingInferenceLongPipeline`` (pipeline.py) and ``Wav2Vec2Model`` (wav2vec.py, the audio encoder on the
+HIP kernels, reading the same transformers model directory); the tokenizer and the wav2vec2 processor come from
+``transformers`` as in the reference.  wav2vec2 features are computed once per window and reused across steps.
 
 Flag mapping:
 * ``--ulysses_degree`` x ``--ring_degree`` > 1 (under torchrun, RCCL): the transformer's sequence parallelism
@@ -140,7 +141,9 @@ def convert_model_weight_to_float8(model, exclude_module_name=("modulation",)):
 
 def main(argv=None):
     args = parse_args(argv)
-    from transformers import AutoTokenizer, Wav2Vec2Model, Wav2Vec2Processor
+    from transformers import AutoTokenizer, Wav2Vec2Processor
+
+    from .wav2vec import Wav2Vec2Model
 
     from .encoders import CLIPModel, WanT5EncoderModel
     from .pipeline import WanI2VTalkingInferenceLongPipeline
@@ -176,7 +179,7 @@ def main(argv=None):
     vk = config["vae_kwargs"]
     vae = AutoencoderKLWan.from_pretrained(os.path.join(root, vk.get("vae_subpath", "vae")), additional_kwargs=vk)
     wav2vec_processor = Wav2Vec2Processor.from_pretrained(args.pretrained_wav2vec_path)
-    wav2vec = Wav2Vec2Model.from_pretrained(args.pretrained_wav2vec_path).to(device).eval()
+    wav2vec = Wav2Vec2Model.from_pretrained(args.pretrained_wav2vec_path).to(device)
     ik = config["image_encoder_kwargs"]
     clip_image_encoder = CLIPModel.from_pretrained(os.path.join(root, ik.get("image_encoder_subpath", "image_encoder")),
                                                    transformer_additional_kwargs=ik).eval()

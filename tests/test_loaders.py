@@ -137,3 +137,27 @@ def test_vae_from_pretrained(tmp_path, fmt):
         save_file(raw, path)
     v = AutoencoderKLWan.from_pretrained(path, additional_kwargs={"dim": 32, "vae_subpath": "x", "unused": 1})
     _same(v, sd)
+
+
+def test_wav2vec2_keys_match_transformers():
+    """the HIP wav2vec2 (stableavatar_amd/wav2vec.py) takes transformers' Wav2Vec2Model state_dict as is, the
+    Wav2Vec2ForCTC prefix / head and the legacy weight-norm names (wav2vec2-base-960h) included, and its
+    feature-encoder length formula matches transformers'"""
+    import torch
+    from transformers import Wav2Vec2Config, Wav2Vec2Model as HF
+
+    from stableavatar_amd.wav2vec import Wav2Vec2Model
+    hf = HF(Wav2Vec2Config(num_hidden_layers=2))
+    ours = Wav2Vec2Model(hf.config)
+    assert set(ours.state_dict()) == set(hf.state_dict()) - {"masked_spec_embed"}
+    ours.load_state_dict(hf.state_dict())
+    legacy = {"wav2vec2." + k.replace("parametrizations.weight.original0", "weight_g")
+              .replace("parametrizations.weight.original1", "weight_v"): v for k, v in hf.state_dict().items()}
+    legacy["lm_head.weight"] = torch.zeros(4, 768)
+    ours.load_state_dict(legacy)
+    sd = ours.state_dict()
+    assert all(torch.equal(sd[k], v) for k, v in hf.state_dict().items() if k in sd)
+    with pytest.raises(KeyError):
+        ours.load_state_dict({k: v for k, v in hf.state_dict().items() if "layers.1." not in k})
+    for n in (400, 8000, 16123, 51840):
+        assert ours.frames(n) == int(hf._get_feat_extract_output_lengths(torch.tensor(n)))
