@@ -158,9 +158,16 @@ def split_index_table(audio_len, num_frames, expand_length=4):
 
 
 def vocal_projector(P, pre, vocal_embeddings, video_sample_n_frames, latents, e0, e, heads=8, eps=1e-6):
-    """FantasyTalkingVocalCondition1BModel.forward (vocal_projector_fantasy_1B.py:433-450)."""
-    feat = F.linear(vocal_embeddings, P[pre + ".proj_model.proj.weight"])
-    feat = layer_norm(feat, 1e-5, P[pre + ".proj_model.norm.weight"], P[pre + ".proj_model.norm.bias"])
+    """FantasyTalkingVocalCondition1BModel.forward (vocal_projector_fantasy_1B.py:433-450); with the
+    14B model's two-layer VocalProjModel (vocal_projector_fantasy_14B.py:385-398) when its keys are present."""
+    if pre + ".proj_model.proj_1.weight" in P:
+        feat = F.linear(vocal_embeddings, P[pre + ".proj_model.proj_1.weight"])
+        feat = layer_norm(feat, 1e-5, P[pre + ".proj_model.norm_1.weight"], P[pre + ".proj_model.norm_1.bias"])
+        feat = F.linear(feat, P[pre + ".proj_model.proj_2.weight"])
+        feat = layer_norm(feat, 1e-5, P[pre + ".proj_model.norm_2.weight"], P[pre + ".proj_model.norm_2.bias"])
+    else:
+        feat = F.linear(vocal_embeddings, P[pre + ".proj_model.proj.weight"])
+        feat = layer_norm(feat, 1e-5, P[pre + ".proj_model.norm.weight"], P[pre + ".proj_model.norm.bias"])
     rows, _ = split_index_table(feat.size(1), video_sample_n_frames)
     Fn = len(rows)
     zero = feat.new_zeros(feat.size(0), 1, feat.size(2))
@@ -192,7 +199,9 @@ def vocal_projector(P, pre, vocal_embeddings, video_sample_n_frames, latents, e0
 
 def forward(P, cfg, x, t, context, seq_len, clip_fea, y, vocal_embeddings, video_sample_n_frames=81):
     """WanTransformer3DFantasyModel.forward 1B:928-1159 for the inference call of
-    wan_inference_long_pipeline.py:740-750 (is_clip_level_modeling=False, SP off, TeaCache off).
+    wan_inference_long_pipeline.py:740-750 (is_clip_level_modeling=False, SP off, TeaCache off); with
+    cfg["vocal"] == "14B" WanTransformer3DFantasy14BModel.forward (14B:922-1152: 81-frame vocal path on
+    every CFG row).
     x, y: [B, C, F, H, W]; context: list of [L_i, text_dim]; returns [B, out_dim, F, H, W]."""
     dim, heads, eps = cfg["dim"], cfg["num_heads"], cfg.get("eps", 1e-6)
     text_len, freq_dim, out_dim = cfg["text_len"], cfg["freq_dim"], cfg["out_dim"]
@@ -215,7 +224,9 @@ def forward(P, cfg, x, t, context, seq_len, clip_fea, y, vocal_embeddings, video
     ci = linear(P, "img_emb.proj.3", F.gelu(linear(P, "img_emb.proj.1", ci)))
     ci = layer_norm(ci, 1e-5, P["img_emb.proj.4.weight"], P["img_emb.proj.4.bias"])
     ctx = torch.cat([ci, ctx], dim=1)
-    if vocal_embeddings.size(0) > 1:
+    if cfg.get("vocal", "1B") == "14B":  # every row through the projector (14B:1008)
+        vocal_ctx = vocal_projector(P, "vocal_projector", vocal_embeddings.float(), 81, xe, e0, e)
+    elif vocal_embeddings.size(0) > 1:
         v = vocal_projector(P, "vocal_projector", vocal_embeddings[-1:].float(), video_sample_n_frames,
                             xe[-1:], e0[-1:], e[-1:])
         vocal_ctx = torch.cat([torch.zeros_like(v), v, v])
@@ -236,7 +247,10 @@ def forward(P, cfg, x, t, context, seq_len, clip_fea, y, vocal_embeddings, video
 
 
 def param_shapes(cfg):
-    """{name: shape} of the reference module for config `cfg` (same keys as its state_dict)."""
+    """{name: shape} of the reference module for config `cfg` (same keys as its state_dict); the 14B
+    module's with cfg["vocal"] == "14B"."""
+    if cfg.get("vocal", "1B") == "14B":
+        return _param_shapes_14b(cfg)
     dim, ffn, L = cfg["dim"], cfg["ffn_dim"], cfg["num_layers"]
     S = {"patch_embedding.weight": (dim, cfg["in_dim"], 1, 2, 2), "patch_embedding.bias": (dim,),
          "text_embedding.0.weight": (dim, cfg["text_dim"]), "text_embedding.0.bias": (dim,),
@@ -294,6 +308,31 @@ def param_shapes(cfg):
     S[vp + ".final_head.modulation"] = (1, 2, 1536)
     S[vp + ".final_head.final_proj.weight"] = (1536, 1536)
     S[vp + ".final_head.final_proj.bias"] = (1536,)
+    return S
+
+
+def _param_shapes_14b(cfg):
+    """WanTransformer3DFantasy14BModel (14B:823-866): the 1.3B layout at the model's width, plus the 14B
+    vocal projector (vocal_projector_fantasy_14B.py:385-425): 768 -> 2048 -> dim projection, width dim."""
+    S = {k: v for k, v in param_shapes(dict(cfg, vocal="1B")).items() if not k.startswith("vocal_projector")}
+    dim, vp = cfg["dim"], "vocal_projector"
+    S.update({vp + ".proj_model.proj_1.weight": (2048, 768), vp + ".proj_model.norm_1.weight": (2048,),
+              vp + ".proj_model.norm_1.bias": (2048,), vp + ".proj_model.proj_2.weight": (dim, 2048),
+              vp + ".proj_model.norm_2.weight": (dim,), vp + ".proj_model.norm_2.bias": (dim,)})
+    for i in range(2):
+        bp = f"{vp}.blocks.{i}"
+        S[bp + ".modulation"] = (1, 6, dim)
+        for n in ("norm3.weight", "norm3.bias", "cross_attn.norm_q.weight", "cross_attn.norm_k.weight",
+                  "cross_attn.q.bias", "cross_attn.k.bias", "cross_attn.v.bias", "cross_attn.o.bias", "ffn.2.bias"):
+            S[f"{bp}.{n}"] = (dim,)
+        for n in ("q", "k", "v", "o"):
+            S[f"{bp}.cross_attn.{n}.weight"] = (dim, dim)
+        S[bp + ".ffn.0.weight"] = (2 * dim, dim)
+        S[bp + ".ffn.0.bias"] = (2 * dim,)
+        S[bp + ".ffn.2.weight"] = (dim, 2 * dim)
+    S[vp + ".final_head.modulation"] = (1, 2, dim)
+    S[vp + ".final_head.final_proj.weight"] = (dim, dim)
+    S[vp + ".final_head.final_proj.bias"] = (dim,)
     return S
 
 

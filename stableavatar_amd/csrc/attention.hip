@@ -392,11 +392,12 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
   }
 }
 
-// ---- small-query attention for head dims the MFMA kernel does not take (vocal projector, D=192,
-// 17 queries per frame vs 1024 latent tokens: vocal_projector_fantasy_1B.py:259-270).  One wave
+// ---- small-query attention for head dims the MFMA kernel does not take (vocal projector, D=192 for
+// 1.3B and 640 for 14B, 17 queries per frame vs one latent frame's tokens: vocal_projector_fantasy_1B.py:
+// 259-270, vocal_projector_fantasy_14B.py:254-267; wav2vec2, D=64).  One wave
 // per (segment, head, query): scores for all keys in LDS, exact softmax, lane-parallel P·V.
 constexpr int SMALL_MAXK = 4096;
-constexpr int SMALL_MAXD = 256;
+constexpr int SMALL_MAXD = 640;
 
 __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* q, const bf16* k, const bf16* v, bf16* o,
                                                          const int* segs, int heads, int D, long qs, long ks, long vs,

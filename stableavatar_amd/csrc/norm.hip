@@ -50,10 +50,10 @@ struct LnArgs {
   float eps;
 };
 
-constexpr int MAXV = 8;  // up to 8 chunks of 8 per lane -> C <= 4096
+constexpr int MAXV = 10;  // up to 10 chunks of 8 per lane -> C <= 5120 (the 14B DiT width)
 
 // FIXED > 0: C == FIXED * 512 known at compile time (the DiT's C = 1536), so every chunk's loads are
-// unconditional and issue together; FIXED == 0: any C % 8 == 0 up to 4096.
+// unconditional and issue together; FIXED == 0: any C % 8 == 0 up to 5120.
 template <typename TI, typename TO, int FIXED = 0>
 __global__ __launch_bounds__(256) void layernorm_mod_kernel(LnArgs a) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -263,6 +263,8 @@ template <typename TI, typename TO>
 int launch_ln(const LnArgs& a, hipStream_t st) {
   if (a.C == 1536)
     hipLaunchKernelGGL((layernorm_mod_kernel<TI, TO, 3>), dim3((a.M + 3) / 4), dim3(256), 0, st, a);
+  else if (a.C == 5120)
+    hipLaunchKernelGGL((layernorm_mod_kernel<TI, TO, 10>), dim3((a.M + 3) / 4), dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL((layernorm_mod_kernel<TI, TO>), dim3((a.M + 3) / 4), dim3(256), 0, st, a);
   SA_LAUNCH_CHECK();
@@ -299,10 +301,13 @@ extern "C" int sa_qk_rmsnorm_rope(void* x, int64_t ldx, int q_col, int k_col, co
   if (rope && (rows_per_batch <= 0 || head_dim % 8 || F <= 0 || H <= 0 || W <= 0)) return SA_ERR_ARG;
   QkArgs a{(bf16*)x, ldx, q_col, k_col, wq, wk, M, C, head_dim, eps, rope, rows_per_batch > 0 ? rows_per_batch : 1,
            tok_offset, F, H, W, n_frame_pairs, n_height_pairs};
-  if (rope && k_col >= 0 && C == 1536 && head_dim == 128 && getenv("SA_QK_GENERIC") == nullptr)
+  static const bool generic = getenv("SA_QK_GENERIC") != nullptr;  // A/B switch, read once
+  if (rope && k_col >= 0 && C == 1536 && head_dim == 128 && !generic)
     hipLaunchKernelGGL(qk_rmsnorm_rope_pair_kernel, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
   else if (C == 1536)
     hipLaunchKernelGGL(qk_rmsnorm_rope_kernel<3>, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
+  else if (C == 5120)
+    hipLaunchKernelGGL(qk_rmsnorm_rope_kernel<10>, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(qk_rmsnorm_rope_kernel<0>, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
   SA_LAUNCH_CHECK();

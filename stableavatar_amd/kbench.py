@@ -178,12 +178,54 @@ def main(which=("gemm", "attn")):
     if "dit" in which:
         res.append(bench_dit())
         print(json.dumps(res[-1]), flush=True)
+    if "dit14" in which:
+        res.append(bench_dit14())
+        print(json.dumps(res[-1]), flush=True)
     if "ditvar" in which:  # in-situ A/B of attention variants inside full DiT forwards (interleaved)
         import os
         avars = tuple(int(v) for v in os.environ.get("SA_KB_AVARS", "1").split(","))
         res.append(bench_dit(attn_variants=avars))
         print(json.dumps(res[-1]), flush=True)
     return res
+
+
+def bench_dit14(layer_counts=(1, 2)):
+    """BASELINE config 4's model on one GPU: WanTransformer3DFantasy14BModel (dim 5120, 40 heads, ffn 13824)
+    at 720x1280 (90x160 latent, 21 latent frames: L = 75 600 tokens, B = 3 CFG rows), forwards with 1 and 2
+    layers; the difference is one block's time, the remainder the embeddings + 14B vocal projector + head."""
+    from . import synthetic
+    from .flops import dit_forward_flops
+    from .transformer import WanTransformer3DFantasy14BModel, param_shapes
+    cfg = dict(model_type="i2v", dim=5120, ffn_dim=13824, freq_dim=256, text_dim=4096, in_dim=36, out_dim=16,
+               num_heads=40, text_len=512)
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(0)
+    lat = torch.randn(1, 16, 21, 90, 160, device=dev, generator=g).bfloat16()
+    y = torch.randn(3, 20, 21, 90, 160, device=dev, generator=g).bfloat16()
+    ctx = [torch.randn(n, 4096, device=dev, generator=g) for n in (120, 120, 60)]
+    clip = torch.randn(3, 257, 1280, device=dev, generator=g)
+    a = torch.randn(1, 161, 768, device=dev, generator=g)
+    voc = torch.cat([torch.zeros_like(a), a, a])
+    t = torch.tensor([990.0], device=dev)
+    L = 21 * 45 * 80
+    ms = {}
+    for nl in layer_counts:
+        m = WanTransformer3DFantasy14BModel(**cfg, num_layers=nl).to(dev)
+        m.load_state_dict(synthetic.fill_state_dict(param_shapes(dict(cfg, num_layers=nl, vocal="14B")), 0,
+                                                    backend="torch", device=dev))
+        with torch.no_grad():
+            ms[nl] = _time(lambda: m.forward_window(lat, 0, True, 3, t, ctx, L, clip, y, voc, 81), iters=2, warmup=1)
+        del m
+        torch.cuda.empty_cache()
+    per_layer = ms[2] - ms[1]
+    fl_layer = dit_forward_flops(B=3, L=L, dim=5120, ffn=13824, layers=1) - dit_forward_flops(
+        B=3, L=L, dim=5120, ffn=13824, layers=0)
+    fl_fwd = dit_forward_flops(B=3, L=L, dim=5120, ffn=13824, layers=40)
+    fwd40 = ms[1] - per_layer + 40 * per_layer
+    return {"kernel": "dit14_forward_720p", "L": L, "ms_1_layer": round(ms[1], 1), "ms_2_layers": round(ms[2], 1),
+            "ms_per_layer": round(per_layer, 1), "tflops_per_layer": round(fl_layer / per_layer / 1e9, 1),
+            "ms_forward_40_layers_projected": round(fwd40, 0), "tflop_per_forward": round(fl_fwd / 1e12, 0),
+            "tflops_forward_projected": round(fl_fwd / fwd40 / 1e9, 1)}
 
 
 def bench_dit(iters=3, attn_variants=None):

@@ -137,6 +137,9 @@ def qk_rmsnorm_rope(x, q_col, k_col, wq, wk, C, eps, rope=None, rows_per_batch=0
 
 def patch_im2col(x, y, B, F, H, W, out, Kpad, Lpad, x_frame_offset=0, x_batch_broadcast=False):
     """x: [Bx, Cx, Tx, H, W] bf16 (frames x_frame_offset.. used), y: [B, Cy, >=F, H, W] bf16."""
+    _check(x, torch.bfloat16, "patch_im2col.x")
+    if y is not None:
+        _check(y, torch.bfloat16, "patch_im2col.y")
     xc = x.stride(1)
     xb = 0 if x_batch_broadcast else x.stride(0)
     xf = x.stride(2)

@@ -84,8 +84,14 @@ def split_rows(audio_len, num_frames, expand_length=4):
     return rows
 
 
+def vocal_dim(cfg: dict) -> int:
+    """width of the vocal projector: 1536 for the 1.3B model (1B:872), the DiT width for 14B (14B:866)"""
+    return cfg["dim"] if cfg.get("vocal", "1B") == "14B" else 1536
+
+
 def param_shapes(cfg: dict) -> dict:
-    """{state_dict key: shape} of the reference WanTransformer3DFantasyModel (1B:829-872)."""
+    """{state_dict key: shape} of the reference WanTransformer3DFantasyModel (1B:829-872), or of
+    WanTransformer3DFantasy14BModel (14B:823-866) with cfg["vocal"] = "14B"."""
     dim, ffn, L = cfg["dim"], cfg["ffn_dim"], cfg["num_layers"]
     S = {"patch_embedding.weight": (dim, cfg["in_dim"], 1, 2, 2), "patch_embedding.bias": (dim,),
          "text_embedding.0.weight": (dim, cfg["text_dim"]), "text_embedding.0.bias": (dim,),
@@ -121,29 +127,41 @@ def param_shapes(cfg: dict) -> dict:
                   "img_emb.proj.3.weight": (dim, 1280), "img_emb.proj.3.bias": (dim,),
                   "img_emb.proj.4.weight": (dim,), "img_emb.proj.4.bias": (dim,)})
     vp = "vocal_projector"
-    S[vp + ".proj_model.proj.weight"] = (1536, 768)
-    S[vp + ".proj_model.norm.weight"] = (1536,)
-    S[vp + ".proj_model.norm.bias"] = (1536,)
+    # 1.3B: FantasyTalkingVocalCondition1BModel(audio_proj_dim=1536) (1B:872, vocal_projector_fantasy_1B.py:
+    # 389-431); 14B: audio_proj_dim = dim and a two-layer audio projection 768 -> 2048 -> dim (14B:866,
+    # vocal_projector_fantasy_14B.py:385-425); both: 2 blocks of 8 heads, ffn 2 x width, final head
+    vd = vocal_dim(cfg)
+    if cfg.get("vocal", "1B") == "14B":
+        S[vp + ".proj_model.proj_1.weight"] = (2048, 768)
+        S[vp + ".proj_model.norm_1.weight"] = (2048,)
+        S[vp + ".proj_model.norm_1.bias"] = (2048,)
+        S[vp + ".proj_model.proj_2.weight"] = (vd, 2048)
+        S[vp + ".proj_model.norm_2.weight"] = (vd,)
+        S[vp + ".proj_model.norm_2.bias"] = (vd,)
+    else:
+        S[vp + ".proj_model.proj.weight"] = (vd, 768)
+        S[vp + ".proj_model.norm.weight"] = (vd,)
+        S[vp + ".proj_model.norm.bias"] = (vd,)
     for i in range(2):
         bp = f"{vp}.blocks.{i}"
-        S[bp + ".modulation"] = (1, 6, 1536)
-        S[bp + ".norm3.weight"] = (1536,)
-        S[bp + ".norm3.bias"] = (1536,)
+        S[bp + ".modulation"] = (1, 6, vd)
+        S[bp + ".norm3.weight"] = (vd,)
+        S[bp + ".norm3.bias"] = (vd,)
         for n in ("q", "o"):
-            S[f"{bp}.cross_attn.{n}.weight"] = (1536, 1536)
-            S[f"{bp}.cross_attn.{n}.bias"] = (1536,)
+            S[f"{bp}.cross_attn.{n}.weight"] = (vd, vd)
+            S[f"{bp}.cross_attn.{n}.bias"] = (vd,)
         for n in ("k", "v"):
-            S[f"{bp}.cross_attn.{n}.weight"] = (1536, dim)
-            S[f"{bp}.cross_attn.{n}.bias"] = (1536,)
-        S[bp + ".cross_attn.norm_q.weight"] = (1536,)
-        S[bp + ".cross_attn.norm_k.weight"] = (1536,)
-        S[bp + ".ffn.0.weight"] = (3072, 1536)
-        S[bp + ".ffn.0.bias"] = (3072,)
-        S[bp + ".ffn.2.weight"] = (1536, 3072)
-        S[bp + ".ffn.2.bias"] = (1536,)
-    S[vp + ".final_head.modulation"] = (1, 2, 1536)
-    S[vp + ".final_head.final_proj.weight"] = (1536, 1536)
-    S[vp + ".final_head.final_proj.bias"] = (1536,)
+            S[f"{bp}.cross_attn.{n}.weight"] = (vd, dim)
+            S[f"{bp}.cross_attn.{n}.bias"] = (vd,)
+        S[bp + ".cross_attn.norm_q.weight"] = (vd,)
+        S[bp + ".cross_attn.norm_k.weight"] = (vd,)
+        S[bp + ".ffn.0.weight"] = (2 * vd, vd)
+        S[bp + ".ffn.0.bias"] = (2 * vd,)
+        S[bp + ".ffn.2.weight"] = (vd, 2 * vd)
+        S[bp + ".ffn.2.bias"] = (vd,)
+    S[vp + ".final_head.modulation"] = (1, 2, vd)
+    S[vp + ".final_head.final_proj.weight"] = (vd, vd)
+    S[vp + ".final_head.final_proj.bias"] = (vd,)
     return S
 
 
@@ -175,6 +193,8 @@ class _Seg:
 class WanTransformer3DFantasyModel(nn.Module):
     """Audio-driven Wan-2.1 DiT (1B:741-1184) on HIP kernels."""
 
+    VOCAL = "1B"  # vocal projector family (param_shapes)
+
     def __init__(self, model_type="i2v", patch_size=(1, 2, 2), text_len=512, in_dim=16, dim=2048, ffn_dim=8192,
                  freq_dim=256, text_dim=4096, out_dim=16, num_heads=16, num_layers=32, window_size=(-1, -1),
                  qk_norm=True, cross_attn_norm=True, eps=1e-6, in_channels=16, hidden_size=2048, **_):
@@ -198,7 +218,8 @@ class WanTransformer3DFantasyModel(nn.Module):
                                       eps=eps, in_channels=in_channels, hidden_size=hidden_size)
         self._cfg = dict(model_type=model_type, dim=dim, ffn_dim=ffn_dim, freq_dim=freq_dim, text_dim=text_dim,
                          in_dim=in_dim, out_dim=out_dim, num_heads=num_heads, num_layers=num_layers,
-                         text_len=text_len)
+                         text_len=text_len, vocal=self.VOCAL)
+        self.vd = vocal_dim(self._cfg)
         _register_tree(self, param_shapes(self._cfg), torch.float32)
         self.sp_world_size, self.sp_world_rank, self.sp_group = 1, 0, None
         self.teacache = None  # enable_teacache() (1B:867)
@@ -370,8 +391,14 @@ class WanTransformer3DFantasyModel(nn.Module):
             pk.ie4w, pk.ie4b = f32("img_emb.proj.4.weight"), f32("img_emb.proj.4.bias")
         vp = "vocal_projector."
         V = SimpleNamespace()
-        V.w_proj = bf(vp + "proj_model.proj.weight")
-        V.nw, V.nb = f32(vp + "proj_model.norm.weight"), f32(vp + "proj_model.norm.bias")
+        if self.VOCAL == "14B":  # two-layer audio projection (vocal_projector_fantasy_14B.py:385-398)
+            V.proj = [(bf(vp + "proj_model.proj_1.weight"), f32(vp + "proj_model.norm_1.weight"),
+                       f32(vp + "proj_model.norm_1.bias")),
+                      (bf(vp + "proj_model.proj_2.weight"), f32(vp + "proj_model.norm_2.weight"),
+                       f32(vp + "proj_model.norm_2.bias"))]
+        else:
+            V.proj = [(bf(vp + "proj_model.proj.weight"), f32(vp + "proj_model.norm.weight"),
+                       f32(vp + "proj_model.norm.bias"))]
         V.mod = torch.cat([P[f"{vp}blocks.{i}.modulation"].detach() for i in range(2)], 0).float().contiguous()
         V.blocks = []
         for i in range(2):
@@ -386,7 +413,7 @@ class WanTransformer3DFantasyModel(nn.Module):
             B_.w_f0, B_.b_f0 = bf(b + "ffn.0.weight"), f32(b + "ffn.0.bias")
             B_.w_f2, B_.b_f2 = bf(b + "ffn.2.weight"), f32(b + "ffn.2.bias")
             V.blocks.append(B_)
-        V.fmod = f32(vp + "final_head.modulation").reshape(1, 2, 1536)
+        V.fmod = f32(vp + "final_head.modulation").reshape(1, 2, self.vd)
         V.w_fp, V.b_fp = bf(vp + "final_head.final_proj.weight"), f32(vp + "final_head.final_proj.bias")
         pk.vocal = V
         pk.rope = rope_table(self.d, riflex=self._riflex).to(dev)
@@ -451,13 +478,18 @@ class WanTransformer3DFantasyModel(nn.Module):
     # ------------------------------------------------------------------ vocal projector
 
     def _vocal(self, pk, vocal_embeddings, n_frames, lat_bf16, Lq, e0_row, e_row, dev):
-        """FantasyTalkingVocalCondition1BModel.forward (vocal_projector_fantasy_1B.py:433-450) for one
-        audio row; lat_bf16 = patch-embedded tokens of that row [Lq, dim]. Returns [F*n, 1536] bf16."""
-        V = pk.vocal
-        va = vocal_embeddings.to(device=dev, dtype=torch.bfloat16).contiguous()
-        Na = va.shape[0]
-        feat = ops.linear(va, V.w_proj, None, ops.EPI_F32)
-        ops.layernorm_mod(feat, feat, 1e-5, weight=V.nw, bias=V.nb)
+        """FantasyTalkingVocalCondition{1B,14B}Model.forward (vocal_projector_fantasy_1B.py:433-450,
+        _14B.py:431-449) for one audio row; lat_bf16 = patch-embedded tokens of that row [Lq, dim].
+        Returns [F*n, vd] bf16 (vd = 1536 for 1.3B, the DiT width for 14B)."""
+        V, vd = pk.vocal, self.vd
+        hdv = vd // 8  # 8 heads: D = 192 (1.3B) or 640 (14B)
+        feat = vocal_embeddings.to(device=dev, dtype=torch.bfloat16).contiguous()
+        Na = feat.shape[0]
+        for j, (w, nw, nb) in enumerate(V.proj):  # Linear (no bias) + LayerNorm, once or twice
+            f = ops.linear(feat, w, None, ops.EPI_F32)
+            last = j == len(V.proj) - 1
+            feat = ops.layernorm_mod(f, f if last else torch.empty(Na, f.shape[1], device=dev, dtype=torch.bfloat16),
+                                     1e-5, weight=nw, bias=nb)
         key = (Na, n_frames)
         rows = self._split_cache.get(key)
         if rows is None:
@@ -465,12 +497,12 @@ class WanTransformer3DFantasyModel(nn.Module):
             rows = (torch.tensor([i for row in r for i in row], dtype=torch.int32, device=dev), len(r), len(r[0]))
             self._split_cache[key] = rows
         idx, Fn, nper = rows
-        x = torch.empty(Fn * nper, 1536, device=dev, dtype=torch.float32)
+        x = torch.empty(Fn * nper, vd, device=dev, dtype=torch.float32)
         ops.gather_rows(feat, idx, x)
-        em = torch.empty(2, 1, 6, 1536, device=dev, dtype=torch.float32)
+        em = torch.empty(2, 1, 6, vd, device=dev, dtype=torch.float32)
         ops.mod_add(V.mod, e0_row, em)
         Mv = Fn * nper
-        hb = torch.empty(Mv, 1536, device=dev, dtype=torch.bfloat16)
+        hb = torch.empty(Mv, vd, device=dev, dtype=torch.bfloat16)
         G = Lq // Fn
         segs = self._segs.get(("vp", Fn, nper, G), [[f * nper, nper, f * G, G] for f in range(Fn)], dev)
         for i, B_ in enumerate(V.blocks):
@@ -479,16 +511,16 @@ class WanTransformer3DFantasyModel(nn.Module):
             ops.layernorm_mod(x, x, 1e-6, shift=e[0:1], scale=e[1:2], gate=e[2:3], rows_per_batch=Mv)
             ops.layernorm_mod(x, hb, 1e-6, weight=B_.n3w, bias=B_.n3b)
             q = ops.linear(hb, B_.w_q, B_.b_q, ops.EPI_BF16)
-            ops.qk_rmsnorm_rope(q, 0, -1, B_.nq, None, 1536, 1e-6)
+            ops.qk_rmsnorm_rope(q, 0, -1, B_.nq, None, vd, 1e-6)
             kv = ops.linear(lat_bf16, B_.w_kv, B_.b_kv, ops.EPI_BF16)
-            ops.qk_rmsnorm_rope(kv, 0, -1, B_.nk, None, 1536, 1e-6)
-            o = torch.empty(Mv, 1536, device=dev, dtype=torch.bfloat16)
-            ops.attention_small(q, kv[:, :1536], kv[:, 1536:], o, segs, Fn, nper, G, 8, 192)
+            ops.qk_rmsnorm_rope(kv, 0, -1, B_.nk, None, vd, 1e-6)
+            o = torch.empty(Mv, vd, device=dev, dtype=torch.bfloat16)
+            ops.attention_small(q, kv[:, :vd], kv[:, vd:], o, segs, Fn, nper, G, 8, hdv)
             ops.linear(o, B_.w_o, B_.b_o, ops.EPI_RES_F32, out=x, residual=x)
             ops.layernorm_mod(x, hb, 1e-6, shift=e[3:4], scale=e[4:5], rows_per_batch=Mv)
             h = ops.linear(hb, B_.w_f0, B_.b_f0, ops.EPI_GELU_TANH_BF16)
             ops.linear(h, B_.w_f2, B_.b_f2, ops.EPI_RES_F32, out=x, residual=x, gate=e[5:6], rows_per_batch=Mv)
-        ef = torch.empty(1, 1, 2, 1536, device=dev, dtype=torch.float32)
+        ef = torch.empty(1, 1, 2, vd, device=dev, dtype=torch.float32)
         ops.mod_add(V.fmod, e_row, ef, e_jstride=0)
         ops.layernorm_mod(x, hb, 1e-6, shift=ef[0, 0, 0:1], scale=ef[0, 0, 1:2], rows_per_batch=Mv)
         return ops.linear(hb, V.w_fp, V.b_fp, ops.EPI_BF16), Fn, nper
@@ -533,6 +565,11 @@ class WanTransformer3DFantasyModel(nn.Module):
             raise NotImplementedError("clip-level audio modeling is a training mode (1B:1011-1015)")
         if self.model_type == "i2v":
             assert clip_fea is not None and y is not None
+        # the patch-embedding Conv3d runs under the pipeline's bf16 autocast (pipeline:738): bf16 operands
+        if lat.dtype != torch.bfloat16:
+            lat = lat.to(torch.bfloat16)
+        if y is not None and y.dtype != torch.bfloat16:
+            y = y.to(torch.bfloat16)
         pk = self._pack()
         dev = pk.w_pe.device
         dim, H_ = self.dim, self.num_heads
@@ -595,13 +632,17 @@ class WanTransformer3DFantasyModel(nn.Module):
             lat_row = torch.empty(Lp, dim, device=dev, dtype=torch.bfloat16)
             if vocal_embeddings.shape[0] == 1 and B != 1:
                 raise ValueError("a single audio row drives a batch of 1 (1B:1008-1009); CFG batches pass 3 rows")
-            rows_v = 1 if vocal_embeddings.shape[0] > 1 else B
+            # 1.3B: the projector runs on the last (full-condition) row only, the unconditional row gets
+            # zeros (1B:1004-1009); 14B: every row through the projector with its own audio (14B:1008)
+            rows_v = B if (self.VOCAL == "14B" or vocal_embeddings.shape[0] == 1) else 1
             voc_rows = []
             for r in range(rows_v):
                 src = B - 1 if rows_v == 1 else r
                 ops.cast_bf16(xfull[src * Lp:(src + 1) * Lp], lat_row)
                 vv, Fn, nper = self._vocal(pk, vocal_embeddings[src], video_sample_n_frames, lat_row, Lp,
                                            e0[src:src + 1], e[src:src + 1], dev)
+                if self.vd != dim:
+                    raise ValueError("vocal context width must equal the DiT width")
                 voc_rows.append(vv)
             assert Fn == n_fr
             if rows_v == 1:
@@ -725,6 +766,24 @@ class WanTransformer3DFantasyModel(nn.Module):
             out = torch.empty(B, self.out_dim, Fw, Hh, Ww, device=dev, dtype=torch.bfloat16)
         ops.unpatchify(ho, Lp, B, self.out_dim, Fw, Hh, Ww, out)
         return out
+
+
+class WanTransformer3DFantasy14BModel(WanTransformer3DFantasyModel):
+    """WanTransformer3DFantasy14BModel (wan_fantasy_transformer3d_14B.py:735-1178): the same DiT at the 14B
+    widths (wan_civitai 14B: dim 5120, 40 heads, 40 layers, ffn 13824) with the 14B vocal projector
+    (two-layer audio projection, width = dim, 8 heads of 640, run on every CFG row with its own audio,
+    14B:1008).  The reference's forward has no video_sample_n_frames (its vocal path hard-codes 81 video /
+    21 latent frames, 14B:1008-1010, vocal_projector_fantasy_14B.py:254), which is why its long pipeline
+    cannot drive it; here forward also accepts the 1.3B keyword and requires 81."""
+
+    VOCAL = "14B"
+
+    def forward_window(self, lat, frame_offset, broadcast, B, t, context, seq_len, clip_fea, y, vocal_embeddings,
+                       video_sample_n_frames=81, is_clip_level_modeling=False, out=None, cond_flag=True):
+        if video_sample_n_frames != 81:
+            raise ValueError("the 14B vocal path is built for 81-frame windows (21 latent frames, 14B:1008-1010)")
+        return super().forward_window(lat, frame_offset, broadcast, B, t, context, seq_len, clip_fea, y,
+                                      vocal_embeddings, 81, is_clip_level_modeling, out=out, cond_flag=cond_flag)
 
 
 def call_gemm_batched(cols, w, bias, xout, B, real, Lp, dim, kpad):

@@ -70,6 +70,29 @@ def gen_dit():
     np.savez_compressed(os.path.join(HERE, "dit_small.npz"), **out)
 
 
+def build_ref_dit14(cfg):
+    from wan.models.wan_fantasy_transformer3d_14B import WanTransformer3DFantasy14BModel
+    m = WanTransformer3DFantasy14BModel(model_type="i2v", patch_size=(1, 2, 2), text_len=cfg["text_len"],
+                                        in_dim=cfg["in_dim"], dim=cfg["dim"], ffn_dim=cfg["ffn_dim"],
+                                        freq_dim=cfg["freq_dim"], text_dim=cfg["text_dim"], out_dim=cfg["out_dim"],
+                                        num_heads=cfg["num_heads"], num_layers=cfg["num_layers"], qk_norm=True,
+                                        cross_attn_norm=True, eps=1e-6)
+    return load_synthetic(m.eval(), cfg["seed"])
+
+
+def gen_dit14():
+    """the 14B DiT at its full width (5120, 40 heads; vocal projector 5120 wide, 8 heads of 640) with
+    DIT14_SMALL's reduced depth / ffn / text width, on the 21-latent-frame window its vocal path
+    hard-codes (14B forward signature: no video_sample_n_frames)"""
+    from golden_cases import DIT14_SMALL, dit14_inputs
+    m = build_ref_dit14(DIT14_SMALL)
+    inp = dit14_inputs(DIT14_SMALL)
+    y = m(x=inp["x"], t=inp["t"], context=inp["context"], seq_len=inp["seq_len"], clip_fea=inp["clip_fea"],
+          y=inp["y"], vocal_embeddings=inp["vocal"], is_clip_level_modeling=False)
+    print("dit14", tuple(y.shape), float(y.abs().mean()))
+    np.savez_compressed(os.path.join(HERE, "dit14_small.npz"), out=y.numpy())
+
+
 def build_ref_vae(cfg):
     from wan.models.wan_vae import AutoencoderKLWan, _video_vae
     v = AutoencoderKLWan()
@@ -221,7 +244,14 @@ def gen_keys():
         t5 = WanT5EncoderModel(vocab=256384, dim=4096, dim_attn=4096, dim_ffn=10240, num_heads=64, num_layers=24,
                                num_buckets=32, shared_pos=False, dropout=0.0)  # wan_civitai.yaml:14-26
     clip = build_ref_clip_visual(dict(CLIP_SMALL, dim=1280, num_heads=16, num_layers=32))  # ViT-H/14
+    from wan.models.wan_fantasy_transformer3d_14B import WanTransformer3DFantasy14BModel
+    with torch.device("meta"):  # wan_civitai 14B widths (dim 5120, 40 heads, 40 layers, ffn 13824)
+        m14 = WanTransformer3DFantasy14BModel(model_type="i2v", patch_size=(1, 2, 2), text_len=512, in_dim=36,
+                                              dim=5120, ffn_dim=13824, freq_dim=256, text_dim=4096, out_dim=16,
+                                              num_heads=40, num_layers=40, qk_norm=True, cross_attn_norm=True,
+                                              eps=1e-6)
     out = {"dit_1_3b": {k: list(t.shape) for k, t in m.state_dict().items()},
+           "dit_14b": {k: list(t.shape) for k, t in m14.state_dict().items()},
            "vae": {k[len("model."):]: list(t.shape) for k, t in v.state_dict().items()},
            "umt5_xxl": {k: list(t.shape) for k, t in t5.state_dict().items()},
            "clip_visual_vit_h14": {"model.visual." + k: list(t.shape) for k, t in clip.state_dict().items()}}

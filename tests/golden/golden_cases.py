@@ -34,6 +34,25 @@ def dit_inputs(cfg, case="full"):
                 n_frames=n_frames)
 
 
+# the 14B DiT at full width (dim 5120, 40 heads of 128; vocal projector 5120 wide, 8 heads of 640) with one
+# layer, ffn 256 and text_dim 64 to keep the golden small; its vocal path hard-codes 21 latent frames
+DIT14_SMALL = dict(model_type="i2v", dim=5120, ffn_dim=256, freq_dim=256, text_dim=64, in_dim=36, out_dim=16,
+                   num_heads=40, num_layers=1, text_len=32, eps=1e-6, seed=13)
+
+
+def dit14_inputs(cfg):
+    """CFG batch of 3 on one 81-frame window: 21 latent frames at 4x4 (2x2 tokens per frame, seq_len 84),
+    161 wav2vec tokens (81 frames of 16 kHz audio); the 14B projector runs on all three audio rows."""
+    B, F, H, W = 3, 21, 4, 4
+    lat = synthetic.seeded_normal((1, 16, F, H, W), 111)
+    a = synthetic.seeded_normal((1, 161, 768), 116)
+    return dict(x=torch.cat([lat] * 3), y=synthetic.seeded_normal((B, 20, F, H, W), 112),
+                context=[synthetic.seeded_normal((20, cfg["text_dim"]), 113)] * 2
+                + [synthetic.seeded_normal((25, cfg["text_dim"]), 114)],
+                clip_fea=synthetic.seeded_normal((1, 257, 1280), 115).expand(3, -1, -1).contiguous(),
+                vocal=torch.cat([torch.zeros_like(a), a, a]), t=torch.full((3,), 937.5), seq_len=F * (H // 2) * (W // 2))
+
+
 VAE_SMALL = {"dim32_T3_8x8": dict(dim=32, seed=21, T=3, h=8, w=8),
              "dim96_T2_4x4": dict(dim=96, seed=22, T=2, h=4, w=4),
              "dim32_T1_6x4": dict(dim=32, seed=26, T=1, h=6, w=4)}  # one latent frame, non-square

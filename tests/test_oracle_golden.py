@@ -182,3 +182,29 @@ def test_encoder_keys_match_reference():
     t5 = oenc.t5_param_shapes(256384, 4096, 4096, 10240, 64, 24, 32, shared_pos=False)
     assert {k: list(v) for k, v in t5.items()} == ref["umt5_xxl"]
     assert {k: list(v) for k, v in oenc.clip_param_shapes().items()} == ref["clip_visual_vit_h14"]
+
+
+def test_dit14_keys_match_reference():
+    """the oracle's and the HIP module's 14B layouts == WanTransformer3DFantasy14BModel's state_dict at the
+    wan 14B widths (dim 5120, 40 heads, 40 layers, ffn 13824)"""
+    import json
+    from stableavatar_amd import transformer as T
+    with open(os.path.join(HERE, "golden", "ref_keys.json")) as f:
+        ref = json.load(f)["dit_14b"]
+    cfg = dict(model_type="i2v", dim=5120, ffn_dim=13824, freq_dim=256, text_dim=4096, in_dim=36, out_dim=16,
+               num_heads=40, num_layers=40, text_len=512, vocal="14B")
+    assert {k: list(v) for k, v in odit.param_shapes(cfg).items()} == ref
+    assert {k: list(v) for k, v in T.param_shapes(cfg).items()} == ref
+
+
+def test_dit14_forward_vs_reference():
+    """the oracle's 14B forward (two-layer audio projection, 5120-wide vocal projector with 8 heads of 640
+    run on every CFG row) vs the reference module at full width, one layer"""
+    from golden_cases import DIT14_SMALL, dit14_inputs
+    cfg = dict(DIT14_SMALL, vocal="14B")
+    P = synthetic.fill_state_dict(odit.param_shapes(cfg), cfg["seed"])
+    inp = dit14_inputs(cfg)
+    with torch.no_grad():
+        y = odit.forward(P, cfg, inp["x"], inp["t"], inp["context"], inp["seq_len"], inp["clip_fea"], inp["y"],
+                         inp["vocal"], 81)
+    assert rel(y, G("dit14_small.npz")["out"]) < 1e-5

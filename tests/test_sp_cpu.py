@@ -69,9 +69,10 @@ def _worker(rank, world, port, B, Lp, H, D, q_ret):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3, 4, 8])
-def test_ulysses_exchange_matches_full_attention(world):
-    B, H, D = 3, 12, 16
+@pytest.mark.parametrize("world,H", [(2, 12), (3, 12), (4, 12), (8, 12), (8, 40)])
+def test_ulysses_exchange_matches_full_attention(world, H):
+    """12 heads: the 1.3B model (N = 8 is U4 x 2 query parts); 40 heads: the 14B model (N = 8 is U8)"""
+    B, D = 3, 16
     Lp = sp.padded_len(48, world)
     ctx = mp.get_context("spawn")
     qret = ctx.Queue()
@@ -92,6 +93,7 @@ def test_plan_shapes():
     assert (sp.make_plan(8, 5, 12).G, sp.make_plan(8, 5, 12).R) == (4, 2)
     assert (sp.make_plan(2, 1, 12).G, sp.make_plan(2, 1, 12).R) == (2, 1)
     assert (sp.make_plan(4, 0, 12).G, sp.make_plan(4, 0, 12).R) == (4, 1)
+    assert (sp.make_plan(8, 3, 40).G, sp.make_plan(8, 3, 40).R) == (8, 1)  # 14B: Ulysses 8
     assert sp.padded_len(21504, 8) == 21504 and sp.padded_len(21505, 8) == 21512
 
 
