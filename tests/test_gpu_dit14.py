@@ -81,3 +81,50 @@ def test_dit14_requires_81_frame_windows(model14):
         m(x=inp["x"].cuda(), t=inp["t"].cuda(), context=[c.cuda() for c in inp["context"]], seq_len=inp["seq_len"],
           clip_fea=inp["clip_fea"].cuda(), y=inp["y"].cuda(), vocal_embeddings=inp["vocal"].cuda(),
           video_sample_n_frames=17)
+
+
+def test_pipeline_denoise_drives_14b(model14):
+    """WanI2VTalkingInferenceLongPipeline.denoise on the 14B model (the reference's pipeline cannot call it,
+    SURVEY.md App. A.9): 22 latent frames -> windows (0, 21), (6, 22) at overlap 15 (the second one shorter
+    and padded), 2 steps (the blend runs at step 1), vs the oracle loop (oracle/pipeline.py) on the oracle
+    14B forward"""
+    import math
+
+    from oracle import dit as odit
+    from oracle import pipeline as opipe
+    from stableavatar_amd.pipeline import WanI2VTalkingInferenceLongPipeline, audio_window, window_schedule
+    from stableavatar_amd.scheduler import FlowMatchEulerDiscreteScheduler
+    m, cfg, P = model14
+    T, H, W, steps, overlap, clip_length = 22, 4, 4, 2, 15, 81
+    lat0 = synthetic.seeded_normal((1, 16, T, H, W), 131).bfloat16()
+    y = synthetic.seeded_normal((3, 20, 21, H, W), 132)  # the window conditioning (clip_length frames)
+    audio = synthetic.seeded_normal((((T - 1) * 4 + 1) * 640,), 133, 0.1)
+    inp = dit14_inputs(cfg)
+    ctx = inp["context"]
+    clip = inp["clip_fea"]
+    sched = FlowMatchEulerDiscreteScheduler(1000, shift=5.0)
+    sched.set_timesteps(steps, device="cuda")
+    pipe = WanI2VTalkingInferenceLongPipeline(transformer=m, scheduler=sched)
+    fpb = (clip_length - 1) // 4 + 1
+    feats = {}
+    for (s, e, _) in window_schedule(T, fpb, overlap):
+        a = synthetic.fake_wav2vec_features(audio[audio_window(s, e, T, 640, audio.shape[0])][None]).cuda()
+        feats[(s, e)] = torch.cat([torch.zeros_like(a), a, a])
+    seq_len = math.ceil(W * H / 4 * fpb)
+    with torch.no_grad():
+        out = pipe.denoise(lat0.cuda(), y.cuda().bfloat16(), [c.cuda() for c in ctx], clip.cuda(), feats,
+                           sched.timesteps, sched.sigmas, clip_length=clip_length, seq_len=seq_len, overlap=overlap,
+                           text_guide_scale=3.0, audio_guide_scale=5.0)
+    torch.cuda.synchronize()
+
+    def dit(x, t, context, sl, yy, clip_fea, vocal, n):
+        return odit.forward(P, cfg, x.float(), t, context, sl, clip_fea, yy.float(), vocal, n)
+
+    with torch.no_grad():
+        ref = opipe.denoise(dit, lat0.float(), y.bfloat16(), ctx, clip, audio,
+                            lambda smp: synthetic.fake_wav2vec_features(smp[None]), num_inference_steps=steps,
+                            clip_length=clip_length, num_frames=clip_length, height=H * 8, width=W * 8,
+                            overlap=overlap, text_guide_scale=3.0, audio_guide_scale=5.0)
+    e = rel(out.float(), ref)
+    print(f"14B pipeline denoise (2 windows x 2 steps) vs oracle loop: rel-L2 {e:.2e}")
+    assert e < 3e-2, e
