@@ -485,78 +485,67 @@ __device__ __forceinline__ void s5_half(const S5Ctx& c, f32x4 (&acc)[8][8], u32x
 constexpr int S7_STRIP = 16 * 68 * 4;             // [16 rows][64 (+4) cols] fp32 per wave
 constexpr int S7_LDS = S5_LDS + 4 * S7_STRIP;     // 145 KB
 
-// gated-residual epilogue of an interior tile: the residual / gate rows of the 16 (row block, column
-// half) steps are loaded S7_RES_AHEAD steps ahead (the fragment registers are dead here), bias once per
-// column half, so the residual's HBM latency is paid about once per tile instead of once per step
-constexpr int S7_RES_AHEAD = 2;
-// TILE_GATE: every row of the tile reads the same gate row (no gate, or the tile lies inside one CFG
-// row's token range, e.g. 21 504 = 84 x 256): the gate is loaded once per column half like the bias,
-// and the freed registers deepen the residual prefetch to AHEAD = 3 steps
-template <int AHEAD, bool TILE_GATE>
-__device__ __forceinline__ void s7_res_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8], float* strip, int wm, int wn,
-                                                int fr, int fc, int er, int ec, int m0, int n0, long bz) {
-  f32x4 bias_h[2][4];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      bias_h[h][q] = g.bias ? *(const f32x4*)(g.bias + n0 + wn * 128 + h * 64 + ec + 4 * q) : (f32x4){0.f, 0.f, 0.f, 0.f};
-  f32x4 gate_h[TILE_GATE ? 2 : 1][4];
-  if constexpr (TILE_GATE) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        gate_h[h][q] = g.gate ? *(const f32x4*)(g.gate + (long)(m0 / g.rows_per_batch) * g.gate_bstride + n0 +
-                                                wn * 128 + h * 64 + ec + 4 * q)
-                              : (f32x4){1.f, 1.f, 1.f, 1.f};
-  }
-  f32x4 rb[AHEAD][4], gb[TILE_GATE ? 1 : AHEAD][4];
-  auto fetch = [&](int k, int slot) {
-    const int i = k >> 1, h = k & 1;
-    const int row = m0 + wm * 128 + i * 16 + er;
-    const int col = n0 + wn * 128 + h * 64 + ec;
-    const float* R = g.R + bz * g.sR + (long)row * g.ldr + col;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) rb[slot][q] = *(const f32x4*)(R + 4 * q);
-    if constexpr (!TILE_GATE) {
-      if (g.gate) {
-        const float* G = g.gate + (long)(row / g.rows_per_batch) * g.gate_bstride + col;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) gb[slot][q] = *(const f32x4*)(G + 4 * q);
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) gb[slot][q] = (f32x4){1.f, 1.f, 1.f, 1.f};
-      }
-    }
+// fp32-output epilogue of an interior tile (gated residual, plain f32, SiLU) straight from the accumulators:
+// lane (fr, fc) of wave (wm, wn) holds, in acc[i][j], row m0 + wm*128 + i*16 + fr, columns n0 + wn*128 +
+// j*16 + fc*4 + 0..3, so each (i, j) is one 16-byte store per lane with no LDS round trip.  Walked column
+// group j outer, row block i inner (step s = 8 j + i): the bias (and the tile's gate row, TILE_GATE) of
+// column group j is loaded two groups ahead, the residual (and the per-row gate) AH steps ahead.  a0/b0
+// hold the next tile's first fragments here, which caps AH.  Measured against the LDS-strip path (same
+// box, interleaved, profiles/r02/gemm_epilogue_study.md): O-proj 0.440 vs 0.447 ms, FFN-down 1.474 vs
+// 1.486 ms, 30-layer DiT forward 396.7 vs 398.7 ms; for bf16 outputs the strip path's 16-byte row
+// segments stay faster (QKV 0.80 vs 0.94 ms), so those keep it.
+template <int EPI, bool TILE_GATE>
+__device__ __forceinline__ void s7_f32_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8], int wm, int wn, int fr, int fc,
+                                                int m0, int n0, long bz) {
+  constexpr bool RES = EPI == EPI_RES_F32;
+  constexpr bool PER_ROW_GATE = RES && !TILE_GATE;
+  constexpr int AH = RES ? (PER_ROW_GATE ? 4 : 8) : 1;
+  const int col = n0 + wn * 128 + fc * 4;  // + j * 16
+  const int row0 = m0 + wm * 128 + fr;     // + i * 16
+  const float* tgate = (TILE_GATE && RES && g.gate) ? g.gate + (long)(m0 / g.rows_per_batch) * g.gate_bstride : nullptr;
+  f32x4 bj[3], gj[3], rb[AH], gb[PER_ROW_GATE ? AH : 1];
+  auto fetch_col = [&](int j) {
+    bj[j % 3] = g.bias ? *(const f32x4*)(g.bias + col + j * 16) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    if constexpr (RES && TILE_GATE) gj[j % 3] = tgate ? *(const f32x4*)(tgate + col + j * 16) : (f32x4){1.f, 1.f, 1.f, 1.f};
   };
+  auto fetch = [&](int st) {
+    const int i = st & 7, j = st >> 3;
+    if constexpr (RES) rb[st % AH] = *(const f32x4*)(g.R + bz * g.sR + (long)(row0 + i * 16) * g.ldr + col + j * 16);
+    if constexpr (PER_ROW_GATE)
+      gb[st % AH] = *(const f32x4*)(g.gate + (long)((row0 + i * 16) / g.rows_per_batch) * g.gate_bstride + col + j * 16);
+  };
+  fetch_col(0);
+  fetch_col(1);
+  if constexpr (RES) {
 #pragma unroll
-  for (int k = 0; k < AHEAD; ++k) fetch(k, k);
+    for (int st = 0; st < AH; ++st) fetch(st);
+  }
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int i = k >> 1, h = k & 1, slot = k % AHEAD;
+  for (int j = 0; j < 8; ++j) {
+    if (j + 2 < 8) fetch_col(j + 2);
+    // one column group at a time: its accumulators are read from the AGPRs only here (keeps the
+    // compiler from hoisting all 256 reads into VGPRs) and no store crosses this point
+    asm volatile("" : "+a"(acc[0][j]), "+a"(acc[1][j]), "+a"(acc[2][j]), "+a"(acc[3][j]), "+a"(acc[4][j]),
+                      "+a"(acc[5][j]), "+a"(acc[6][j]), "+a"(acc[7][j])::"memory");
 #pragma unroll
-    for (int j = 0; j < 4; ++j) *(f32x4*)(strip + fr * 68 + j * 16 + fc * 4) = acc[i][4 * h + j];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    f32x4 v[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = *(const f32x4*)(strip + er * 68 + ec + q * 4);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    float* C = (float*)g.C + bz * g.sC + (long)(m0 + wm * 128 + i * 16 + er) * g.ldc + n0 + wn * 128 + h * 64 + ec;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      f32x4 o;
+    for (int i = 0; i < 8; ++i) {
+      const int st = j * 8 + i;
+      f32x4 v = acc[i][j];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float t = bf2f(f2bf(v[q][e] + bias_h[h][q][e]));  // bf16 Linear output (reference autocast)
-        const float gt = TILE_GATE ? gate_h[TILE_GATE ? h : 0][q][e] : gb[TILE_GATE ? 0 : slot][q][e];
-        o[e] = rb[slot][q][e] + t * gt;
+        float t = v[e] + bj[j % 3][e];
+        // the reference's nn.Linear returns bf16 under autocast; the gated residual (1B:677-678,688-690)
+        // consumes that rounded value
+        if constexpr (RES) t = bf2f(f2bf(t));
+        if constexpr (EPI == EPI_SILU_F32) t = silu(t);
+        if constexpr (RES) t = rb[st % AH][e] + t * (TILE_GATE ? gj[j % 3][e] : gb[PER_ROW_GATE ? st % AH : 0][e]);
+        v[e] = t;
       }
-      *(f32x4*)(C + 4 * q) = o;
+      *(f32x4*)((float*)g.C + bz * g.sC + (long)(row0 + i * 16) * g.ldc + col + j * 16) = v;
+      if constexpr (RES) {
+        if (st + AH < 64) fetch(st + AH);
+      }
     }
-    if (k + AHEAD < 16) fetch(k + AHEAD, slot);
   }
 }
 
@@ -566,12 +555,12 @@ __device__ __forceinline__ void s7_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8
   const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fc = lane >> 4;
   float* strip = (float*)(smem + S5_LDS + wave * S7_STRIP);
   const int er = lane >> 2, ec = (lane & 3) * 16;
-  if constexpr (EPI == EPI_RES_F32) {
-    if (m0 + BM <= g.M && n0 + BN <= g.N) {  // wave-uniform
-      if (!g.gate || m0 / g.rows_per_batch == (m0 + BM - 1) / g.rows_per_batch)
-        s7_res_epilogue<3, true>(g, acc, strip, wm, wn, fr, fc, er, ec, m0, n0, bz);
+  if constexpr (EPI == EPI_RES_F32 || EPI == EPI_F32 || EPI == EPI_SILU_F32) {
+    if (m0 + BM <= g.M && n0 + BN <= g.N) {  // interior tile (wave-uniform)
+      if (EPI != EPI_RES_F32 || !g.gate || m0 / g.rows_per_batch == (m0 + BM - 1) / g.rows_per_batch)
+        s7_f32_epilogue<EPI, true>(g, acc, wm, wn, fr, fc, m0, n0, bz);
       else
-        s7_res_epilogue<S7_RES_AHEAD, false>(g, acc, strip, wm, wn, fr, fc, er, ec, m0, n0, bz);
+        s7_f32_epilogue<EPI, false>(g, acc, wm, wn, fr, fc, m0, n0, bz);
       return;
     }
   }
