@@ -50,6 +50,8 @@ def parse(argv=None):
                    help="sampling steps of the config-1 CPU oracle run actually executed (1..5; the rest of the 5 "
                         "are extrapolated from the measured per-step time; 5 = fully end to end)")
     p.add_argument("--no-encode", action="store_true", help="skip the (untimed) VAE encode measurement")
+    p.add_argument("--no-dit14", action="store_true",
+                   help="skip the (untimed) per-block measurement of the 14B model at config 4's 720p geometry")
     p.add_argument("--mode", choices=("sp", "replicas", "window-dp"), default=None,
                    help="N>1 layout (default sp); ignored at N=1")
     p.add_argument("--sp", action="store_true", help="alias of --mode sp")
@@ -397,6 +399,13 @@ def run(args, world, rank, dev, work_factory=ClipWorkload):
     enc = None
     if not args.no_encode and rank == 0 and hasattr(work, "vae"):
         enc = vae_encode_ms(work.vae, args.frames, args.size, dev)
+    dit14 = None
+    if world == 1 and not args.no_dit14 and hasattr(work, "dit"):
+        from stableavatar_amd.kbench import bench_dit14
+        dit14 = dict(bench_dit14(), note="BASELINE config 4's model (Wan-14B StableAvatar widths: dim 5120, 40 heads, "
+                                         "ffn 13824) at 720x1280, 81 frames (L = 75 600, B = 3) on one GPU: forwards "
+                                         "with 1 and 2 blocks, one block's time from their difference, the 40-block "
+                                         "forward projected; outside the timed region and the metric")
     if rank != 0:
         return None
     traffic, traffic_src = attn_traffic(seq_len, layout)
@@ -424,7 +433,7 @@ def run(args, world, rank, dev, work_factory=ClipWorkload):
                         "algorithmic_bytes": 4 * 3 * seq_len * 1536 * 2,
                         "launch_ms": round(attn_ms, 3) if attn_ms else None, "flop_per_launch": attn_flop},
            "path_mfma_frac": round(path_flop * args.steps / dt / PEAK_BF16 / (world if shared else 1), 4),
-           "cpu_baseline": cpu, "vae_encode": enc}
+           "cpu_baseline": cpu, "vae_encode": enc, "config_4_dit14": dit14}
     if replicas is not None:
         out["replicas"] = replicas
     return out

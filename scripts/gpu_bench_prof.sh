@@ -11,5 +11,5 @@ fi
 scripts/gpustep.sh 900 gpurun_out/bench_$tag.log python -u bench.py; rc=$?; echo "bench rc=$rc"
 tail -2 gpurun_out/bench_$tag.log; [ $rc -ne 0 ] && exit $rc
 export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-encode > gpurun_out/prof_$tag.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-encode --no-dit14 > gpurun_out/prof_$tag.log 2>&1
 rc=$?; echo "prof rc=$rc"; exit $rc
