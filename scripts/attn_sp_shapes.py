@@ -20,9 +20,11 @@ for N, hg, R in ((1, 12, 1), (2, 6, 1), (4, 3, 1), (8, 3, 2)):
     kv = torch.randn(B * L, 2 * hg * D, device="cuda").bfloat16()
     o = torch.empty_like(q)
     segs = torch.tensor([[b * Lq, Lq, b * L, L] for b in range(B)], dtype=torch.int32, device="cuda")
-    ms = _time(lambda: ops.attention(q, kv[:, :hg * D], kv[:, hg * D:], o, segs, B, Lq, hg), iters=5, warmup=2)
-    base = base or ms
-    res[f"N{N}"] = {"ms": round(ms, 3), "ideal_ms": round(base / N, 3), "workgroups": B * hg * -(-Lq // 256),
-                    "efficiency": round(base / N / ms, 3)}
+    t = {k_: _time(lambda: ops.attention(q, kv[:, :hg * D], kv[:, hg * D:], o, segs, B, Lq, hg, kernel=k_),
+                   iters=5, warmup=2) for k_ in (1, 2, 0)}  # 256-row, 128-row workgroups, auto
+    base = base or t[1]
+    res[f"N{N}"] = {"ms_wg256": round(t[1], 3), "ms_wg128": round(t[2], 3), "ms_auto": round(t[0], 3),
+                    "ideal_ms": round(base / N, 3), "workgroups_256": B * hg * -(-Lq // 256),
+                    "efficiency_auto": round(base / N / t[0], 3)}
     del q, kv, o
 print(json.dumps(res), flush=True)

@@ -656,14 +656,22 @@ __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2]
   }
 }
 
-__global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) {
+namespace {
+
+// NW = 8: 256 query rows per workgroup, waves w and w+4 share a SIMD (one workgroup per CU); NW = 4: 128
+// query rows, one wave per SIMD, two workgroups per CU -- the same per-SIMD pairing at half the work
+// granularity, for launches whose 256-row workgroup count leaves the last round over the CUs mostly empty
+// (the per-rank shapes of Ulysses SP: 378 workgroups at N = 8)
+template <int NW>
+__device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
+  constexpr int QBW = NW * 32, PPW = 16 / NW;  // query rows per workgroup, K (and V) 1-KB pieces per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nx = gridDim.x, ny = gridDim.y;
   const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
   const int qb = flat % nx, h = (flat / nx) % ny, seg = flat / (nx * ny);
   const int* sg = a.segs + seg * 4;
   const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
-  if (qb * QB >= q_len || kv_len <= 0) return;
+  if (qb * QBW >= q_len || kv_len <= 0) return;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
@@ -672,7 +680,7 @@ __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) {
   bf16x8 qf[2][4];
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
-    const int qc = min(qb * QB + wave * 32 + qt * 16 + r16, q_len - 1);
+    const int qc = min(qb * QBW + wave * 32 + qt * 16 + r16, q_len - 1);
     const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * g;
 #pragma unroll
     for (int dc = 0; dc < 4; ++dc) {
@@ -692,18 +700,18 @@ __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) {
       (void*)(a.k + (long)kv_row0 * a.ks + h * D), (short)0, (int)(((long)kv_len - 1) * a.ks * 2 + 256), 0x00020000);
   const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.v + (long)kv_row0 * a.vs + h * D), (short)0, (int)(((long)kv_len - 1) * a.vs * 2 + 256), 0x00020000);
-  int koff[2], voff[2];
+  int koff[PPW], voff[PPW];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int srow = (wave * 2 + i) * 4 + (lane >> 4);
+  for (int i = 0; i < PPW; ++i) {
+    const int srow = (wave * PPW + i) * 4 + (lane >> 4);
     koff[i] = srow * (int)a.ks * 2 + ((r16 ^ (srow & 15)) << 4);
     voff[i] = srow * (int)a.vs * 2 + ((r16 ^ ((srow & 7) << 1)) << 4);
   }
-  const uint32_t lds_dma = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + wave * 2048);
+  const uint32_t lds_dma = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + wave * PPW * 1024);
   auto stage = [&](int kb, int buf) {
     const int ks_off = kb * KVB * (int)a.ks * 2, vs_off = kb * KVB * (int)a.vs * 2;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < PPW; ++i) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, LDS_PTR((uintptr_t)(lds_dma + buf * STAGE_BYTES + i * 1024)), 16,
                                                koff[i], ks_off, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -737,7 +745,7 @@ __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) {
 
   const int nkb = (kv_len + KVB - 1) / KVB;
   stage(0, 0);
-  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  if (NW == 8 && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
   for (int kb = 0; kb < nkb; kb += 2) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -755,7 +763,7 @@ __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) {
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const float inv = 1.0f / st.L[qt][0];
-    const int qi = qb * QB + wave * 32 + qt * 16 + r16;
+    const int qi = qb * QBW + wave * 32 + qt * 16 + r16;
     bf16* op = a.o + (long)(q_row0 + min(qi, q_len - 1)) * a.os + h * D + 4 * (g & ~1) + 16 * (g & 1);
 #pragma unroll
     for (int dt = 0; dt < 8; dt += 2) {
@@ -780,7 +788,16 @@ __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) {
   }
 }
 
-// kernel: 0 = auto, 1 = attn_fwd_v6_kernel (8 waves x 32 queries, mfma_f32_16x16x32_bf16)
+__global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) { attn_fwd_v6_body<8>(a); }
+__global__ __launch_bounds__(256, 2) void attn_fwd_v6_w4_kernel(AttnArgs a) { attn_fwd_v6_body<4>(a); }
+
+}  // namespace
+
+// kernel: 0 = auto, 1 = attn_fwd_v6_kernel (8 waves x 32 queries, mfma_f32_16x16x32_bf16), 2 = the 4-wave
+// attn_fwd_v6_w4_kernel (two workgroups per CU).  Auto estimates both launches in rounds of one 8-wave
+// workgroup per CU: a 4-wave round holds two workgroups per CU and runs 3 % slower per FLOP; a last 4-wave
+// round of at most one workgroup per CU (one wave per SIMD) takes 0.75 of a round (measured,
+// profiles/r02/attn_sp_shapes.json: the Ulysses N = 8 shape, 378 / 756 workgroups, 1.036 vs 0.927 ms).
 extern "C" int sa_attn_fwd_ex(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
                               int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride,
                               int64_t v_stride, int64_t o_stride, float scale, int accumulate, int kernel,
@@ -789,16 +806,36 @@ extern "C" int sa_attn_fwd_ex(const void* q, const void* k, const void* v, void*
   if (head_dim != D) return SA_ERR_ARG;
   if ((q_stride | k_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
   if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)o)) & 15) return SA_ERR_ARG;
-  if (kernel < 0 || kernel > 1) return SA_ERR_ARG;
+  if (kernel < 0 || kernel > 2) return SA_ERR_ARG;
   static const bool attr = [] {  // one-time, thread-safe
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_v6_w4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
     return true;
   }();
   (void)attr;
   AttnArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, segs,
              q_stride, k_stride, v_stride, o_stride, scale * 1.4426950408889634f, accumulate};
-  dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
-  hipLaunchKernelGGL(attn_fwd_v6_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+  if (kernel == 0) {
+    static int cus[64] = {0};  // per device, queried once
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+      if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus[dev] = 256;
+      ncu = cus[dev] > 0 ? cus[dev] : 256;
+    }
+    const long n8 = (long)nseg * heads * ((max_q_len + 255) / 256), n4 = (long)nseg * heads * ((max_q_len + 127) / 128);
+    const long t8 = (n8 + ncu - 1) / ncu, full = n4 / (2 * ncu), rem = n4 % (2 * ncu);
+    const double t4 = 1.03 * (full + (rem == 0 ? 0.0 : (rem <= ncu ? 0.75 : 1.0)));
+    kernel = t4 < (double)t8 ? 2 : 1;
+  }
+  if (kernel == 2) {
+    dim3 grid((max_q_len + 127) / 128, heads, nseg);
+    hipLaunchKernelGGL(attn_fwd_v6_w4_kernel, grid, dim3(256), LDS_BYTES, (hipStream_t)stream, a);
+  } else {
+    dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
+    hipLaunchKernelGGL(attn_fwd_v6_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+  }
   SA_LAUNCH_CHECK();
   return SA_OK;
 }

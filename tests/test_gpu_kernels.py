@@ -108,8 +108,9 @@ def _ref_attn(q, k, v, scale):
     return torch.softmax(s, -1) @ v.float()
 
 
+@pytest.mark.parametrize("kernel", [1, 2], ids=["wg256", "wg128"])
 @pytest.mark.parametrize("Lq,Lk", [(300, 300), (512, 257), (1024, 17), (64, 512)])
-def test_attention_segments(Lq, Lk):
+def test_attention_segments(Lq, Lk, kernel):
     from stableavatar_amd import ops
     B, H, D = 2, 3, 128
     q = torch.randn(B * Lq, H * D + 64, device=dev).bfloat16()[:, :H * D]  # strided rows
@@ -117,7 +118,7 @@ def test_attention_segments(Lq, Lk):
     v = torch.randn(B * Lk, H * D, device=dev).bfloat16()
     o = torch.empty(B * Lq, H * D, device=dev, dtype=torch.bfloat16)
     segs = torch.tensor([[b * Lq, Lq, b * Lk, Lk] for b in range(B)], dtype=torch.int32, device=dev)
-    ops.attention(q, k, v, o, segs, B, Lq, H)
+    ops.attention(q, k, v, o, segs, B, Lq, H, kernel=kernel)
     for b in range(B):
         for h in range(H):
             ref = _ref_attn(q[b * Lq:(b + 1) * Lq, h * D:(h + 1) * D], k[b * Lk:(b + 1) * Lk, h * D:(h + 1) * D],
@@ -125,7 +126,7 @@ def test_attention_segments(Lq, Lk):
             assert rel(o[b * Lq:(b + 1) * Lq, h * D:(h + 1) * D], ref) < 1e-2, (b, h)
     # accumulate mode adds onto the existing output
     o2 = o.clone()
-    ops.attention(q, k, v, o2, segs, B, Lq, H, accumulate=True)
+    ops.attention(q, k, v, o2, segs, B, Lq, H, accumulate=True, kernel=kernel)
     assert rel(o2, 2 * o.float()) < 1e-2
 
 
