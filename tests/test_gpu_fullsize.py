@@ -173,6 +173,40 @@ def test_dit_block_fullsize_vs_oracle():
     assert e < 2e-2 and cos > 0.9995, (e, cos)
 
 
+@pytest.mark.timeout(600)
+def test_dit_ragged_nonsquare_vs_oracle():
+    """A non-square size whose token counts align with nothing: 240x416 video (30x52 latent, 15x26 = 390
+    tokens per frame, L = 8 190 over 21 frames): partial last query / key blocks in self-attention, the
+    3-launch cross-attention (frames are not 256-token aligned) with per-frame vocal segments of 390
+    query rows, 1 full-width layer, vs the CPU oracle"""
+    from oracle import dit as odit
+    from stableavatar_amd.transformer import WanTransformer3DFantasyModel, param_shapes
+    cfg = dict(DIT_FULL, num_layers=1)
+    P = synthetic.fill_state_dict(param_shapes(cfg), 52)
+    m = WanTransformer3DFantasyModel(**cfg)
+    m.load_state_dict(P)
+    m = m.to(dev)
+    lat = synthetic.seeded_normal((1, 16, 21, 30, 52), 511)
+    x = torch.cat([lat] * 3)
+    y = synthetic.seeded_normal((3, 20, 21, 30, 52), 512)
+    ctx = [synthetic.seeded_normal((24, 4096), 513)] * 2 + [synthetic.seeded_normal((31, 4096), 514)]
+    clip = synthetic.seeded_normal((1, 257, 1280), 515).expand(3, -1, -1).contiguous()
+    a = synthetic.seeded_normal((1, 161, 768), 516)
+    voc = torch.cat([torch.zeros_like(a), a, a])
+    t = torch.full((3,), 512.0)
+    Lr = 21 * 15 * 26
+    with torch.no_grad():
+        out = m(x=x.to(dev).bfloat16(), t=t.to(dev), context=[c.to(dev) for c in ctx], seq_len=Lr,
+                clip_fea=clip.to(dev), y=y.to(dev).bfloat16(), vocal_embeddings=voc.to(dev),
+                video_sample_n_frames=81).float().cpu()
+        torch.set_num_threads(min(16, os.cpu_count() or 1))
+        ref = odit.forward(P, cfg, x, t, ctx, Lr, clip, y, voc, 81)
+    e = rel(out, ref)
+    cos = torch.nn.functional.cosine_similarity(out.flatten().double(), ref.flatten().double(), dim=0).item()
+    print(f"DiT 240x416 (L={Lr}): rel-L2 {e:.2e}, cosine {cos:.6f}")
+    assert out.shape == ref.shape and e < 2e-2 and cos > 0.9995, (e, cos)
+
+
 def _drop_in_pipeline(P):
     from stableavatar_amd.pipeline import WanI2VTalkingInferenceLongPipeline
     from stableavatar_amd.scheduler import FlowMatchEulerDiscreteScheduler
