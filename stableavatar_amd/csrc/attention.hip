@@ -117,28 +117,33 @@ __device__ __forceinline__ bf16x8 pslice(const f32x16& S, int s) {
   return pb;
 }
 
+// non-canonicalising f32 max (MFMA outputs are never signalling NaNs): fmaxf makes hipcc insert a
+// v_max_f32 x, x canonicalisation per operand (MI355X_MICROARCH.md, App. B attention pitfalls)
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float vmax2(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 struct V3State {
   f32x16 O[4];
-  float m_run, l_run;
-  f32x16 negm;  // -m broadcast (NEGM blocks only)
+  float m_run, l_run;  // running max (log2 units, c·S) and row sum of this lane's query
 };
 
-// NEGM (cdna_hip_programming.md App. B "row constants as the initial accumulator"): Q is prescaled
-// by c = scale·log2(e) and the QK^T chain starts from -m (st.negm), so S' = c·S - m comes out of the
-// MFMA and p = exp2(S') needs no VALU subtract; the row max runs relative to m.
-template <int BUF, bool NEGM = false>
+// one 64-key block of the cross-attention streams: S^T = K Q^T on mfma_f32_32x32x16_bf16 (lane = query,
+// hi = key half), online softmax with a deferred rescale (RESCALE_THR), O^T += V^T P^T
+template <int BUF>
 __device__ __forceinline__ void attn_v3_block(V3State& st, const bf16x8* qf, const uint32_t* ka, const uint32_t* va,
                                               int kb, int kv_len, float c, int hi) {
   // S^T[key][query] = K · Q^T, K fragments two groups ahead
   u32x4 ka0[4], ka1[4], kb0[4], kb1[4];
   f32x16 S[2];
-  if constexpr (NEGM) {
-    S[0] = st.negm;
-    S[1] = st.negm;
-  } else {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) { S[0][r] = 0.f; S[1][r] = 0.f; }
-  }
+  for (int r = 0; r < 16; ++r) { S[0][r] = 0.f; S[1][r] = 0.f; }
   read_k4<BUF, 0, 0>(ka0, ka);
   read_k4<BUF, 0, 4>(ka1, ka);
   read_k4<BUF, 1, 0>(kb0, ka);
@@ -165,42 +170,6 @@ __device__ __forceinline__ void attn_v3_block(V3State& st, const bf16x8* qf, con
         if (key >= kv_len) S[t][r] = -INFINITY;
       }
   }
-  if constexpr (NEGM) {
-    float mx = S[0][0];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[t][r]);
-    {
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));  // max of c·S - m over the block
-    }
-    const bool first = kb == 0;
-    if (first || !__all(mx <= RESCALE_THR)) {  // wave-uniform; the first block sets m exactly
-      const float delta = first ? mx : fmaxf(mx, 0.f);
-      const float alpha = __builtin_amdgcn_exp2f(-delta);
-      st.l_run *= alpha;
-#pragma unroll
-      for (int db = 0; db < 4; ++db)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) st.O[db][r] *= alpha;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        st.negm[r] -= delta;
-        S[0][r] -= delta;
-        S[1][r] -= delta;
-      }
-    }
-    float ps0 = 0.f, ps1 = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      S[0][r] = __builtin_amdgcn_exp2f(S[0][r]);
-      S[1][r] = __builtin_amdgcn_exp2f(S[1][r]);
-      ps0 += S[0][r];
-      ps1 += S[1][r];
-    }
-    st.l_run += ps0 + ps1;
-  } else {
   float mx = S[0][0];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -227,7 +196,6 @@ __device__ __forceinline__ void attn_v3_block(V3State& st, const bf16x8* qf, con
       ps += p;
     }
   st.l_run += ps;
-  }
 
   // O^T[d][query] += V^T · P^T, slice g = 2t + s
   wait_v<8>(v0);
@@ -529,18 +497,6 @@ struct V6State {
   f32x4 negm4[2];  // the same as the QK^T chains' initial accumulator (refreshed only on a rescale)
 };
 
-// non-canonicalising f32 max (MFMA outputs are never signalling NaNs): fmaxf makes hipcc insert a
-// v_max_f32 x, x canonicalisation per operand (MI355X_MICROARCH.md, App. B attention pitfalls)
-__device__ __forceinline__ float vmax3(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-__device__ __forceinline__ float vmax2(float a, float b) {
-  float r;
-  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
 // max over 16 values of one query's S^T column slice, then over the 4 lane groups (permlane32 / 16 swaps)
 __device__ __forceinline__ float rowmax64(const f32x4 (&S)[4][2], int qt) {
   float m = vmax3(S[0][qt][0], S[0][qt][1], S[0][qt][2]);
@@ -555,6 +511,22 @@ __device__ __forceinline__ float rowmax64(const f32x4 (&S)[4][2], int qt) {
   m = vmax2(__uint_as_float(a[0]), __uint_as_float(a[1]));
   const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
   return vmax2(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+// max over this lane's 32 scores (both query tiles)
+__device__ __forceinline__ float lanemax32(const f32x4 (&S)[4][2]) {
+  float m = vmax3(S[0][0][0], S[0][0][1], S[0][0][2]);
+  m = vmax3(m, S[0][0][3], S[0][1][0]);
+  m = vmax3(m, S[0][1][1], S[0][1][2]);
+  m = vmax3(m, S[0][1][3], S[1][0][0]);
+#pragma unroll
+  for (int kt = 1; kt < 4; ++kt) {
+    m = vmax3(m, S[kt][0][1], S[kt][0][2]);
+    m = vmax3(m, S[kt][0][3], S[kt][1][0]);
+    m = vmax3(m, S[kt][1][1], S[kt][1][2]);
+    m = (kt < 3) ? vmax3(m, S[kt][1][3], S[kt + 1][0][0]) : vmax2(m, S[kt][1][3]);
+  }
+  return m;
 }
 
 template <int BUF>
@@ -592,13 +564,15 @@ __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2]
       for (int i = 0; i < 4; ++i)
         if (kb * KVB + kt * 16 + 4 * g + i >= kv_len) { S[kt][0][i] = -INFINITY; S[kt][1][i] = -INFINITY; }
   }
-  float mx[2];
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    mx[qt] = rowmax64(S, qt);  // max of c S - m over the block's 64 keys
-  }
+  // the rescale test needs no row reduction: some row's max exceeds the threshold iff some lane's max
+  // over its 32 scores does (16 v_max3 and one compare per block instead of two row-max trees with their
+  // lane swaps: 6.59 vs 6.77 ms per config-2 launch, bit-identical); the rows' maxima are formed only on
+  // the (rare) rescale path
   const bool first = kb == 0;
-  if (first || !__all(mx[0] <= RESCALE_THR && mx[1] <= RESCALE_THR)) {  // wave-uniform
+  if (first || !__all(lanemax32(S) <= RESCALE_THR)) {  // wave-uniform
+    float mx[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) mx[qt] = rowmax64(S, qt);  // max of c S - m over the block's 64 keys
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       const float delta = first ? mx[qt] : fmaxf(mx[qt], 0.f);

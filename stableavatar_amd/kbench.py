@@ -97,6 +97,21 @@ def main(which=("gemm", "attn")):
             r[f"v{v}_tflops"] = round(fl / ms / 1e9, 1)
         res.append(r)
         print(json.dumps(r), flush=True)
+    if "cross3" in which:  # the fused text + image + per-frame vocal cross-attention at config 2
+        L, H, D, B, nper, nfr = 21504, 12, 128, 3, 32, 21
+        q = torch.randn(B * L, H * D, device=dev).bfloat16()
+        kvt = torch.randn(B * 512, 2 * H * D, device=dev).bfloat16()
+        kvi = torch.randn(B * 257, 2 * H * D, device=dev).bfloat16()
+        kvv = torch.randn(B * nfr * nper, 2 * H * D, device=dev).bfloat16()
+        o = torch.empty(B * L, H * D, device=dev, dtype=torch.bfloat16)
+        fn = lambda: ops.attention_cross3(q, kvt[:, :H * D], kvt[:, H * D:], 512, kvi[:, :H * D], kvi[:, H * D:], 257,
+                                          kvv[:, :H * D], kvv[:, H * D:], nper, L // nfr, nfr, o, B, L, H)
+        ms = sorted(_time(fn, iters=20, warmup=3) for _ in range(5))[2]
+        fl = 4.0 * B * H * L * D * (512 + 257 + nper)
+        r = {"kernel": "attn_cross3", "ms": round(ms, 4), "tflops": round(fl / ms / 1e9, 1),
+             "out_sum": float(o.float().abs().sum())}
+        res.append(r)
+        print(json.dumps(r), flush=True)
     if "gemm" in which:
         for (N, K, epi, name) in [(4608, 1536, ops.EPI_BF16, "qkv"), (1536, 1536, ops.EPI_RES_F32, "o_proj"),
                                   (8960, 1536, ops.EPI_GELU_TANH_BF16, "ffn_up"),
