@@ -53,10 +53,10 @@ constexpr int LDS_BYTES = 2 * STAGE_BYTES;      // 128 KB
 __device__ __forceinline__ int swz128(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 
 // apply the epilogue to NC consecutive columns of one output row and store them
-template <int EPI, int NC>
+template <int EPI, int NC, bool BIAS = true>
 __device__ __forceinline__ void epi_row(const GemmArgs& g, float* v, long bz, int grow, int gcol) {
   const bool full = (gcol + NC <= g.N);
-  if (g.bias) {
+  if (BIAS && g.bias) {
     if (full) {
 #pragma unroll
       for (int j = 0; j < NC / 4; ++j) {
@@ -564,6 +564,37 @@ __device__ __forceinline__ void s7_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8
       return;
     }
   }
+  // the bias of this lane's 32 output columns, loaded once per tile: a global load inside the row loop
+  // below would wait (vmcnt retires in order and counts stores) for every store issued before it, i.e.
+  // serialise the tile's 16 store bursts
+  f32x4 bias4[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bias4[h][q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if (g.bias) {
+    const int c0 = n0 + wn * 128 + ec;
+    if (n0 + wn * 128 + 128 <= g.N) {  // wave-uniform: all 8 loads issued back to back
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bias4[h][q] = *(const f32x4*)(g.bias + c0 + h * 64 + 4 * q);
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int c = c0 + h * 64 + 4 * q + e;
+            bias4[h][q][e] = c < g.N ? g.bias[c] : 0.f;
+          }
+    }
+  }
+  // one wait for them here, before the row loop (otherwise the compiler's wait before their first use
+  // inside a non-unrolled loop body is repeated every iteration, behind that iteration's stores)
+  asm volatile("" ::"v"(bias4[0][0]), "v"(bias4[0][1]), "v"(bias4[0][2]), "v"(bias4[0][3]), "v"(bias4[1][0]),
+               "v"(bias4[1][1]), "v"(bias4[1][2]), "v"(bias4[1][3]));
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int grow = m0 + wm * 128 + i * 16 + er;
@@ -581,8 +612,12 @@ __device__ __forceinline__ void s7_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int q = 0; q < 4; ++q)  // unconditional (zeros without a bias): one wait for the loads above
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * q + e] += bias4[h][q][e];
       const int gcol = n0 + wn * 128 + h * 64 + ec;
-      if (grow < g.M && gcol < g.N) epi_row<EPI, 16>(g, v, bz, grow, gcol);
+      if (grow < g.M && gcol < g.N) epi_row<EPI, 16, false>(g, v, bz, grow, gcol);
     }
   }
 }
