@@ -118,17 +118,14 @@ __device__ __forceinline__ bf16x8 pslice(const f32x16& S, int s) {
 }
 
 // non-canonicalising f32 max (MFMA outputs are never signalling NaNs): fmaxf makes hipcc insert a
-// v_max_f32 x, x canonicalisation per operand (MI355X_MICROARCH.md, App. B attention pitfalls)
+// v_max_f32 x, x canonicalisation per operand (MI355X_MICROARCH.md, App. B attention pitfalls).  The
+// IEEE-2019 maximum lowers to gfx950's v_maximum3_f32 with no canonicalisation, and, unlike an inline-asm
+// v_max3_f32, needs no conservative s_nop after each link of a dependent chain (hipcc pads every VGPR an
+// asm statement defines before the next VALU reads it: 16+ s_nop per block on the rescale test)
 __device__ __forceinline__ float vmax3(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
+  return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
 }
-__device__ __forceinline__ float vmax2(float a, float b) {
-  float r;
-  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
+__device__ __forceinline__ float vmax2(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 struct V3State {
   f32x16 O[4];
   float m_run, l_run;  // running max (log2 units, c·S) and row sum of this lane's query
@@ -513,23 +510,26 @@ __device__ __forceinline__ float rowmax64(const f32x4 (&S)[4][2], int qt) {
   return vmax2(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 
-// max over this lane's 32 scores (both query tiles)
+// max over this lane's 32 scores (both query tiles), as a 3-ary tree (depth 4 instead of a 16-long chain)
 __device__ __forceinline__ float lanemax32(const f32x4 (&S)[4][2]) {
-  float m = vmax3(S[0][0][0], S[0][0][1], S[0][0][2]);
-  m = vmax3(m, S[0][0][3], S[0][1][0]);
-  m = vmax3(m, S[0][1][1], S[0][1][2]);
-  m = vmax3(m, S[0][1][3], S[1][0][0]);
+  float v[32];
 #pragma unroll
-  for (int kt = 1; kt < 4; ++kt) {
-    m = vmax3(m, S[kt][0][1], S[kt][0][2]);
-    m = vmax3(m, S[kt][0][3], S[kt][1][0]);
-    m = vmax3(m, S[kt][1][1], S[kt][1][2]);
-    m = (kt < 3) ? vmax3(m, S[kt][1][3], S[kt + 1][0][0]) : vmax2(m, S[kt][1][3]);
-  }
-  return m;
+  for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[kt * 8 + qt * 4 + i] = S[kt][qt][i];
+  float r[12];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) r[j] = vmax3(v[3 * j], v[3 * j + 1], v[3 * j + 2]);
+  r[10] = v[30];
+  r[11] = v[31];
+  const float a = vmax3(r[0], r[1], r[2]), b = vmax3(r[3], r[4], r[5]), c = vmax3(r[6], r[7], r[8]),
+              d = vmax3(r[9], r[10], r[11]);
+  return vmax2(vmax3(a, b, c), d);
 }
 
-template <int BUF>
+template <int BUF, bool FIRST>
 __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2][4], const uint32_t* ka,
                                               const uint32_t* va, int kb, int kv_len, int g) {
   f32x4 S[4][2];
@@ -568,14 +568,14 @@ __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2]
   // over its 32 scores does (16 v_max3 and one compare per block instead of two row-max trees with their
   // lane swaps: 6.59 vs 6.77 ms per config-2 launch, bit-identical); the rows' maxima are formed only on
   // the (rare) rescale path
-  const bool first = kb == 0;
-  if (first || !__all(lanemax32(S) <= RESCALE_THR)) {  // wave-uniform
+  // the first block (peeled: FIRST) always sets the running max
+  if (FIRST || !__all(lanemax32(S) <= RESCALE_THR)) {  // wave-uniform
     float mx[2];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) mx[qt] = rowmax64(S, qt);  // max of c S - m over the block's 64 keys
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
-      const float delta = first ? mx[qt] : fmaxf(mx[qt], 0.f);
+      const float delta = FIRST ? mx[qt] : fmaxf(mx[qt], 0.f);
       const float alpha = __builtin_amdgcn_exp2f(-delta);
       st.L[qt] *= alpha;
 #pragma unroll
@@ -720,16 +720,20 @@ __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
   const int nkb = (kv_len + KVB - 1) / KVB;
   stage(0, 0);
   if (NW == 8 && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-  for (int kb = 0; kb < nkb; kb += 2) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (1 < nkb) stage(1, 1);
+  attn_v6_block<0, true>(st, qf, ka, va, 0, kv_len, g);
+  for (int kb = 1; kb < nkb; kb += 2) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (kb + 1 < nkb) stage(kb + 1, 1);
-    attn_v6_block<0>(st, qf, ka, va, kb, kv_len, g);
+    if (kb + 1 < nkb) stage(kb + 1, 0);
+    attn_v6_block<1, false>(st, qf, ka, va, kb, kv_len, g);
     if (kb + 1 >= nkb) break;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (kb + 2 < nkb) stage(kb + 2, 0);
-    attn_v6_block<1>(st, qf, ka, va, kb + 1, kv_len, g);
+    if (kb + 2 < nkb) stage(kb + 2, 1);
+    attn_v6_block<0, false>(st, qf, ka, va, kb + 1, kv_len, g);
   }
 
   // lane rows g and g^1 (lanes l, l^16) hold adjacent 4-column groups of one query row: one
