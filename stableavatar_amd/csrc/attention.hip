@@ -44,12 +44,15 @@ __device__ __forceinline__ int gsw(int r) { return ((r & 3) << 2) | ((r >> 2) & 
 
 constexpr float RESCALE_THR = 8.0f;  // log2 units: P <= 2^8 between rescales
 
-__device__ __forceinline__ float fmax_nc(float a, float b) { return a > b ? a : b; }
-__device__ __forceinline__ float half_swap_max(float v) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmax_nc(__uint_as_float(r[0]), __uint_as_float(r[1]));
+// non-canonicalising f32 max (MFMA outputs are never signalling NaNs): fmaxf makes hipcc insert a
+// v_max_f32 x, x canonicalisation per operand (MI355X_MICROARCH.md, App. B attention pitfalls).  The
+// IEEE-2019 maximum lowers to gfx950's v_maximum3_f32 with no canonicalisation, and, unlike an inline-asm
+// v_max3_f32, needs no conservative s_nop after each link of a dependent chain (hipcc pads every VGPR an
+// asm statement defines before the next VALU reads it: 16+ s_nop per block on the rescale test)
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
 }
-
+__device__ __forceinline__ float vmax2(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 // ---- 32x32x16 block body (used by the fused cross-attention): every LDS read issued from inline asm
 // at base+immediate addresses and retired by counted lgkmcnt waits (cdna_hip_programming.md §5.7
 // item 1 form (ii)), so hipcc neither serialises each K fragment behind its own wait nor drains the
@@ -117,30 +120,23 @@ __device__ __forceinline__ bf16x8 pslice(const f32x16& S, int s) {
   return pb;
 }
 
-// non-canonicalising f32 max (MFMA outputs are never signalling NaNs): fmaxf makes hipcc insert a
-// v_max_f32 x, x canonicalisation per operand (MI355X_MICROARCH.md, App. B attention pitfalls).  The
-// IEEE-2019 maximum lowers to gfx950's v_maximum3_f32 with no canonicalisation, and, unlike an inline-asm
-// v_max3_f32, needs no conservative s_nop after each link of a dependent chain (hipcc pads every VGPR an
-// asm statement defines before the next VALU reads it: 16+ s_nop per block on the rescale test)
-__device__ __forceinline__ float vmax3(float a, float b, float c) {
-  return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
-}
-__device__ __forceinline__ float vmax2(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 struct V3State {
   f32x16 O[4];
-  float m_run, l_run;  // running max (log2 units, c·S) and row sum of this lane's query
+  float negm, l_run;  // -(running max) in log2 units (the QK^T chain's initial accumulator) and the row sum
 };
 
-// one 64-key block of the cross-attention streams: S^T = K Q^T on mfma_f32_32x32x16_bf16 (lane = query,
-// hi = key half), online softmax with a deferred rescale (RESCALE_THR), O^T += V^T P^T
+// one 64-key block of the cross-attention streams: S'^T = K (cQ)^T - m on mfma_f32_32x32x16_bf16 (lane =
+// query, hi = key half; Q prescaled by c = scale·log2e and -m as the chain's initial accumulator, as the
+// self-attention kernel), online softmax with a deferred rescale (RESCALE_THR), O^T += V^T P^T.  first:
+// the source's first block sets the running max.
 template <int BUF>
 __device__ __forceinline__ void attn_v3_block(V3State& st, const bf16x8* qf, const uint32_t* ka, const uint32_t* va,
-                                              int kb, int kv_len, float c, int hi) {
+                                              int kb, int kv_len, int hi) {
   // S^T[key][query] = K · Q^T, K fragments two groups ahead
   u32x4 ka0[4], ka1[4], kb0[4], kb1[4];
   f32x16 S[2];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) { S[0][r] = 0.f; S[1][r] = 0.f; }
+  for (int r = 0; r < 16; ++r) { S[0][r] = st.negm; S[1][r] = st.negm; }
   read_k4<BUF, 0, 0>(ka0, ka);
   read_k4<BUF, 0, 4>(ka1, ka);
   read_k4<BUF, 1, 0>(kb0, ka);
@@ -167,28 +163,45 @@ __device__ __forceinline__ void attn_v3_block(V3State& st, const bf16x8* qf, con
         if (key >= kv_len) S[t][r] = -INFINITY;
       }
   }
-  float mx = S[0][0];
+  // row max: 3-ary v_maximum3 tree over the lane's 32 scores (no canonicalisation, depth 4), then the
+  // other key half by one permlane32 swap
+  float r12[12];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int j = 0; j < 10; ++j) {
+    const int a0 = 3 * j, a1 = 3 * j + 1, a2 = 3 * j + 2;
+    r12[j] = vmax3(S[a0 >> 4][a0 & 15], S[a1 >> 4][a1 & 15], S[a2 >> 4][a2 & 15]);
+  }
+  r12[10] = S[1][14];
+  r12[11] = S[1][15];
+  float mx = vmax2(vmax3(vmax3(r12[0], r12[1], r12[2]), vmax3(r12[3], r12[4], r12[5]), vmax3(r12[6], r12[7], r12[8])),
+                   vmax3(r12[9], r12[10], r12[11]));
+  {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+    mx = vmax2(__uint_as_float(sw[0]), __uint_as_float(sw[1]));  // row max of c S - m over the block
+  }
+  const bool first = kb == 0;
+  if (first || !__all(mx <= RESCALE_THR)) {  // wave-uniform, before this block's P exists
+    const float delta = first ? mx : fmaxf(mx, 0.f);
+    if (!first) {  // O and l are still zero on a source's first block (no 0 x inf for a very negative max)
+      const float alpha = __builtin_amdgcn_exp2f(-delta);
+      st.l_run *= alpha;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[t][r]);
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * c;
-  if (!__all(mx <= st.m_run + RESCALE_THR)) {  // wave-uniform, before this block's P exists
-    const float m_new = fmaxf(st.m_run, mx);
-    const float alpha = __builtin_amdgcn_exp2f(st.m_run - m_new);
-    st.l_run *= alpha;
-    st.m_run = m_new;
+      for (int db = 0; db < 4; ++db)
 #pragma unroll
-    for (int db = 0; db < 4; ++db)
+        for (int r = 0; r < 16; ++r) st.O[db][r] *= alpha;
+    }
+    st.negm -= delta;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) st.O[db][r] *= alpha;
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) S[t][r] -= delta;
   }
   float ps = 0.f;
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float p = __builtin_amdgcn_exp2f(fmaf(S[t][r], c, -st.m_run));
+      const float p = __builtin_amdgcn_exp2f(S[t][r]);
       S[t][r] = p;
       ps += p;
     }
@@ -236,9 +249,13 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
   const int qi = qb * QB + wave * 32 + (lane & 31);
   const int qc = min(qi, a.q_len - 1);
   const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * hi;
-  bf16x8 qf[8];
+  bf16x8 qf[8];  // prescaled by c (the self-attention kernel's rounding)
 #pragma unroll
-  for (int s = 0; s < 8; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
+  for (int s = 0; s < 8; ++s) {
+    qf[s] = *(const bf16x8*)(qp + 16 * s);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[s][j] = f2bf(bf2f(qf[s][j]) * a.c);
+  }
 
   // block stream: text blocks, image blocks, vocal block(s)
   const int nT = (a.t_len + KVB - 1) / KVB, nI = (a.i_len + KVB - 1) / KVB, nV = (a.nper + KVB - 1) / KVB;
@@ -294,7 +311,7 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
     for (int db = 0; db < 4; ++db)
 #pragma unroll
       for (int r = 0; r < 16; ++r) st.O[db][r] = 0.f;
-    st.m_run = -INFINITY;
+    st.negm = 0.f;
     st.l_run = 0.f;
   };
   reset();
@@ -328,7 +345,7 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
       const int src = j < nT ? 0 : (j < nT + nI ? 1 : 2);
       const int kb = src == 0 ? j : (src == 1 ? j - nT : j - nT - nI);
       const int len = src == 0 ? a.t_len : (src == 1 ? a.i_len : a.nper);
-      attn_v3_block<0>(st, qf, ka, va, kb, len, a.c, hi);
+      attn_v3_block<0>(st, qf, ka, va, kb, len, hi);
       if (j == nT - 1 || j == nT + nI - 1 || j == ntot - 1) finish(src);
     }
     if (j + 1 >= ntot) break;
@@ -340,7 +357,7 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
       const int src = jj < nT ? 0 : (jj < nT + nI ? 1 : 2);
       const int kb = src == 0 ? jj : (src == 1 ? jj - nT : jj - nT - nI);
       const int len = src == 0 ? a.t_len : (src == 1 ? a.i_len : a.nper);
-      attn_v3_block<1>(st, qf, ka, va, kb, len, a.c, hi);
+      attn_v3_block<1>(st, qf, ka, va, kb, len, hi);
       if (jj == nT - 1 || jj == nT + nI - 1 || jj == ntot - 1) finish(src);
     }
   }
@@ -437,12 +454,6 @@ extern "C" int sa_attn_small(const void* q, const void* k, const void* v, void* 
 //   the end.
 // LDS images: K rows chunk ^ (row & 15) (conflict-free 16-row b128 reads), V rows chunk ^ 2(row & 7)
 // (conflict-free transposed reads).
-__device__ __forceinline__ float max16x2(float v) {
-  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
-  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
-}
 __device__ __forceinline__ bf16x8 v6_as_bf8(u32x4 x) { return __builtin_bit_cast(bf16x8, x); }
 __device__ __forceinline__ bf16x8 v6_as_bf8(u32x2 lo, u32x2 hi) {
   const u32x4 x = {lo[0], lo[1], hi[0], hi[1]};
@@ -576,12 +587,14 @@ __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2]
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       const float delta = FIRST ? mx[qt] : fmaxf(mx[qt], 0.f);
-      const float alpha = __builtin_amdgcn_exp2f(-delta);
-      st.L[qt] *= alpha;
+      if (!FIRST) {  // O and L are still zero on the first block (no 0 x inf for a very negative max)
+        const float alpha = __builtin_amdgcn_exp2f(-delta);
+        st.L[qt] *= alpha;
 #pragma unroll
-      for (int dt = 0; dt < 8; ++dt)
+        for (int dt = 0; dt < 8; ++dt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) st.O[dt][qt][i] *= alpha;
+          for (int i = 0; i < 4; ++i) st.O[dt][qt][i] *= alpha;
+      }
       st.negm[qt] -= delta;
       st.negm4[qt] = (f32x4){st.negm[qt], st.negm[qt], st.negm[qt], st.negm[qt]};
 #pragma unroll
