@@ -38,7 +38,8 @@ int sa_gemm_bf16(const void* A, int64_t lda, int64_t strideA, const void* W, int
 
 /* sa_gemm_bf16 with the kernel chosen per call (re-entrant A/B; no process-wide state):
  * kernel 0 = auto (the persistent one-wave-per-SIMD kernel where K % 128 == 0, else the 8-wave
- * ping-pong), 1 = ping-pong, 2 = persistent (rejected with 1 when K % 128 != 0);
+ * ping-pong), 1 = ping-pong, 2 = persistent (rejected with 1 when K % 128 != 0), 3 = persistent with two
+ * workgroups per CU (256x128 tiles; rejected with 1 when K % 64 != 0);
  * group_m = tile-raster run length (0 = per-kernel default, or env SA_GEMM_GROUP_M read once). */
 int sa_gemm_bf16_ex(const void* A, int64_t lda, int64_t strideA, const void* W, int64_t ldw, int64_t strideW,
                     const float* bias, void* C, int64_t ldc, int64_t strideC, int M, int N, int K, int batch,
@@ -55,7 +56,8 @@ int sa_attn_fwd(const void* q, const void* k, const void* v, void* o, const int3
                 float scale, int accumulate, void* stream);
 
 /* sa_attn_fwd with the kernel chosen per call (A/B without process-wide state): 0 = auto,
- * 1 = 8 waves x 32 queries on mfma_f32_16x16x32_bf16. */
+ * 1 = 8 waves x 32 queries on mfma_f32_16x16x32_bf16 (one 256-row workgroup per CU), 2 = the same body
+ * with 4 waves x 32 queries (two 128-row workgroups per CU; bit-identical output). */
 int sa_attn_fwd_ex(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
                    int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride, int64_t v_stride,
                    int64_t o_stride, float scale, int accumulate, int kernel, void* stream);
