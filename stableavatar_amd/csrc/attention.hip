@@ -425,6 +425,130 @@ __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* q, const bf
   }
 }
 
+// ---- small-query attention, head dim <= 256 (vocal projector D = 192, wav2vec2 D = 64, CLIP D = 80): one
+// workgroup per (32-query chunk, head, segment), 4 waves x 8 queries; keys in chunks of 64 staged into LDS
+// (K / V rows padded by 16 B: conflict-free row-per-lane b128 reads), scores with the key on the lane
+// (Q broadcast from LDS, prescaled by scale·log2e), online softmax in fp32, then O with 4 head dims per
+// lane.  The one-wave-per-query kernel above re-read K and V from L2 for every query (0.7 ms per vocal-
+// projector call at config 2); this reads them once per 32 queries.
+constexpr int SM2_D = 256, SM2_DP = SM2_D + 8, SM2_KC = 64, SM2_QW = 32;
+
+__global__ __launch_bounds__(256) void attn_small2_kernel(const bf16* q, const bf16* k, const bf16* v, bf16* o,
+                                                          const int* segs, int D, long qs, long ks, long vs, long os,
+                                                          float c) {
+  __shared__ __attribute__((aligned(16))) bf16 Ks[SM2_KC * SM2_DP];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[SM2_KC * SM2_DP];
+  __shared__ __attribute__((aligned(16))) float Qs[SM2_QW * SM2_D];
+  __shared__ __attribute__((aligned(16))) float Ps[4][8][SM2_KC];
+  const int* sg = segs + blockIdx.z * 4;
+  const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
+  const int q0 = blockIdx.x * SM2_QW;
+  if (q0 >= q_len) return;
+  const int h = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int DP = D + 8, nch = D / 8;  // padded row (elements), 16-B chunks per row
+  // Q rows of this chunk, fp32, prescaled (rows past q_len: zeros, never stored)
+  for (int i = tid; i < SM2_QW * nch; i += 256) {
+    const int r = i / nch, ch = i % nch;
+    float* dst = Qs + r * SM2_D + ch * 8;
+    if (q0 + r < q_len) {
+      const bf16x8 x = *(const bf16x8*)(q + (long)(q_row0 + q0 + r) * qs + h * D + ch * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dst[j] = bf2f(x[j]) * c;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dst[j] = 0.f;
+    }
+  }
+  float m[8], l[8], O[8][4];
+#pragma unroll
+  for (int qq = 0; qq < 8; ++qq) {
+    m[qq] = -INFINITY;
+    l[qq] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) O[qq][t] = 0.f;
+  }
+  const float* Qw = Qs + w * 8 * SM2_D;
+  for (int kc = 0; kc < kv_len; kc += SM2_KC) {
+    __syncthreads();  // previous chunk's K / V reads done (and Q written, first time)
+    for (int i = tid; i < SM2_KC * nch; i += 256) {
+      const int r = i / nch, ch = i % nch;
+      u32x4 kx = {0u, 0u, 0u, 0u}, vx = {0u, 0u, 0u, 0u};
+      if (kc + r < kv_len) {
+        kx = *(const u32x4*)(k + (long)(kv_row0 + kc + r) * ks + h * D + ch * 8);
+        vx = *(const u32x4*)(v + (long)(kv_row0 + kc + r) * vs + h * D + ch * 8);
+      }
+      *(u32x4*)(Ks + r * DP + ch * 8) = kx;
+      *(u32x4*)(Vs + r * DP + ch * 8) = vx;
+    }
+    __syncthreads();
+    // scores of this lane's key for the wave's 8 queries
+    float sc[8];
+#pragma unroll
+    for (int qq = 0; qq < 8; ++qq) sc[qq] = 0.f;
+    for (int d = 0; d < D; d += 8) {
+      const bf16x8 kk = *(const bf16x8*)(Ks + lane * DP + d);
+      float kf[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kf[j] = bf2f(kk[j]);
+#pragma unroll
+      for (int qq = 0; qq < 8; ++qq) {
+        const f32x4 a = *(const f32x4*)(Qw + qq * SM2_D + d), b = *(const f32x4*)(Qw + qq * SM2_D + d + 4);
+        sc[qq] = fmaf(kf[0], a[0], sc[qq]); sc[qq] = fmaf(kf[1], a[1], sc[qq]);
+        sc[qq] = fmaf(kf[2], a[2], sc[qq]); sc[qq] = fmaf(kf[3], a[3], sc[qq]);
+        sc[qq] = fmaf(kf[4], b[0], sc[qq]); sc[qq] = fmaf(kf[5], b[1], sc[qq]);
+        sc[qq] = fmaf(kf[6], b[2], sc[qq]); sc[qq] = fmaf(kf[7], b[3], sc[qq]);
+      }
+    }
+    const bool valid = kc + lane < kv_len;
+#pragma unroll
+    for (int qq = 0; qq < 8; ++qq) {
+      const float s = valid ? sc[qq] : -INFINITY;
+      const float m_new = fmaxf(m[qq], wave_max(s));  // finite: every chunk has a valid key
+      const float alpha = __builtin_amdgcn_exp2f(m[qq] - m_new);
+      const float p = __builtin_amdgcn_exp2f(s - m_new);
+      l[qq] = l[qq] * alpha + wave_sum(p);
+      m[qq] = m_new;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) O[qq][t] *= alpha;
+      Ps[w][qq][lane] = p;
+    }
+    __builtin_amdgcn_wave_barrier();  // the wave's own P writes before its broadcast reads (LDS is in order)
+    // O[q][4 lane .. 4 lane + 3] += sum_j P[q][j] V[j][..]
+    if (4 * lane < D) {
+      for (int j = 0; j < SM2_KC; j += 4) {
+        float vf[4][4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const bf16x4 vv = *(const bf16x4*)(Vs + (j + jj) * DP + 4 * lane);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) vf[jj][t] = bf2f(vv[t]);
+        }
+#pragma unroll
+        for (int qq = 0; qq < 8; ++qq) {
+          const f32x4 p4 = *(const f32x4*)(&Ps[w][qq][j]);
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) O[qq][t] = fmaf(p4[jj], vf[jj][t], O[qq][t]);
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // P reads done before the next chunk overwrites P
+  }
+  if (4 * lane < D) {
+#pragma unroll
+    for (int qq = 0; qq < 8; ++qq) {
+      const int qi = q0 + w * 8 + qq;
+      if (qi < q_len) {
+        const float inv = 1.f / l[qq];
+        *(bf16x4*)(o + (long)(q_row0 + qi) * os + h * D + 4 * lane) =
+            (bf16x4){f2bf(O[qq][0] * inv), f2bf(O[qq][1] * inv), f2bf(O[qq][2] * inv), f2bf(O[qq][3] * inv)};
+      }
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int sa_attn_small(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
@@ -433,6 +557,15 @@ extern "C" int sa_attn_small(const void* q, const void* k, const void* v, void* 
   if (!q || !k || !v || !o || !segs || nseg <= 0 || max_q_len <= 0 || heads <= 0) return SA_ERR_ARG;
   if (head_dim <= 0 || head_dim > SMALL_MAXD || head_dim % 8 || max_kv_len > SMALL_MAXK) return SA_ERR_ARG;
   if ((k_stride % 8) || (((uintptr_t)k) & 15)) return SA_ERR_ARG;
+  if (head_dim <= SM2_D && head_dim % 4 == 0 && !(v_stride % 8) && !(q_stride % 8) && !(o_stride % 4) &&
+      !(((uintptr_t)q | (uintptr_t)v) & 15) && !(((uintptr_t)o) & 7) && head_dim % 8 == 0) {
+    dim3 grid2((max_q_len + SM2_QW - 1) / SM2_QW, heads, nseg);
+    hipLaunchKernelGGL(attn_small2_kernel, grid2, dim3(256), 0, (hipStream_t)stream, (const bf16*)q, (const bf16*)k,
+                       (const bf16*)v, (bf16*)o, segs, head_dim, q_stride, k_stride, v_stride, o_stride,
+                       scale * 1.4426950408889634f);
+    SA_LAUNCH_CHECK();
+    return SA_OK;
+  }
   dim3 grid((max_q_len + 3) / 4, heads, nseg);
   hipLaunchKernelGGL(attn_small_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const bf16*)q, (const bf16*)k,
                      (const bf16*)v, (bf16*)o, segs, heads, head_dim, q_stride, k_stride, v_stride, o_stride, scale);

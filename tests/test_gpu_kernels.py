@@ -192,6 +192,32 @@ def test_attention_cross3(tok_offset):
             assert rel(o[b * Lq:(b + 1) * Lq, sl], ref) < 1e-2, (b, h)
 
 
+@pytest.mark.parametrize("D,H,segs", [
+    (192, 8, [(0, 32, 0, 1024), (32, 32, 1024, 1024), (64, 17, 2048, 1000)]),  # vocal projector (1B)
+    (64, 12, [(0, 299, 0, 299)]),                                              # wav2vec2 self-attention
+    (80, 16, [(0, 257, 0, 257)]),                                              # CLIP ViT-H/14
+    (256, 2, [(0, 40, 0, 130), (40, 1, 130, 3)]),
+    (640, 8, [(0, 17, 0, 300)]),                                               # vocal projector (14B)
+])
+def test_attention_small(D, H, segs):
+    """sa_attn_small (the head dims sa_attn_fwd does not take) vs torch fp32 per segment and head,
+    ragged query / key counts (tiled kernel for D <= 256, one wave per query above)."""
+    from stableavatar_amd import ops
+    nq = max(a + b for a, b, _, _ in segs)
+    nk = max(c + d for _, _, c, d in segs)
+    q = torch.randn(nq, H * D, device=dev).bfloat16()
+    kv = torch.randn(nk, 2 * H * D, device=dev).bfloat16()
+    k, v = kv[:, :H * D], kv[:, H * D:]
+    o = torch.full((nq, H * D), float("nan"), device=dev, dtype=torch.bfloat16)
+    st = torch.tensor(segs, dtype=torch.int32, device=dev)
+    ops.attention_small(q, k, v, o, st, len(segs), max(b for _, b, _, _ in segs), max(d for *_, d in segs), H, D)
+    for q0, ql, k0, kl in segs:
+        for h in range(H):
+            sl = slice(h * D, (h + 1) * D)
+            ref = _ref_attn(q[q0:q0 + ql, sl], k[k0:k0 + kl, sl], v[k0:k0 + kl, sl], D ** -0.5)
+            assert rel(o[q0:q0 + ql, sl], ref) < 1e-2, (q0, h)
+
+
 def test_layernorm_modulate():
     from stableavatar_amd import ops
     M, C, B = 1000, 1536, 2
