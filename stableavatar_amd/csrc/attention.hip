@@ -557,8 +557,9 @@ extern "C" int sa_attn_small(const void* q, const void* k, const void* v, void* 
   if (!q || !k || !v || !o || !segs || nseg <= 0 || max_q_len <= 0 || heads <= 0) return SA_ERR_ARG;
   if (head_dim <= 0 || head_dim > SMALL_MAXD || head_dim % 8 || max_kv_len > SMALL_MAXK) return SA_ERR_ARG;
   if ((k_stride % 8) || (((uintptr_t)k) & 15)) return SA_ERR_ARG;
-  if (head_dim <= SM2_D && head_dim % 4 == 0 && !(v_stride % 8) && !(q_stride % 8) && !(o_stride % 4) &&
-      !(((uintptr_t)q | (uintptr_t)v) & 15) && !(((uintptr_t)o) & 7) && head_dim % 8 == 0) {
+  // the tiled kernel: 16-byte Q / K / V row chunks, 8-byte O stores (head_dim % 8 == 0 already holds)
+  if (head_dim <= SM2_D && !(q_stride % 8) && !(v_stride % 8) && !(o_stride % 4) &&
+      !(((uintptr_t)q | (uintptr_t)v) & 15) && !(((uintptr_t)o) & 7)) {
     dim3 grid2((max_q_len + SM2_QW - 1) / SM2_QW, heads, nseg);
     hipLaunchKernelGGL(attn_small2_kernel, grid2, dim3(256), 0, (hipStream_t)stream, (const bf16*)q, (const bf16*)k,
                        (const bf16*)v, (bf16*)o, segs, head_dim, q_stride, k_stride, v_stride, o_stride,
