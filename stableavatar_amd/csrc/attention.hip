@@ -18,6 +18,8 @@
 // 32x32x16 block body (attn_v3_block).
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -84,10 +86,13 @@ __device__ __forceinline__ bf16x8 as_bf8(u32x2 lo, u32x2 hi) {
   return __builtin_bit_cast(bf16x8, x);
 }
 
-// K fragments for (t, s0..s0+3) of stage BUF
+// The fused cross-attention keeps K and V of a block in separate 3-stage regions (K stage b at b * 16 KB,
+// V stage b at 48 KB + b * 16 KB; the V read bases include the 48 KB) so a block's DMA is issued two blocks
+// ahead.  K fragments for (t, s0..s0+3) of stage BUF
+constexpr int X3_VBASE = 3 * TILE_BYTES, X3_LDS = 6 * TILE_BYTES;  // 96 KB
 template <int BUF, int T, int S0>
 __device__ __forceinline__ void read_k4(u32x4* f, const uint32_t* ka) {
-  constexpr int base = BUF * STAGE_BYTES + T * 8192;
+  constexpr int base = BUF * TILE_BYTES + T * 8192;
   ds_b128<base>(f[0], ka[S0 + 0]);
   ds_b128<base>(f[1], ka[S0 + 1]);
   ds_b128<base>(f[2], ka[S0 + 2]);
@@ -96,7 +101,7 @@ __device__ __forceinline__ void read_k4(u32x4* f, const uint32_t* ka) {
 // V^T fragments for P slice (t, s) of stage BUF: f[2*db + h] (h = rows r0 / r0+8)
 template <int BUF, int T, int S>
 __device__ __forceinline__ void read_v8(u32x2* f, const uint32_t* va) {
-  constexpr int base = BUF * STAGE_BYTES + TILE_BYTES + T * 8192 + S * 4096;
+  constexpr int base = BUF * TILE_BYTES + T * 8192 + S * 4096;
   ds_tr64<base>(f[0], va[0]); ds_tr64<base>(f[1], va[1]);
   ds_tr64<base>(f[2], va[2]); ds_tr64<base>(f[3], va[3]);
   ds_tr64<base>(f[4], va[4]); ds_tr64<base>(f[5], va[5]);
@@ -277,14 +282,15 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
     } else {
       kb = a.kv; vb = a.vv; st = a.vs; row0 = (b * a.n_frames + frame) * a.nper; len = a.nper; blk = j - nT - nI;
     }
-    char* base = smem + buf * STAGE_BYTES;
+    char* kbase = smem + buf * TILE_BYTES;
+    char* vbase = smem + X3_VBASE + buf * TILE_BYTES;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const long key = row0 + min(blk * KVB + srow[i], len - 1);
       __builtin_amdgcn_global_load_lds((const void*)(kb + key * st + h * D + schunk[i] * 8),
-                                       LDS_PTR(base + (wave * 2 + i) * 1024), 16, 0, 0);
+                                       LDS_PTR(kbase + (wave * 2 + i) * 1024), 16, 0, 0);
       __builtin_amdgcn_global_load_lds((const void*)(vb + key * st + h * D + schunk[i] * 8),
-                                       LDS_PTR(base + TILE_BYTES + (wave * 2 + i) * 1024), 16, 0, 0);
+                                       LDS_PTR(vbase + (wave * 2 + i) * 1024), 16, 0, 0);
     }
   };
 
@@ -301,7 +307,7 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
       for (int hh = 0; hh < 2; ++hh) {
         const int r = 4 * hi + q4 + 8 * hh;
         const int col = db * 32 + 16 * ((lane >> 4) & 1) + 4 * p4;
-        va[2 * db + hh] = lds0 + r * 256 + (((col >> 3) ^ gsw(r)) << 4) + 8 * ((col >> 2) & 1);
+        va[2 * db + hh] = lds0 + X3_VBASE + r * 256 + (((col >> 3) ^ gsw(r)) << 4) + 8 * ((col >> 2) & 1);
       }
   }
 
@@ -335,31 +341,31 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
     reset();
   };
 
+  // block j in stage j % 3, its DMA issued two blocks ahead (the K/V streams are short: with one block of
+  // lead the L2 latency of the next block's DMA was exposed at every barrier)
+  auto step = [&](int jj, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    if (jj + 1 < ntot)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // block jj landed; jj+1 may still fly
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (jj + 2 < ntot) stage(jj + 2, (BUF + 2) % 3);
+    const int src = jj < nT ? 0 : (jj < nT + nI ? 1 : 2);
+    const int kb = src == 0 ? jj : (src == 1 ? jj - nT : jj - nT - nI);
+    const int len = src == 0 ? a.t_len : (src == 1 ? a.i_len : a.nper);
+    attn_v3_block<BUF>(st, qf, ka, va, kb, len, hi);
+    if (jj == nT - 1 || jj == nT + nI - 1 || jj == ntot - 1) finish(src);
+  };
   stage(0, 0);
+  if (1 < ntot) stage(1, 1);
   if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-  for (int j = 0; j < ntot; j += 2) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (j + 1 < ntot) stage(j + 1, 1);
-    {
-      const int src = j < nT ? 0 : (j < nT + nI ? 1 : 2);
-      const int kb = src == 0 ? j : (src == 1 ? j - nT : j - nT - nI);
-      const int len = src == 0 ? a.t_len : (src == 1 ? a.i_len : a.nper);
-      attn_v3_block<0>(st, qf, ka, va, kb, len, hi);
-      if (j == nT - 1 || j == nT + nI - 1 || j == ntot - 1) finish(src);
-    }
+  for (int j = 0; j < ntot; j += 3) {
+    step(j, std::integral_constant<int, 0>{});
     if (j + 1 >= ntot) break;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (j + 2 < ntot) stage(j + 2, 0);
-    {
-      const int jj = j + 1;
-      const int src = jj < nT ? 0 : (jj < nT + nI ? 1 : 2);
-      const int kb = src == 0 ? jj : (src == 1 ? jj - nT : jj - nT - nI);
-      const int len = src == 0 ? a.t_len : (src == 1 ? a.i_len : a.nper);
-      attn_v3_block<1>(st, qf, ka, va, kb, len, hi);
-      if (jj == nT - 1 || jj == nT + nI - 1 || jj == ntot - 1) finish(src);
-    }
+    step(j + 1, std::integral_constant<int, 1>{});
+    if (j + 2 >= ntot) break;
+    step(j + 2, std::integral_constant<int, 2>{});
   }
 
   // 16-byte stores from permlane32-swapped column-group pairs, as the self-attention epilogue (T21)
@@ -988,8 +994,7 @@ extern "C" int sa_attn_cross3(const void* q, int64_t q_stride, const void* kt, c
        ((uintptr_t)vv) | ((uintptr_t)o)) & 15)
     return SA_ERR_ARG;
   static const bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)attn_cross3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)attn_cross3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, X3_LDS);
     return true;
   }();
   (void)attr;
@@ -997,7 +1002,7 @@ extern "C" int sa_attn_cross3(const void* q, int64_t q_stride, const void* kt, c
                (const bf16*)vi, i_stride, i_len, (const bf16*)kv, (const bf16*)vv, v_stride, nper,
                tokens_per_frame, n_frames, tok_offset, (bf16*)o, o_stride, q_len, scale * 1.4426950408889634f};
   dim3 grid((q_len + QB - 1) / QB, heads, batch);
-  hipLaunchKernelGGL(attn_cross3_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(attn_cross3_kernel, grid, dim3(512), X3_LDS, (hipStream_t)stream, a);
   SA_LAUNCH_CHECK();
   return SA_OK;
 }
