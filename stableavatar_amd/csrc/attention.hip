@@ -14,8 +14,8 @@
 // Swapped product S^T = K·Q^T puts one query per lane, so the online softmax is lane-local; P^T is
 // fed back as the B operand straight from the accumulator and V^T comes from ds_read_b64_tr_b16,
 // giving O^T with the query on the lane (rescale is per lane).  Self-attention runs the
-// mfma_f32_16x16x32_bf16 kernel (attn_fwd_v6_kernel); the fused cross-attention reuses the
-// 32x32x16 block body (attn_v3_block).
+// mfma_f32_16x16x32_bf16 block body (attn_v6_block), shared by the self-attention kernels and the fused
+// cross-attention.
 #include <stdlib.h>
 
 #include <type_traits>
@@ -55,13 +55,9 @@ __device__ __forceinline__ float vmax3(float a, float b, float c) {
   return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
 }
 __device__ __forceinline__ float vmax2(float a, float b) { return __builtin_elementwise_maximum(a, b); }
-// ---- 32x32x16 block body (used by the fused cross-attention): every LDS read issued from inline asm
-// at base+immediate addresses and retired by counted lgkmcnt waits (cdna_hip_programming.md §5.7
-// item 1 form (ii)), so hipcc neither serialises each K fragment behind its own wait nor drains the
-// next block's LDS-DMA (vmcnt(0)) before the V^T reads.  K fragments come in groups of 4 (16 VGPR)
-// two groups ahead of their MFMAs; V^T fragments in groups of 8 (one per (t, s) P slice), the first
-// two issued before the softmax.  Deferred rescale (T13): O and l are rescaled only when some
-// query's running max grows by more than RESCALE_THR (log2 units).
+// LDS reads issued from inline asm at base+immediate addresses and retired by counted lgkmcnt waits
+// (cdna_hip_programming.md §5.7 item 1 form (ii)), so hipcc neither serialises each fragment behind its own
+// wait nor drains the next block's LDS-DMA (vmcnt(0)) before them
 template <int OFF>
 __device__ __forceinline__ void ds_b128(u32x4& d, uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF));
@@ -71,159 +67,16 @@ __device__ __forceinline__ void ds_tr64(u32x2& d, uint32_t addr) {
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF));
 }
 template <int N>
-__device__ __forceinline__ void wait_k(u32x4* f) {
-  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]) : "i"(N));
-}
-template <int N>
 __device__ __forceinline__ void wait_v(u32x2* f) {
   asm volatile("s_waitcnt lgkmcnt(%8)"
                : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7])
                : "i"(N));
 }
-__device__ __forceinline__ bf16x8 as_bf8(u32x4 x) { return __builtin_bit_cast(bf16x8, x); }
-__device__ __forceinline__ bf16x8 as_bf8(u32x2 lo, u32x2 hi) {
-  const u32x4 x = {lo[0], lo[1], hi[0], hi[1]};
-  return __builtin_bit_cast(bf16x8, x);
-}
-
 // The fused cross-attention keeps K and V of a block in separate 3-stage regions (K stage b at b * 16 KB,
 // V stage b at 48 KB + b * 16 KB; the V read bases include the 48 KB) so a block's DMA is issued two blocks
-// ahead.  K fragments for (t, s0..s0+3) of stage BUF
+// ahead
 constexpr int X3_VBASE = 3 * TILE_BYTES, X3_LDS = 6 * TILE_BYTES;  // 96 KB
-template <int BUF, int T, int S0>
-__device__ __forceinline__ void read_k4(u32x4* f, const uint32_t* ka) {
-  constexpr int base = BUF * TILE_BYTES + T * 8192;
-  ds_b128<base>(f[0], ka[S0 + 0]);
-  ds_b128<base>(f[1], ka[S0 + 1]);
-  ds_b128<base>(f[2], ka[S0 + 2]);
-  ds_b128<base>(f[3], ka[S0 + 3]);
-}
-// V^T fragments for P slice (t, s) of stage BUF: f[2*db + h] (h = rows r0 / r0+8)
-template <int BUF, int T, int S>
-__device__ __forceinline__ void read_v8(u32x2* f, const uint32_t* va) {
-  constexpr int base = BUF * TILE_BYTES + T * 8192 + S * 4096;
-  ds_tr64<base>(f[0], va[0]); ds_tr64<base>(f[1], va[1]);
-  ds_tr64<base>(f[2], va[2]); ds_tr64<base>(f[3], va[3]);
-  ds_tr64<base>(f[4], va[4]); ds_tr64<base>(f[5], va[5]);
-  ds_tr64<base>(f[6], va[6]); ds_tr64<base>(f[7], va[7]);
-}
-__device__ __forceinline__ void mfma_k4(f32x16& acc, const u32x4* f, const bf16x8* qf) {
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(f[0]), qf[0], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(f[1]), qf[1], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(f[2]), qf[2], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(f[3]), qf[3], acc, 0, 0, 0);
-}
-__device__ __forceinline__ void mfma_v8(f32x16* O, const u32x2* f, bf16x8 pb) {
-#pragma unroll
-  for (int db = 0; db < 4; ++db)
-    O[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(f[2 * db], f[2 * db + 1]), pb, O[db], 0, 0, 0);
-}
-__device__ __forceinline__ bf16x8 pslice(const f32x16& S, int s) {
-  bf16x8 pb;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) pb[j] = f2bf(S[8 * s + j]);
-  return pb;
-}
 
-struct V3State {
-  f32x16 O[4];
-  float negm, l_run;  // -(running max) in log2 units (the QK^T chain's initial accumulator) and the row sum
-};
-
-// one 64-key block of the cross-attention streams: S'^T = K (cQ)^T - m on mfma_f32_32x32x16_bf16 (lane =
-// query, hi = key half; Q prescaled by c = scale·log2e and -m as the chain's initial accumulator, as the
-// self-attention kernel), online softmax with a deferred rescale (RESCALE_THR), O^T += V^T P^T.  first:
-// the source's first block sets the running max.
-template <int BUF>
-__device__ __forceinline__ void attn_v3_block(V3State& st, const bf16x8* qf, const uint32_t* ka, const uint32_t* va,
-                                              int kb, int kv_len, int hi) {
-  // S^T[key][query] = K · Q^T, K fragments two groups ahead
-  u32x4 ka0[4], ka1[4], kb0[4], kb1[4];
-  f32x16 S[2];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) { S[0][r] = st.negm; S[1][r] = st.negm; }
-  read_k4<BUF, 0, 0>(ka0, ka);
-  read_k4<BUF, 0, 4>(ka1, ka);
-  read_k4<BUF, 1, 0>(kb0, ka);
-  wait_k<8>(ka0);
-  mfma_k4(S[0], ka0, qf);
-  read_k4<BUF, 1, 4>(kb1, ka);
-  wait_k<8>(ka1);
-  mfma_k4(S[0], ka1, qf + 4);
-  wait_k<4>(kb0);
-  mfma_k4(S[1], kb0, qf);
-  wait_k<0>(kb1);
-  mfma_k4(S[1], kb1, qf + 4);
-  // first two V^T slices under the softmax
-  u32x2 v0[8], v1[8];
-  read_v8<BUF, 0, 0>(v0, va);
-  read_v8<BUF, 0, 1>(v1, va);
-
-  if (kb * KVB + KVB > kv_len) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kb * KVB + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-        if (key >= kv_len) S[t][r] = -INFINITY;
-      }
-  }
-  // row max: 3-ary v_maximum3 tree over the lane's 32 scores (no canonicalisation, depth 4), then the
-  // other key half by one permlane32 swap
-  float r12[12];
-#pragma unroll
-  for (int j = 0; j < 10; ++j) {
-    const int a0 = 3 * j, a1 = 3 * j + 1, a2 = 3 * j + 2;
-    r12[j] = vmax3(S[a0 >> 4][a0 & 15], S[a1 >> 4][a1 & 15], S[a2 >> 4][a2 & 15]);
-  }
-  r12[10] = S[1][14];
-  r12[11] = S[1][15];
-  float mx = vmax2(vmax3(vmax3(r12[0], r12[1], r12[2]), vmax3(r12[3], r12[4], r12[5]), vmax3(r12[6], r12[7], r12[8])),
-                   vmax3(r12[9], r12[10], r12[11]));
-  {
-    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-    mx = vmax2(__uint_as_float(sw[0]), __uint_as_float(sw[1]));  // row max of c S - m over the block
-  }
-  const bool first = kb == 0;
-  if (first || !__all(mx <= RESCALE_THR)) {  // wave-uniform, before this block's P exists
-    const float delta = first ? mx : fmaxf(mx, 0.f);
-    if (!first) {  // O and l are still zero on a source's first block (no 0 x inf for a very negative max)
-      const float alpha = __builtin_amdgcn_exp2f(-delta);
-      st.l_run *= alpha;
-#pragma unroll
-      for (int db = 0; db < 4; ++db)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) st.O[db][r] *= alpha;
-    }
-    st.negm -= delta;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) S[t][r] -= delta;
-  }
-  float ps = 0.f;
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float p = __builtin_amdgcn_exp2f(S[t][r]);
-      S[t][r] = p;
-      ps += p;
-    }
-  st.l_run += ps;
-
-  // O^T[d][query] += V^T · P^T, slice g = 2t + s
-  wait_v<8>(v0);
-  mfma_v8(st.O, v0, pslice(S[0], 0));
-  read_v8<BUF, 1, 0>(v0, va);
-  wait_v<8>(v1);
-  mfma_v8(st.O, v1, pslice(S[0], 1));
-  read_v8<BUF, 1, 1>(v1, va);
-  wait_v<8>(v0);
-  mfma_v8(st.O, v0, pslice(S[1], 0));
-  wait_v<0>(v1);
-  mfma_v8(st.O, v1, pslice(S[1], 1));
-}
 // ---- fused cross-attention of WanI2VTalkingCrossAttention (1B:556-603): per query block, the text
 // (1B:564-570), image (1B:556-562) and per-frame vocal (1B:575-586) attentions run back to back over
 // one K/V block stream, each with its own online softmax, and the three outputs are summed with the
@@ -238,147 +91,6 @@ struct Cross3Args {
   int q_len;
   float c;
 };
-
-__global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nx = gridDim.x, ny = gridDim.y;
-  const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
-  const int qb = flat % nx, h = (flat / nx) % ny, b = flat / (nx * ny);
-  if (qb * QB >= a.q_len) return;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hi = lane >> 5;
-  const int q_row0 = b * a.q_len;
-  const int frame = (a.tok_offset + qb * QB) / a.tpf;
-
-  const int qi = qb * QB + wave * 32 + (lane & 31);
-  const int qc = min(qi, a.q_len - 1);
-  const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * hi;
-  bf16x8 qf[8];  // prescaled by c (the self-attention kernel's rounding)
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    qf[s] = *(const bf16x8*)(qp + 16 * s);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qf[s][j] = f2bf(bf2f(qf[s][j]) * a.c);
-  }
-
-  // block stream: text blocks, image blocks, vocal block(s)
-  const int nT = (a.t_len + KVB - 1) / KVB, nI = (a.i_len + KVB - 1) / KVB, nV = (a.nper + KVB - 1) / KVB;
-  const int ntot = nT + nI + nV;
-  int srow[2], schunk[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    srow[i] = (wave * 2 + i) * 4 + (lane >> 4);
-    schunk[i] = (lane & 15) ^ gsw(srow[i]);
-  }
-  auto stage = [&](int j, int buf) {
-    const bf16 *kb, *vb;
-    long st;
-    int row0, len, blk;
-    if (j < nT) {
-      kb = a.kt; vb = a.vt; st = a.ts; row0 = b * a.t_len; len = a.t_len; blk = j;
-    } else if (j < nT + nI) {
-      kb = a.ki; vb = a.vi; st = a.is; row0 = b * a.i_len; len = a.i_len; blk = j - nT;
-    } else {
-      kb = a.kv; vb = a.vv; st = a.vs; row0 = (b * a.n_frames + frame) * a.nper; len = a.nper; blk = j - nT - nI;
-    }
-    char* kbase = smem + buf * TILE_BYTES;
-    char* vbase = smem + X3_VBASE + buf * TILE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const long key = row0 + min(blk * KVB + srow[i], len - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(kb + key * st + h * D + schunk[i] * 8),
-                                       LDS_PTR(kbase + (wave * 2 + i) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(vb + key * st + h * D + schunk[i] * 8),
-                                       LDS_PTR(vbase + (wave * 2 + i) * 1024), 16, 0, 0);
-    }
-  };
-
-  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
-  uint32_t ka[8], va[8];
-  {
-    const int row = lane & 31;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) ka[s] = lds0 + row * 256 + (((2 * s + hi) ^ gsw(row)) << 4);
-    const int q4 = (lane & 15) >> 2, p4 = lane & 3;
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const int r = 4 * hi + q4 + 8 * hh;
-        const int col = db * 32 + 16 * ((lane >> 4) & 1) + 4 * p4;
-        va[2 * db + hh] = lds0 + X3_VBASE + r * 256 + (((col >> 3) ^ gsw(r)) << 4) + 8 * ((col >> 2) & 1);
-      }
-  }
-
-  V3State st;
-  auto reset = [&]() {
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) st.O[db][r] = 0.f;
-    st.negm = 0.f;
-    st.l_run = 0.f;
-  };
-  reset();
-  bf16x2 acc[32];  // running (text + img) + vocal, bf16 as in the reference
-  // finish source `src` (0 text, 1 image, 2 vocal): bf16(O / l) folded into acc
-  auto finish = [&](int src) {
-    const float lt = st.l_run + __shfl_xor(st.l_run, 32, 64);
-    const float inv = 1.0f / lt;
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const bf16 x0 = f2bf(st.O[db][r] * inv), x1 = f2bf(st.O[db][r + 1] * inv);
-        bf16x2& s = acc[db * 8 + r / 2];
-        if (src == 0) {
-          s = (bf16x2){x0, x1};
-        } else {
-          s = (bf16x2){f2bf(bf2f(s[0]) + bf2f(x0)), f2bf(bf2f(s[1]) + bf2f(x1))};
-        }
-      }
-    reset();
-  };
-
-  // block j in stage j % 3, its DMA issued two blocks ahead (the K/V streams are short: with one block of
-  // lead the L2 latency of the next block's DMA was exposed at every barrier)
-  auto step = [&](int jj, auto bufc) {
-    constexpr int BUF = decltype(bufc)::value;
-    if (jj + 1 < ntot)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // block jj landed; jj+1 may still fly
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (jj + 2 < ntot) stage(jj + 2, (BUF + 2) % 3);
-    const int src = jj < nT ? 0 : (jj < nT + nI ? 1 : 2);
-    const int kb = src == 0 ? jj : (src == 1 ? jj - nT : jj - nT - nI);
-    const int len = src == 0 ? a.t_len : (src == 1 ? a.i_len : a.nper);
-    attn_v3_block<BUF>(st, qf, ka, va, kb, len, hi);
-    if (jj == nT - 1 || jj == nT + nI - 1 || jj == ntot - 1) finish(src);
-  };
-  stage(0, 0);
-  if (1 < ntot) stage(1, 1);
-  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-  for (int j = 0; j < ntot; j += 3) {
-    step(j, std::integral_constant<int, 0>{});
-    if (j + 1 >= ntot) break;
-    step(j + 1, std::integral_constant<int, 1>{});
-    if (j + 2 >= ntot) break;
-    step(j + 2, std::integral_constant<int, 2>{});
-  }
-
-  // 16-byte stores from permlane32-swapped column-group pairs, as the self-attention epilogue (T21)
-  bf16* op = a.o + (long)(q_row0 + min(qi, a.q_len - 1)) * a.os + h * D + 8 * hi;
-#pragma unroll
-  for (int k = 0; k < 16; k += 2) {
-    const uint32_t a0 = __builtin_bit_cast(uint32_t, acc[2 * k]), a1 = __builtin_bit_cast(uint32_t, acc[2 * k + 1]);
-    const uint32_t b0 = __builtin_bit_cast(uint32_t, acc[2 * k + 2]), b1 = __builtin_bit_cast(uint32_t, acc[2 * k + 3]);
-    const auto rx = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
-    const auto ry = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
-    if (qi < a.q_len) *(u32x4*)(op + 8 * k) = (u32x4){rx[0], ry[0], rx[1], ry[1]};
-  }
-}
 
 // ---- small-query attention for head dims the MFMA kernel does not take (vocal projector, D=192 for
 // 1.3B and 640 for 14B, 17 queries per frame vs one latent frame's tokens: vocal_projector_fantasy_1B.py:
@@ -600,19 +312,20 @@ __device__ __forceinline__ bf16x8 v6_as_bf8(u32x2 lo, u32x2 hi) {
   return __builtin_bit_cast(bf16x8, x);
 }
 
-// K fragments of key tile KT (d chunks 0-3) of stage BUF
-template <int BUF, int KT>
+// K fragments of key tile KT (d chunks 0-3) of the K stage at byte KOFF from the K read bases
+template <int KOFF, int KT>
 __device__ __forceinline__ void v6_read_k(u32x4* f, const uint32_t* ka) {
-  constexpr int base = BUF * STAGE_BYTES + KT * 4096;
+  constexpr int base = KOFF + KT * 4096;
   ds_b128<base>(f[0], ka[0]);
   ds_b128<base>(f[1], ka[1]);
   ds_b128<base>(f[2], ka[2]);
   ds_b128<base>(f[3], ka[3]);
 }
-// V^T fragments of key chunk C for d tiles DT0..DT0+3: f[2*t + h], h = rows +0 / +16
-template <int BUF, int C, int DT0>
+// V^T fragments of key chunk C for d tiles DT0..DT0+3 of the V stage at byte VOFF from the V read bases:
+// f[2*t + h], h = rows +0 / +16
+template <int VOFF, int C, int DT0>
 __device__ __forceinline__ void v6_read_v(u32x2* f, const uint32_t* va) {
-  constexpr int base = BUF * STAGE_BYTES + TILE_BYTES + C * 8192;
+  constexpr int base = VOFF + C * 8192;
   ds_tr64<base>(f[0], va[DT0 + 0]); ds_tr64<base + 4096>(f[1], va[DT0 + 0]);
   ds_tr64<base>(f[2], va[DT0 + 1]); ds_tr64<base + 4096>(f[3], va[DT0 + 1]);
   ds_tr64<base>(f[4], va[DT0 + 2]); ds_tr64<base + 4096>(f[5], va[DT0 + 2]);
@@ -680,9 +393,15 @@ __device__ __forceinline__ float lanemax32(const f32x4 (&S)[4][2]) {
   return vmax2(vmax3(a, b, c), d);
 }
 
-template <int BUF, bool FIRST>
+// one 64-key block whose K / V stages sit at KOFF / VOFF from the read bases (self-attention: K and V of a
+// stage adjacent in a 2-stage ring; the fused cross-attention: separate 3-stage K and V regions).  The first
+// block of a softmax sets the running max: FIRST_CT at compile time (self-attention), first_rt per source
+// (cross-attention)
+template <int KOFF, int VOFF, bool FIRST_CT>
 __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2][4], const uint32_t* ka,
-                                              const uint32_t* va, int kb, int kv_len, int g) {
+                                              const uint32_t* va, int kb, int kv_len, int g,
+                                              bool first_rt = false) {
+  const bool FIRST = FIRST_CT || first_rt;
   f32x4 S[4][2];
 #pragma unroll
   for (int kt = 0; kt < 4; ++kt)
@@ -691,22 +410,22 @@ __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2]
       S[kt][qt] = st.negm4[qt];
   // S'^T = c K Q^T - m, K fragments two key tiles ahead
   u32x4 k0[4], k1[4];
-  v6_read_k<BUF, 0>(k0, ka);
-  v6_read_k<BUF, 1>(k1, ka);
+  v6_read_k<KOFF, 0>(k0, ka);
+  v6_read_k<KOFF, 1>(k1, ka);
   wait_k4<4>(k0);
   v6_mma_k(S, 0, k0, qf);
-  v6_read_k<BUF, 2>(k0, ka);
+  v6_read_k<KOFF, 2>(k0, ka);
   wait_k4<4>(k1);
   v6_mma_k(S, 1, k1, qf);
-  v6_read_k<BUF, 3>(k1, ka);
+  v6_read_k<KOFF, 3>(k1, ka);
   wait_k4<4>(k0);
   v6_mma_k(S, 2, k0, qf);
   wait_k4<0>(k1);
   v6_mma_k(S, 3, k1, qf);
   // first V^T fragments under the softmax
   u32x2 v0[8], v1[8];
-  v6_read_v<BUF, 0, 0>(v0, va);
-  v6_read_v<BUF, 0, 4>(v1, va);
+  v6_read_v<VOFF, 0, 0>(v0, va);
+  v6_read_v<VOFF, 0, 4>(v1, va);
 
   if (kb * KVB + KVB > kv_len) {
 #pragma unroll
@@ -770,10 +489,10 @@ __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2]
     if (c == 0) {
       wait_v<8>(v0);
       v6_mma_v(st.O, 0, v0, pb);
-      v6_read_v<BUF, 1, 0>(v0, va);
+      v6_read_v<VOFF, 1, 0>(v0, va);
       wait_v<8>(v1);
       v6_mma_v(st.O, 4, v1, pb);
-      v6_read_v<BUF, 1, 4>(v1, va);
+      v6_read_v<VOFF, 1, 4>(v1, va);
     } else {
       wait_v<8>(v0);
       v6_mma_v(st.O, 0, v0, pb);
@@ -876,17 +595,17 @@ __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (1 < nkb) stage(1, 1);
-  attn_v6_block<0, true>(st, qf, ka, va, 0, kv_len, g);
+  attn_v6_block<0, TILE_BYTES, true>(st, qf, ka, va, 0, kv_len, g);
   for (int kb = 1; kb < nkb; kb += 2) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (kb + 1 < nkb) stage(kb + 1, 0);
-    attn_v6_block<1, false>(st, qf, ka, va, kb, kv_len, g);
+    attn_v6_block<STAGE_BYTES, STAGE_BYTES + TILE_BYTES, false>(st, qf, ka, va, kb, kv_len, g);
     if (kb + 1 >= nkb) break;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (kb + 2 < nkb) stage(kb + 2, 1);
-    attn_v6_block<0, false>(st, qf, ka, va, kb + 1, kv_len, g);
+    attn_v6_block<0, TILE_BYTES, false>(st, qf, ka, va, kb + 1, kv_len, g);
   }
 
   // lane rows g and g^1 (lanes l, l^16) hold adjacent 4-column groups of one query row: one
@@ -915,6 +634,159 @@ __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
         out = __builtin_bit_cast(u32x4, nv);
       }
       if (qi < q_len) *(u32x4*)p = out;
+    }
+  }
+}
+
+// the fused cross-attention on the self-attention block body: 8 waves x 32 queries of one query block,
+// the text, image and per-frame vocal K/V streams one after the other through 3-stage K / V regions (each
+// block's DMA two blocks ahead), a separate online softmax per source (its first block sets the max), the
+// three bf16 outputs summed as the reference does
+__global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nx = gridDim.x, ny = gridDim.y;
+  const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
+  const int qb = flat % nx, h = (flat / nx) % ny, b = flat / (nx * ny);
+  if (qb * QB >= a.q_len) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int q_row0 = b * a.q_len;
+  const int frame = (a.tok_offset + qb * QB) / a.tpf;
+
+  // Q as the B operand (query tile qt, d chunk dc), prescaled by c; rows clamped to the segment
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qc = min(qb * QB + wave * 32 + qt * 16 + r16, a.q_len - 1);
+    const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * g;
+#pragma unroll
+    for (int dc = 0; dc < 4; ++dc) {
+      qf[qt][dc] = *(const bf16x8*)(qp + 32 * dc);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[qt][dc][j] = f2bf(bf2f(qf[qt][dc][j]) * a.c);
+    }
+  }
+
+  // block stream: text blocks, image blocks, vocal block(s); LDS images as the self-attention kernel's
+  // (K rows chunk ^ (row & 15), V rows chunk ^ 2 (row & 7)); each wave moves 2 x 1-KB pieces of K and V
+  const int nT = (a.t_len + KVB - 1) / KVB, nI = (a.i_len + KVB - 1) / KVB, nV = (a.nper + KVB - 1) / KVB;
+  const int ntot = nT + nI + nV;
+  int srow[2], kch[2], vch[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    srow[i] = (wave * 2 + i) * 4 + (lane >> 4);
+    kch[i] = r16 ^ (srow[i] & 15);
+    vch[i] = r16 ^ ((srow[i] & 7) << 1);
+  }
+  auto stage = [&](int j, int buf) {
+    const bf16 *kb, *vb;
+    long st;
+    int row0, len, blk;
+    if (j < nT) {
+      kb = a.kt; vb = a.vt; st = a.ts; row0 = b * a.t_len; len = a.t_len; blk = j;
+    } else if (j < nT + nI) {
+      kb = a.ki; vb = a.vi; st = a.is; row0 = b * a.i_len; len = a.i_len; blk = j - nT;
+    } else {
+      kb = a.kv; vb = a.vv; st = a.vs; row0 = (b * a.n_frames + frame) * a.nper; len = a.nper; blk = j - nT - nI;
+    }
+    char* kbase = smem + buf * TILE_BYTES;
+    char* vbase = smem + X3_VBASE + buf * TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long key = row0 + min(blk * KVB + srow[i], len - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(kb + key * st + h * D + kch[i] * 8),
+                                       LDS_PTR(kbase + (wave * 2 + i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(vb + key * st + h * D + vch[i] * 8),
+                                       LDS_PTR(vbase + (wave * 2 + i) * 1024), 16, 0, 0);
+    }
+  };
+
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
+  uint32_t ka[4], va[8];
+#pragma unroll
+  for (int dc = 0; dc < 4; ++dc) ka[dc] = lds0 + r16 * 256 + (((dc * 4 + g) ^ r16) << 4);
+  {
+    const int q4 = r16 >> 2, p4 = r16 & 3;
+    const int row = 4 * g + q4;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      const int ch = 2 * dt + (p4 >> 1);
+      va[dt] = lds0 + X3_VBASE + row * 256 + ((ch ^ ((row & 7) << 1)) << 4) + 8 * (p4 & 1);
+    }
+  }
+
+  V6State st;
+  auto reset = [&]() {
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) st.O[dt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    st.L[0] = st.L[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    st.negm[0] = st.negm[1] = 0.f;
+    st.negm4[0] = st.negm4[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  };
+  reset();
+  bf16x4 acc[8][2];  // running (text + img) + vocal, bf16 as in the reference
+  // finish source `src` (0 text, 1 image, 2 vocal): bf16(O / l) folded into acc
+  auto finish = [&](int src) {
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const float inv = 1.0f / st.L[qt][0];
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        bf16x4 x;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = f2bf(st.O[dt][qt][i] * inv);
+        if (src == 0) {
+          acc[dt][qt] = x;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[dt][qt][i] = f2bf(bf2f(acc[dt][qt][i]) + bf2f(x[i]));
+        }
+      }
+    }
+    reset();
+  };
+
+  // block j in stage j % 3, its DMA issued two blocks ahead (with one block of lead the L2 latency of
+  // the next block was exposed at the barriers of these short streams)
+  auto step = [&](int jj, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    if (jj + 1 < ntot)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // block jj landed; jj+1 may still fly
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (jj + 2 < ntot) stage(jj + 2, (BUF + 2) % 3);
+    const int src = jj < nT ? 0 : (jj < nT + nI ? 1 : 2);
+    const int kb = src == 0 ? jj : (src == 1 ? jj - nT : jj - nT - nI);
+    const int len = src == 0 ? a.t_len : (src == 1 ? a.i_len : a.nper);
+    attn_v6_block<BUF * TILE_BYTES, BUF * TILE_BYTES, false>(st, qf, ka, va, kb, len, g, kb == 0);
+    if (jj == nT - 1 || jj == nT + nI - 1 || jj == ntot - 1) finish(src);
+  };
+  stage(0, 0);
+  if (1 < ntot) stage(1, 1);
+  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  for (int j = 0; j < ntot; j += 3) {
+    step(j, std::integral_constant<int, 0>{});
+    if (j + 1 >= ntot) break;
+    step(j + 1, std::integral_constant<int, 1>{});
+    if (j + 2 >= ntot) break;
+    step(j + 2, std::integral_constant<int, 2>{});
+  }
+
+  // 16-byte stores from permlane16-swapped column-group pairs, as the self-attention epilogue (T21)
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qi = qb * QB + wave * 32 + qt * 16 + r16;
+    bf16* op = a.o + (long)(q_row0 + min(qi, a.q_len - 1)) * a.os + h * D + 4 * (g & ~1) + 16 * (g & 1);
+#pragma unroll
+    for (int dt = 0; dt < 8; dt += 2) {
+      const u32x2 ga = __builtin_bit_cast(u32x2, acc[dt][qt]), gb = __builtin_bit_cast(u32x2, acc[dt + 1][qt]);
+      const auto rx = __builtin_amdgcn_permlane16_swap(ga[0], gb[0], false, false);
+      const auto ry = __builtin_amdgcn_permlane16_swap(ga[1], gb[1], false, false);
+      if (qi < a.q_len) *(u32x4*)(op + dt * 16) = (u32x4){rx[0], ry[0], rx[1], ry[1]};
     }
   }
 }
