@@ -73,8 +73,9 @@ int sa_attn_cross3(const void* q, int64_t q_stride, const void* kt, const void* 
                    int64_t o_stride, int batch, int q_len, int heads, float scale, void* stream);
 
 /* attention for head dims other than 128 and few queries per segment (vocal projector D=192,
- * vocal_projector_fantasy_1B.py:259-270; 14B :254-267, D = 640; wav2vec2 D = 64): exact softmax, fp32 math, kv_len <= 4096,
- * head_dim <= 640. */
+ * vocal_projector_fantasy_1B.py:259-270; 14B :254-267, D = 640; wav2vec2 D = 64): fp32 softmax and math.
+ * head_dim <= 256 (multiple of 8): any kv_len (keys in 64-key chunks, online softmax); 256 < head_dim <= 640:
+ * exact softmax, kv_len <= 4096. */
 int sa_attn_small(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg, int max_q_len,
                   int max_kv_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride, int64_t v_stride,
                   int64_t o_stride, float scale, void* stream);

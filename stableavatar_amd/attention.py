@@ -8,7 +8,7 @@ dropout_p=dropout_p)`` is called, so the scale is always 1/sqrt(D) (``softmax_sc
 ``q_lens`` / ``k_lens`` only raise a warning (1B:190-193).  This function keeps that contract:
 
 * head_dim 128 -> ``sa_attn_fwd`` (flash attention, bf16 in, fp32 softmax/accumulate, bf16 out);
-* other head dims (<= 256, key length <= 4096) -> ``sa_attn_small`` (exact fp32 softmax);
+* other head dims (<= 256, multiple of 8) -> ``sa_attn_small`` (fp32 online softmax);
 * causal masks and dropout are not part of the inference path: they raise instead of silently differing.
 Returns [B, Lq, N, D] in the dtype of q (bf16 on the reference's autocast path).
 """
@@ -46,8 +46,7 @@ def attention(q, k, v, q_lens=None, k_lens=None, dropout_p=0., softmax_scale=Non
     if D == 128:
         ops.attention(qb, kb, vb, o, segs, B, Lq, N)
     else:
-        if D > 256 or D % 8 or Lk > 4096:
-            raise NotImplementedError(f"head_dim {D} / key length {Lk}: the small-attention kernel takes D <= 256 "
-                                      "(multiple of 8) and at most 4096 keys")
+        if D > 256 or D % 8:
+            raise NotImplementedError(f"head_dim {D}: the small-attention kernel takes D <= 256 (multiple of 8)")
         ops.attention_small(qb, kb, vb, o, segs, B, Lq, Lk, N, D)
     return o.view(B, Lq, N, D).to(out_dtype)

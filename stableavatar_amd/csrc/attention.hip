@@ -273,7 +273,7 @@ extern "C" int sa_attn_small(const void* q, const void* k, const void* v, void* 
                              int max_q_len, int max_kv_len, int heads, int head_dim, int64_t q_stride,
                              int64_t k_stride, int64_t v_stride, int64_t o_stride, float scale, void* stream) {
   if (!q || !k || !v || !o || !segs || nseg <= 0 || max_q_len <= 0 || heads <= 0) return SA_ERR_ARG;
-  if (head_dim <= 0 || head_dim > SMALL_MAXD || head_dim % 8 || max_kv_len > SMALL_MAXK) return SA_ERR_ARG;
+  if (head_dim <= 0 || head_dim > SMALL_MAXD || head_dim % 8 || max_kv_len <= 0) return SA_ERR_ARG;
   if ((k_stride % 8) || (((uintptr_t)k) & 15)) return SA_ERR_ARG;
   // the tiled kernel: 16-byte Q / K / V row chunks, 8-byte O stores (head_dim % 8 == 0 already holds)
   if (head_dim <= SM2_D && !(q_stride % 8) && !(v_stride % 8) && !(o_stride % 4) &&
@@ -285,6 +285,7 @@ extern "C" int sa_attn_small(const void* q, const void* k, const void* v, void* 
     SA_LAUNCH_CHECK();
     return SA_OK;
   }
+  if (max_kv_len > SMALL_MAXK) return SA_ERR_ARG;  // the one-wave-per-query kernel keeps a score row in LDS
   dim3 grid((max_q_len + 3) / 4, heads, nseg);
   hipLaunchKernelGGL(attn_small_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const bf16*)q, (const bf16*)k,
                      (const bf16*)v, (bf16*)o, segs, heads, head_dim, q_stride, k_stride, v_stride, o_stride, scale);

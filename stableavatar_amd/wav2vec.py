@@ -247,9 +247,6 @@ class Wav2Vec2Model(nn.Module):
         ops.layernorm_mod(x, x, eps, weight=P.enc_ln_w, bias=P.enc_ln_b)
         nh = c.num_attention_heads
         hd = H // nh
-        if T > 4096:  # sa_attn_small keeps one row of scores in LDS
-            raise ValueError(f"wav2vec2: {T} frames (> 4096, ~82 s of audio) in one call; the pipeline calls it per "
-                             "window")
         segs = torch.tensor([[0, T, 0, T]], dtype=torch.int32, device=dev)
         att = torch.empty(T, H, device=dev, dtype=torch.bfloat16)
         for L in P.layers:

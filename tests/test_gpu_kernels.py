@@ -197,6 +197,7 @@ def test_attention_cross3(tok_offset):
     (64, 12, [(0, 299, 0, 299)]),                                              # wav2vec2 self-attention
     (80, 16, [(0, 257, 0, 257)]),                                              # CLIP ViT-H/14
     (256, 2, [(0, 40, 0, 130), (40, 1, 130, 3)]),
+    (64, 2, [(0, 70, 0, 5000)]),                                               # > 4096 keys (tiled kernel)
     (640, 8, [(0, 17, 0, 300)]),                                               # vocal projector (14B)
 ])
 def test_attention_small(D, H, segs):
