@@ -286,13 +286,15 @@ class ClipWorkload:
         self.dit._events = []
 
     def attention_launch_ms(self):
-        """mean duration of one whole self-attention launch (per-row SP launches are summed by their
-        share of the CFG batch), from HIP events on the launching stream"""
+        """(mean duration of one self-attention launch, the share of the CFG batch one launch covers), from
+        HIP events on the launching stream (per-row launches -- the per-row stream loop, per-row SP -- cover
+        1/3 of the batch each)"""
         ev, self.dit._events = self.dit._events or [], None
         if not ev:
-            return None
+            return None, 1.0
         tot = sum(e0.elapsed_time(e1) for e0, e1, _ in ev)
-        return tot / sum(f for _, _, f in ev)
+        share = sum(f for _, _, f in ev) / len(ev)
+        return tot / len(ev), share
 
     def n_fwd(self):
         return self.args.sample_steps * len(self.wins)
@@ -373,9 +375,9 @@ def run(args, world, rank, dev, work_factory=ClipWorkload):
     work.set_layout(layout)
     dt, video = timed(work, args.steps, args.warmup, world, dev, events=True)
     work.check(video)
-    attn_ms = work.attention_launch_ms()
+    attn_ms, attn_share = work.attention_launch_ms()
     seq_len = work.seq_len
-    attn_flop = flops.self_attention_flops(B=3, L=seq_len)
+    attn_flop = flops.self_attention_flops(B=3, L=seq_len) * attn_share
     parallelism = {"single": "single", "replicas": f"replicas{world}", "window-dp": f"windows{world}"}.get(layout)
     if layout == "sp":
         plan = sp.make_plan(world, rank, 12)
@@ -429,8 +431,9 @@ def run(args, world, rank, dev, work_factory=ClipWorkload):
            "roofline": {"bound": "mfma", "kernel": f"{ATTN_KERNEL_NAME} (self-attention, flash, D=128)",
                         "achieved": round(achieved / 1e12, 1) if achieved else None, "peak": PEAK_BF16 / 1e12,
                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16, 4) if achieved else None,
-                        "traffic": traffic, "traffic_source": traffic_src,
-                        "algorithmic_bytes": 4 * 3 * seq_len * 1536 * 2,
+                        "traffic": round(traffic * attn_share) if traffic else None, "traffic_source": traffic_src,
+                        "algorithmic_bytes": round(4 * 3 * seq_len * 1536 * 2 * attn_share),
+                        "launch_share_of_cfg_batch": round(attn_share, 4),
                         "launch_ms": round(attn_ms, 3) if attn_ms else None, "flop_per_launch": attn_flop},
            "path_mfma_frac": round(path_flop * args.steps / dt / PEAK_BF16 / (world if shared else 1), 4),
            "cpu_baseline": cpu, "vae_encode": enc, "config_4_dit14": dit14}

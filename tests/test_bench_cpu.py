@@ -70,9 +70,9 @@ class FakeClip:
     def start_events(self):
         self.events = []
 
-    def attention_launch_ms(self):
+    def attention_launch_ms(self):  # per-launch mean and the CFG-batch share of one launch, as ClipWorkload
         ev, self.events = self.events, None
-        return sum(a.elapsed_time(b) for a, b, _ in ev) / sum(f for _, _, f in ev)
+        return sum(a.elapsed_time(b) for a, b, _ in ev) / len(ev), sum(f for _, _, f in ev) / len(ev)
 
     def n_fwd(self):
         return self.args.sample_steps * len(self.wins)
@@ -106,9 +106,10 @@ def test_bench_sp_default_world2(tmp_path):
     assert j["value"] > 0 and j["ms_per_step"] > 0
     # one clip of 81 frames per step, over all ranks
     assert abs(j["value"] * j["ms_per_step"] / 1e3 / 81 - 1) < 0.1  # ms_per_step is rounded to 0.1 ms
-    # per-row spans (3 x 1/3 of the batch, 2 ms each) -> 6 ms per whole launch, flop = this rank's half
-    assert j["roofline"]["launch_ms"] == 6.0
-    assert j["roofline"]["flop_per_launch"] == 4.0 * 3 * 12 * 21504 ** 2 * 128 / 2
+    # per-row launches (1/3 of the batch, 2 ms each): the roofline is quoted per launch, flop = this
+    # rank's half of one CFG row (the achieved rate is the same as per whole-batch launch)
+    assert j["roofline"]["launch_ms"] == 2.0 and j["roofline"]["launch_share_of_cfg_batch"] == round(1 / 3, 4)
+    assert abs(j["roofline"]["flop_per_launch"] - 4.0 * 3 * 12 * 21504 ** 2 * 128 / 2 / 3) < 1e3
     assert j["replicas"]["scaling"] == "weak" and j["replicas"]["parallelism"] == "replicas2"
     for k in ("metric", "unit", "higher_is_better", "vs_baseline", "dtype", "data", "config", "roofline",
               "cpu_baseline"):
