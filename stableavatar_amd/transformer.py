@@ -225,10 +225,6 @@ class WanTransformer3DFantasyModel(nn.Module):
         self.teacache = None  # enable_teacache() (1B:867)
         self._riflex = None  # enable_riflex() (1B:890-905)
         self.attn_kernel = 0  # self-attention schedule (sa_attn_fwd_ex; 0 = auto), for in-situ A/B
-        # single-GPU layer loop with each CFG row on its own HIP stream (rows are independent inside the
-        # 30 blocks): a kernel's partial last round over the CUs is filled by the next kernel of another row
-        self.row_streams = os.environ.get("SA_ROW_STREAMS", "0") == "1"
-        self._streams = {}
         self._packed = None
         self._ws = {}
         self._ctx_cache = None
@@ -529,55 +525,6 @@ class WanTransformer3DFantasyModel(nn.Module):
         ops.layernorm_mod(x, hb, 1e-6, shift=ef[0, 0, 0:1], scale=ef[0, 0, 1:2], rows_per_batch=Mv)
         return ops.linear(hb, V.w_fp, V.b_fp, ops.EPI_BF16), Fn, nper
 
-    def _layers_by_row(self, pk, ws, emod, ctx, vctx, kvv, B, L, dim, H_, n_fr, nper, G, grid, dev):
-        """The 30 blocks (1B:650-695) for each CFG row on its own stream.  Same kernels and arguments per row
-        as the batched loop (a row's outputs depend only on its own rows of every operand): bit-identical.
-        With every row's kernel stream in flight, the CUs a kernel leaves idle in its last partial round
-        (252 x n tiles or 84 query blocks per head over 256 CUs) take the next row's kernel."""
-        key = (dev.index, B)
-        if key not in self._streams:
-            self._streams[key] = [torch.cuda.Stream(device=dev) for _ in range(B)]
-        streams = self._streams[key]
-        main = torch.cuda.current_stream(dev)
-        segs1 = self._segs.get(("self_row", L), [[0, L, 0, L]], dev)
-        tl, il, nv = ctx.text_len, ctx.img_len, n_fr * nper
-        rope_kw = dict(rope=pk.rope, rows_per_batch=L, tok_offset=0, grid=grid, head_dim=self.d,
-                       n_frame_pairs=self.d // 2 - 2 * (self.d // 6), n_height_pairs=self.d // 6)
-        for s_ in streams:
-            s_.wait_stream(main)
-        for b in range(B):
-            with torch.cuda.stream(streams[b]):
-                rs = slice(b * L, (b + 1) * L)
-                x, mod, qkv, att, ffn = ws.x[rs], ws.mod[rs], ws.qkv[rs], ws.att[rs], ws.ffn[rs]
-                vrow, kvvr = vctx[b * nv:(b + 1) * nv], kvv[b * nv:(b + 1) * nv]
-                for li, Lw in enumerate(pk.layers):
-                    em = emod[li, b:b + 1]  # [1, 6, dim]
-                    ops.layernorm_mod(x, mod, self.eps, shift=em[:, 0], scale=em[:, 1], rows_per_batch=L)
-                    ops.linear(mod, Lw.w_qkv, Lw.b_qkv, ops.EPI_BF16, out=qkv)
-                    ops.qk_rmsnorm_rope(qkv, 0, dim, Lw.nq, Lw.nk, dim, self.eps, **rope_kw)
-                    ev0 = self._record_event()
-                    ops.attention(qkv[:, :dim], qkv[:, dim:2 * dim], qkv[:, 2 * dim:], att, segs1, 1, L, H_,
-                                  kernel=self.attn_kernel)
-                    self._record_span(ev0, rows=1, batch=B)
-                    ops.linear(att, Lw.w_o, Lw.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2],
-                               rows_per_batch=L)
-                    ops.layernorm_mod(x, mod, self.eps, weight=Lw.n3w, bias=Lw.n3b)
-                    qc = qkv[:, :dim]
-                    ops.linear(mod, Lw.w_cq, Lw.b_cq, ops.EPI_BF16, out=qc)
-                    ops.qk_rmsnorm_rope(qc, 0, -1, Lw.cnq, None, dim, self.eps)
-                    kvt, kvi = ctx.kv[li]
-                    kvt, kvi = kvt[b * tl:(b + 1) * tl], kvi[b * il:(b + 1) * il]
-                    ops.linear(vrow, Lw.w_kv_v, Lw.b_kv_v, ops.EPI_BF16, out=kvvr)
-                    ops.attention_cross3(qc, kvt[:, :dim], kvt[:, dim:], tl, kvi[:, :dim], kvi[:, dim:], il,
-                                         kvvr[:, :dim], kvvr[:, dim:], nper, G, n_fr, att, 1, L, H_, tok_offset=0)
-                    ops.linear(att, Lw.w_co, Lw.b_co, ops.EPI_RES_F32, out=x, residual=x)
-                    ops.layernorm_mod(x, mod, self.eps, shift=em[:, 3], scale=em[:, 4], rows_per_batch=L)
-                    ops.linear(mod, Lw.w_f0, Lw.b_f0, ops.EPI_GELU_TANH_BF16, out=ffn)
-                    ops.linear(ffn, Lw.w_f2, Lw.b_f2, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 5],
-                               rows_per_batch=L)
-        for s_ in streams:
-            main.wait_stream(s_)
-
     # ------------------------------------------------------------------ timing hooks (bench.py)
 
     def _record_event(self):
@@ -738,10 +685,7 @@ class WanTransformer3DFantasyModel(nn.Module):
             x = ws.x
             kvv = torch.empty(B * n_fr * nper, 2 * dim, device=dev, dtype=torch.bfloat16)  # per-frame vocal K|V
             grid = (Fw, hp, wp)
-            by_row = not SP and use_cross3 and B > 1 and self.row_streams and dev.type == "cuda"
-            if by_row:
-                self._layers_by_row(pk, ws, emod, ctx, vctx, kvv, B, Lp, dim, H_, n_fr, nper, G, grid, dev)
-            for li, L in enumerate(() if by_row else pk.layers):
+            for li, L in enumerate(pk.layers):
                 em = emod[li]  # [B, 6, dim]
                 # self-attention (1B:675-679)
                 ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 0], scale=em[:, 1], rows_per_batch=Lc)

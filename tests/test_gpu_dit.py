@@ -90,25 +90,6 @@ def test_dit_fused_cross_attention_matches_unfused(monkeypatch):
     assert rel(fused, ref) < 1e-2 and cos(fused, ref) > 0.9999, (rel(fused, ref), cos(fused, ref))
 
 
-def test_dit_row_streams_bit_identical():
-    """The single-GPU layer loop with each CFG row on its own HIP stream (SA_ROW_STREAMS=1) equals the batched loop
-    bit for bit: same kernels and arguments per row; only the launch interleaving differs."""
-    from stableavatar_amd import synthetic as syn
-    m = make_model(DIT_SMALL)
-    B, Fw, H, W = 3, 2, 32, 32
-    lat = syn.seeded_normal((1, 16, Fw, H, W), 121)
-    inp = dict(x=torch.cat([lat] * 3), y=syn.seeded_normal((B, 20, Fw, H, W), 122),
-               context=[syn.seeded_normal((20, 64), 123)] * 2 + [syn.seeded_normal((25, 64), 124)],
-               clip_fea=syn.seeded_normal((1, 257, 1280), 125).expand(3, -1, -1).contiguous(),
-               vocal=torch.cat([torch.zeros(1, 15, 768), syn.seeded_normal((1, 15, 768), 126).repeat(2, 1, 1)]),
-               t=torch.full((3,), 700.0), seq_len=Fw * (H // 2) * (W // 2), n_frames=5)
-    m.row_streams = True
-    a = run(m, inp)
-    m.row_streams = False
-    b = run(m, inp)
-    assert torch.equal(a, b)
-
-
 def test_dit_qfloat8_weights():
     """GPU_memory_mode 'model_cpu_offload_and_qfloat8' (inference.py:517-518): every parameter except
     'modulation' stored as float8_e4m3fn (fp8_optimization.py:29-43).  The HIP path packs the fp8
