@@ -72,9 +72,13 @@ __global__ __launch_bounds__(256) void conv3d_cl_kernel(ConvArgs a) {
   constexpr int BPT = (BCH + 255) / 256;
 
   u32x4 ra[2], rb[BPT];
-  auto load = [&](int ks) {
-    const int k0 = ks * BK;
-    const int tap = k0 / a.Cin, ci0 = k0 % a.Cin;
+  // The K loop walks (tap, channel chunk) in order; the A-row source pointers are recomputed only
+  // when the tap changes (every Cin/BK steps) and the chunk offset advances in between, so the
+  // im2col index arithmetic is off the per-step path (Cin % BK == 0 is checked by the launcher).
+  const bf16* asrc[2];
+  int ld_tap = 0, ld_ci = 0;
+  long ld_k0 = 0;
+  auto set_tap = [&](int tap) {
     const int dt = tap / (a.kh * a.kw), dh = (tap / a.kw) % a.kh, dw = tap % a.kw;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -96,6 +100,7 @@ __global__ __launch_bounds__(256) void conv3d_cl_kernel(ConvArgs a) {
         wi = aw[j] + dw - (a.kw - 1) / 2;
         ok = arow_ok[j] && (ti >= 0 || a.xprev) && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
       }
+      asrc[j] = nullptr;
       if (ok) {
         const int hp = a.upsample ? (hi >> 1) : hi, wp = a.upsample ? (wi >> 1) : wi;
         const bf16* xb = a.x;
@@ -103,19 +108,28 @@ __global__ __launch_bounds__(256) void conv3d_cl_kernel(ConvArgs a) {
           xb = a.xprev;
           ti += a.kt - 1;
         }
-        const bf16* src = xb + (((long)ti * a.Hin + hp) * a.Win + wp) * a.Cin + ci0 + ac[j] * 8;
-        ra[j] = *(const u32x4*)src;
-      } else {
-        ra[j] = (u32x4){0u, 0u, 0u, 0u};
+        asrc[j] = xb + (((long)ti * a.Hin + hp) * a.Win + wp) * a.Cin + ac[j] * 8;
       }
     }
+  };
+  auto load = [&]() {  // loads step (ld_tap, ld_ci) and advances to the next one
+    if (ld_ci == 0) set_tap(ld_tap);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      ra[j] = asrc[j] ? *(const u32x4*)(asrc[j] + ld_ci) : (u32x4){0u, 0u, 0u, 0u};
 #pragma unroll
     for (int j = 0; j < BPT; ++j) {
       const int idx = tid + j * 256;
       if (idx < BCH) {
         const int r = idx >> 2, c = idx & 3;
-        rb[j] = *(const u32x4*)(a.w + (long)(n0 + r) * K + k0 + c * 8);
+        rb[j] = *(const u32x4*)(a.w + (long)(n0 + r) * K + ld_k0 + c * 8);
       }
+    }
+    ld_k0 += BK;
+    ld_ci += BK;
+    if (ld_ci == a.Cin) {
+      ld_ci = 0;
+      ++ld_tap;
     }
   };
   auto store = [&](int buf) {
@@ -134,12 +148,12 @@ __global__ __launch_bounds__(256) void conv3d_cl_kernel(ConvArgs a) {
 #pragma unroll
     for (int n = 0; n < NT; ++n) acc[i][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  load(0);
+  load();
   for (int ks = 0; ks < nk; ++ks) {
     const int buf = ks & 1;
     store(buf);
     __syncthreads();
-    if (ks + 1 < nk) load(ks + 1);
+    if (ks + 1 < nk) load();
     const int c = lane >> 4;
     bf16x8 af[2];
 #pragma unroll
