@@ -152,8 +152,8 @@ __global__ __launch_bounds__(256) void conv3d_cl_kernel(ConvArgs a) {
   for (int ks = 0; ks < nk; ++ks) {
     const int buf = ks & 1;
     store(buf);
+    if (ks + 1 < nk) load();  // issued before the barrier: the wait at the barrier hides part of its latency
     __syncthreads();
-    if (ks + 1 < nk) load();
     const int c = lane >> 4;
     bf16x8 af[2];
 #pragma unroll
