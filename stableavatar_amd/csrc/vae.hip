@@ -142,11 +142,16 @@ __global__ __launch_bounds__(256) void conv3d_cl_kernel(ConvArgs a) {
     }
   };
 
-  f32x4 acc[2][NT];
+  // wave tile: WM x WN waves over the BM x BN tile; each wave holds AI 16-row A fragments x NB 16-column
+  // B fragments (2 x 2 when NT is even: 4 + NT/2 fragment reads per NT*2 MFMAs instead of 2 + NT)
+  constexpr int WN = NT % 2 == 0 ? 2 : 1, WM = 4 / WN;
+  constexpr int AI = BM / WM / 16, NB = NT / WN;
+  const int wm = wave / WN, wn = wave % WN;
+  f32x4 acc[AI][NB];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < AI; ++i)
 #pragma unroll
-    for (int n = 0; n < NT; ++n) acc[i][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < NB; ++n) acc[i][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   load();
   for (int ks = 0; ks < nk; ++ks) {
@@ -155,37 +160,38 @@ __global__ __launch_bounds__(256) void conv3d_cl_kernel(ConvArgs a) {
     if (ks + 1 < nk) load();  // issued before the barrier: the wait at the barrier hides part of its latency
     __syncthreads();
     const int c = lane >> 4;
-    bf16x8 af[2];
+    bf16x8 af[AI];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(smem + buf * SBYTES + swz64(wave * 32 + i * 16 + (lane & 15), c));
+    for (int i = 0; i < AI; ++i)
+      af[i] = *(const bf16x8*)(smem + buf * SBYTES + swz64(wm * AI * 16 + i * 16 + (lane & 15), c));
 #pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      const bf16x8 bfr = *(const bf16x8*)(smem + buf * SBYTES + BM * 64 + swz64(n * 16 + (lane & 15), c));
+    for (int n = 0; n < NB; ++n) {
+      const bf16x8 bfr = *(const bf16x8*)(smem + buf * SBYTES + BM * 64 + swz64((wn * NB + n) * 16 + (lane & 15), c));
 #pragma unroll
-      for (int i = 0; i < 2; ++i) acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][n], 0, 0, 0);
+      for (int i = 0; i < AI; ++i) acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][n], 0, 0, 0);
     }
   }
   __syncthreads();
 
-  // epilogue through a per-wave 16 x BN fp32 strip
-  constexpr int LD = BN + 4;
+  // epilogue through a per-wave 16 x (NB*16) fp32 strip
+  constexpr int LD = NB * 16 + 4;
   float* strip = (float*)(smem + wave * 16 * LD * 4);
   const int er = lane >> 2, q = lane & 3;
-  constexpr int CPL = BN / 4;  // columns per lane
+  constexpr int CPL = NB * 4;  // columns per lane
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < AI; ++i) {
 #pragma unroll
-    for (int n = 0; n < NT; ++n)
+    for (int n = 0; n < NB; ++n)
 #pragma unroll
       for (int r = 0; r < 4; ++r) strip[((lane >> 4) * 4 + r) * LD + n * 16 + (lane & 15)] = acc[i][n][r];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    const long m = m0 + wave * 32 + i * 16 + er;
+    const long m = m0 + wm * AI * 16 + i * 16 + er;
     if (m < a.M) {
       const long t = m / HW, p = m % HW;
 #pragma unroll
       for (int g = 0; g < CPL; g += 4) {
-        const int n = n0 + q * CPL + g;
+        const int n = n0 + wn * NB * 16 + q * CPL + g;
         if (n < a.Cout) {
           float v[4];
 #pragma unroll
