@@ -30,6 +30,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "denoised frames/sec, Wan-1.3B 512²×81f audio-driven, 1/2/4/8 MI355X"
+T0 = time.time()  # the time budget counts from process start
 PEAK_BF16 = 2.5e15  # dense bf16 MFMA, MI355X_MICROARCH.md
 ATTN_KERNEL_NAME = "attn_fwd_v6_kernel"
 
@@ -46,12 +47,23 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-cpu-config1", action="store_true",
                    help="skip the config-1 run of the CPU oracle inside cpu_baseline")
-    p.add_argument("--cpu-config1-steps", type=int, default=1,
+    p.add_argument("--cpu-config1-steps", type=int, default=5,
                    help="sampling steps of the config-1 CPU oracle run actually executed (1..5; the rest of the 5 "
                         "are extrapolated from the measured per-step time; 5 = fully end to end)")
     p.add_argument("--no-encode", action="store_true", help="skip the (untimed) VAE encode measurement")
-    p.add_argument("--no-dit14", action="store_true",
-                   help="skip the (untimed) per-block measurement of the 14B model at config 4's 720p geometry")
+    p.add_argument("--dit14", action="store_true",
+                   help="also time (untimed extra) one block of the 14B model at config 4's 720p geometry")
+    p.add_argument("--no-dit14", action="store_true", help=argparse.SUPPRESS)  # the default since round 3
+    p.add_argument("--time-budget", type=float, default=540.0,
+                   help="seconds from process start within which the untimed extras must end (the driver kills "
+                        "the run at 600 s): the CPU baseline's config-1 leg, the VAE encode and --dit14 are "
+                        "skipped, and say so in the JSON, when they would not fit")
+    p.add_argument("--cpu-child", type=str, default=None, help=argparse.SUPPRESS)  # internal: CPU baseline process
+    p.add_argument("--vae-parallel", action="store_true",
+                   help="N>1 sp / window-dp: split the VAE decode over the ranks (default: every rank decodes "
+                        "the whole clip, as the reference does)")
+    p.add_argument("--replica-warmup", type=int, default=1,
+                   help="sp mode: untimed replicas clips per rank after the layout switch, before the timed ones")
     p.add_argument("--mode", choices=("sp", "replicas", "window-dp"), default=None,
                    help="N>1 layout (default sp); ignored at N=1")
     p.add_argument("--sp", action="store_true", help="alias of --mode sp")
@@ -111,18 +123,28 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(size, frames, sample_steps, n_fwd, out_frames, config1=True, config1_steps=1):
-    """The CPU oracle (oracle/, fp32 restatement of the reference) on this host's cores:
-    (a) config 2, bounded sample: one of the 30 DiT blocks at the full shape + the VAE decoder on one
-        latent frame, extrapolated to the clip (n_fwd forwards x 30 blocks + out_frames frames);
-    (b) config 1 (BASELINE.json configs[0]): the restated pipeline with the full 30-layer DiT at 256x256
-        clip 17 (2 windows per step) + the full VAE decode of the 21-frame video; config1_steps of its 5
-        sampling steps run (5 = end to end), the others extrapolated at the measured per-step time."""
+def _emit(path, rec):
+    with open(path, "a") as f:
+        f.write(json.dumps(rec) + "\n")
+
+
+def cpu_child(args):
+    """`bench.py --cpu-child PATH`: the CPU baseline in its own process, started by the N = 1 bench before it
+    touches the GPU so that it runs during the (untimed) warmup clips and has ended before the timed region
+    starts.  No GPU use here.  Each finished leg is appended to PATH as one JSON line:
+    (a) config 2, bounded sample: one of the 30 DiT blocks at the full shape + the VAE decoder on one latent
+        frame (the parent extrapolates them to the clip: forwards x 30 blocks + output frames);
+    (b) config 1 (BASELINE.json configs[0]): the restated pipeline with the full 30-layer DiT at 256x256,
+        clip 17 (2 windows per step) + the full VAE decode of the 21-frame video, one line per sampling step
+        and one at the end."""
     from oracle import dit as odit
+    from oracle import pipeline as opipe
     from oracle import vae as ovae
     from stableavatar_amd import synthetic
-    threads = cpu_cores()
+    path = args.cpu_child
+    threads = max(1, cpu_cores() - 1)  # one core stays with the GPU process's launch thread
     torch.set_num_threads(threads)
+    size, frames = args.size, args.frames
     h = size // 8
     T = (frames - 1) // 4 + 1
     L = T * (h // 2) ** 2
@@ -144,62 +166,136 @@ def cpu_baseline(size, frames, sample_steps, n_fwd, out_frames, config1=True, co
         ovae.decode(Pv, z)
         t_vae_frame = time.time() - t0
     del P, x, ctx, voc
-    t_clip = n_fwd * 30 * t_block + out_frames * t_vae_frame
-    out = {"value": round(out_frames / t_clip, 6), "unit": "frames/s", "cores": threads, "kind": "port",
-           "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
-           "sample": f"oracle fp32 (oracle/dit.py, oracle/vae.py) on {threads} threads: 1 of 30 DiT blocks at "
-                     f"B=3,L={L} ({t_block:.1f}s) + VAE decode of 1 latent frame at {size}x{size} "
-                     f"({t_vae_frame:.1f}s), extrapolated to {n_fwd} forwards x 30 blocks + {out_frames} frames "
-                     f"= {t_clip:.0f}s per clip"}
-    if config1:
-        out["config_1"] = cpu_config1(Pv, config1_steps)
-    return out
-
-
-def cpu_config1(Pv, run_steps=5):
-    """BASELINE config 1 on the CPU oracle: the full 30-layer DiT (synthetic weights) through the
-    restated sliding-window loop (oracle/pipeline.py) + the full VAE decode; encoders excluded (once
-    per call).  run_steps of the 5 sampling steps are executed (the denoise loop takes
-    the first run_steps sigmas of the 5-step schedule); the remaining steps cost the measured per-step
-    time."""
-    from oracle import dit as odit
-    from oracle import pipeline as opipe
-    from oracle import vae as ovae
-    from stableavatar_amd import synthetic
+    _emit(path, {"leg": "config2", "t_block": t_block, "t_vae_frame": t_vae_frame, "L": L, "threads": threads})
+    if args.no_cpu_config1:
+        return 0
+    # config 1: the 30-layer DiT (synthetic weights) through the restated sliding-window loop + the full decode;
+    # encoders excluded (once per call)
     cfg = dict(odit.CONFIG_1_3B)
     Pd = synthetic.fill_state_dict(odit.param_shapes(cfg), 41)
-    size, clip_length, steps, overlap, audio_frames = 256, 17, 5, 2, 24
-    run_steps = max(1, min(steps, run_steps))
-    T = (audio_frames - 1) // 4 + 1
-    lat0 = synthetic.seeded_normal((1, 16, T, size // 8, size // 8), 301)
-    y = synthetic.seeded_normal((3, 20, (clip_length - 1) // 4 + 1, size // 8, size // 8), 302)
-    ctx = [synthetic.seeded_normal((24, 4096), 303)] * 2 + [synthetic.seeded_normal((31, 4096), 304)]
+    size1, clip_length, steps, overlap, audio_frames = 256, 17, 5, 2, 24
+    run_steps = max(1, min(steps, args.cpu_config1_steps))
+    T1 = (audio_frames - 1) // 4 + 1
+    lat0 = synthetic.seeded_normal((1, 16, T1, size1 // 8, size1 // 8), 301)
+    y = synthetic.seeded_normal((3, 20, (clip_length - 1) // 4 + 1, size1 // 8, size1 // 8), 302)
+    ctx1 = [synthetic.seeded_normal((24, 4096), 303)] * 2 + [synthetic.seeded_normal((31, 4096), 304)]
     clip = synthetic.seeded_normal((1, 257, 1280), 305).expand(3, -1, -1).contiguous()
     audio = synthetic.seeded_normal((audio_frames * 640,), 306, 0.1)
     n_fwd = [0]
 
-    def dit(x, t, context, seq_len, yy, clip_fea, vocal, n):
+    def dit(xx, t, context, seq_len, yy, clip_fea, vocal, n):
         n_fwd[0] += 1
-        return odit.forward(Pd, cfg, x, t, context, seq_len, clip_fea, yy, vocal, n)
+        return odit.forward(Pd, cfg, xx, t, context, seq_len, clip_fea, yy, vocal, n)
 
     enc = lambda s: synthetic.fake_wav2vec_features(torch.as_tensor(s)[None])  # noqa: E731
+    t0 = time.time()
+    step_cb = lambda i: _emit(path, {"leg": "config1_step", "i": i, "s": time.time() - t0,  # noqa: E731
+                                     "dit_forwards": n_fwd[0]})
     with torch.no_grad():
-        t0 = time.time()
-        lat = opipe.denoise(dit, lat0, y, ctx, clip, audio, enc, num_inference_steps=steps, clip_length=clip_length,
-                            num_frames=clip_length, height=size, width=size, overlap=overlap, text_guide_scale=3.0,
-                            audio_guide_scale=5.0, max_steps=run_steps)
+        lat = opipe.denoise(dit, lat0, y, ctx1, clip, audio, enc, num_inference_steps=steps, clip_length=clip_length,
+                            num_frames=clip_length, height=size1, width=size1, overlap=overlap, text_guide_scale=3.0,
+                            audio_guide_scale=5.0, max_steps=run_steps, step_callback=step_cb)
         t_denoise = time.time() - t0
         t1 = time.time()
         video = ovae.decode(Pv, lat)
         t_decode = time.time() - t1
     n_out = video.shape[2]
     total = t_denoise * steps / run_steps + t_decode
-    return {"value": round(n_out / total, 5), "unit": "frames/s", "seconds": round(total, 1),
-            "denoise_s_measured": round(t_denoise, 1), "decode_s": round(t_decode, 1), "steps_run": run_steps,
-            "dit_forwards_run": n_fwd[0], "frames": n_out,
-            "workload": f"Wan-1.3B 30 layers {size}x{size}, clip {clip_length}, {audio_frames} frames of audio "
-                        f"(T_lat {T}, 2 windows/step), {steps} steps, fp32, + VAE decode"
-                        + ("" if run_steps == steps else f"; {run_steps} of {steps} steps run, the rest extrapolated")}
+    _emit(path, {"leg": "config1", "value": round(n_out / total, 5), "unit": "frames/s", "seconds": round(total, 1),
+                 "denoise_s_measured": round(t_denoise, 1), "decode_s": round(t_decode, 1), "steps_run": run_steps,
+                 "dit_forwards_run": n_fwd[0], "frames": n_out, "threads": threads,
+                 "workload": f"Wan-1.3B 30 layers {size1}x{size1}, clip {clip_length}, {audio_frames} frames of audio "
+                             f"(T_lat {T1}, 2 windows/step), {steps} steps, fp32, + VAE decode"
+                             + ("" if run_steps == steps else
+                                f"; {run_steps} of {steps} steps run, the rest extrapolated")})
+    return 0
+
+
+class CpuBaseline:
+    """The parent's handle on the CPU-baseline child process (see cpu_child)."""
+
+    def __init__(self, args):
+        import tempfile
+        fd, self.path = tempfile.mkstemp(prefix="sa_cpu_baseline_", suffix=".jsonl")
+        os.close(fd)
+        self.log = self.path[:-6] + ".log"
+        argv = [sys.executable, os.path.abspath(__file__), "--cpu-child", self.path, "--size", str(args.size),
+                "--frames", str(args.frames), "--cpu-config1-steps", str(args.cpu_config1_steps)]
+        if args.no_cpu_config1:
+            argv.append("--no-cpu-config1")
+        self.t_start = time.time()
+        with open(self.log, "w") as lf:
+            self.proc = subprocess.Popen(argv, stdout=lf, stderr=subprocess.STDOUT)
+        self.killed = False
+
+    def records(self):
+        try:
+            with open(self.path) as f:
+                return [json.loads(ln) for ln in f if ln.strip()]
+        except (OSError, ValueError):
+            return []
+
+    def _has(self, leg):
+        return any(r["leg"] == leg for r in self.records())
+
+    def wait(self, deadline, required_by):
+        """wait for the child to end; past `deadline` (time.time()) end it, but never before the config-2 leg
+        is in (bounded by `required_by`)"""
+        while self.proc.poll() is None:
+            now = time.time()
+            if now > deadline and (self._has("config2") or now > required_by):
+                self.proc.terminate()
+                try:
+                    self.proc.wait(timeout=10)
+                except subprocess.TimeoutExpired:
+                    self.proc.kill()
+                    self.proc.wait()
+                self.killed = True
+                break
+            time.sleep(0.5)
+        return self.proc.returncode
+
+    def result(self, n_fwd, out_frames, size):
+        recs = self.records()
+        c2 = next((r for r in recs if r["leg"] == "config2"), None)
+        if c2 is None:
+            tail = ""
+            try:
+                with open(self.log) as f:
+                    tail = f.read()[-400:]
+            except OSError:
+                pass
+            return {"value": None, "error": f"CPU baseline child ended without a result (rc {self.proc.returncode})",
+                    "log_tail": tail}
+        t_clip = n_fwd * 30 * c2["t_block"] + out_frames * c2["t_vae_frame"]
+        th = c2["threads"]
+        out = {"value": round(out_frames / t_clip, 6), "unit": "frames/s", "cores": th, "kind": "port",
+               "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+               "sample": f"oracle fp32 (oracle/dit.py, oracle/vae.py) on {th} threads (one core of this process's "
+                         f"share left to the GPU launch thread; run during the untimed warmup clips, ended before "
+                         f"the timed region): 1 of 30 DiT blocks at B=3,L={c2['L']} ({c2['t_block']:.1f}s) + VAE "
+                         f"decode of 1 latent frame at {size}x{size} ({c2['t_vae_frame']:.1f}s), extrapolated to "
+                         f"{n_fwd} forwards x 30 blocks + {out_frames} frames = {t_clip:.0f}s per clip"}
+        c1 = next((r for r in recs if r["leg"] == "config1"), None)
+        if c1 is not None:
+            c1 = {k: v for k, v in c1.items() if k != "leg"}
+        else:
+            steps = [r for r in recs if r["leg"] == "config1_step"]
+            c1 = {"value": None, "skipped": "not finished within the time budget" if self.killed else
+                  "not run" if not steps else "child ended early", "steps_done": len(steps),
+                  "step_s": [round(b["s"] - a, 1) for a, b in zip([0.0] + [s["s"] for s in steps], steps)]}
+        out["config_1"] = c1
+        return out
+
+    def cleanup(self):
+        if self.proc.poll() is None:
+            self.proc.kill()
+            self.proc.wait()
+        for p in (self.path, self.log):
+            try:
+                os.remove(p)
+            except OSError:
+                pass
 
 
 # ------------------------------------------------------------------------------------------------ GPU workload
@@ -257,11 +353,13 @@ class ClipWorkload:
         self.layout = layout
         self.dit.disable_multi_gpus_inference()
         self.pipe.disable_window_parallel()
-        if layout == "sp":  # Ulysses DiT + the VAE decode split over the ranks
+        if layout == "sp":  # Ulysses DiT
             self.dit.enable_multi_gpus_inference()
-            self.pipe._decode_group_sync()
-        elif layout == "window-dp":  # windows + the VAE decode split over the ranks
+        elif layout == "window-dp":  # the windows of each step over the ranks
             self.pipe.enable_window_parallel()
+        # --vae-parallel: the decode split over the ranks of a shared clip (else every rank decodes it whole)
+        self.pipe.enable_vae_parallel(getattr(self.args, "vae_parallel", False) and layout in ("sp", "window-dp"))
+        self.pipe._decode_group_sync()
         shared = layout in ("sp", "window-dp")  # one clip over all ranks
         a = self.args
         self.latents, self.y, self.ctx, self.clip, au = make_inputs(self.dev, a.frames, a.size,
@@ -313,11 +411,17 @@ def barrier(world, dev):
         sync(dev)
 
 
-def timed(work, steps, warmup, world, dev, events=False):
-    """W untimed warmup steps, then EXACTLY K steps between barriers; the max over ranks."""
+def timed(work, steps, warmup, world, dev, events=False, before_timed=None):
+    """W untimed warmup steps, then EXACTLY K steps between barriers; the max over ranks.
+    before_timed(warmup_seconds) runs after the warmup, before the opening barrier."""
     with torch.no_grad():
+        tw = time.perf_counter()
         for _ in range(warmup):
             work.step()
+        sync(dev)
+        tw = time.perf_counter() - tw
+        if before_timed is not None:
+            before_timed(tw)
         barrier(world, dev)
         if events:
             work.start_events()
@@ -366,14 +470,31 @@ def attn_traffic(seq_len, layout):
     return tj["hbm_bytes_per_launch"], f"profiles/pmc_attn_traffic.json ({tj.get('source', 'rocprofv3 --pmc')})"
 
 
-def run(args, world, rank, dev, work_factory=ClipWorkload):
-    """The measurement; returns the JSON dict on rank 0 (None elsewhere)."""
+POST_RESERVE_S = 15.0  # after the timed region: result assembly, JSON, process-group teardown
+
+
+def run(args, world, rank, dev, work_factory=ClipWorkload, cpu=None):
+    """The measurement; returns the JSON dict on rank 0 (None elsewhere).  `cpu`: the CpuBaseline child
+    (N = 1), collected after the warmup so it never overlaps the timed region."""
     from stableavatar_amd import flops
     from stableavatar_amd import sp
+    budget_end = T0 + args.time_budget
+    skipped = []
     layout = "single" if world == 1 else args.mode
     work = work_factory(args, dev, rank, world)
     work.set_layout(layout)
-    dt, video = timed(work, args.steps, args.warmup, world, dev, events=True)
+
+    def collect_cpu(t_warm):
+        if cpu is None:
+            return
+        per_step = t_warm / args.warmup if args.warmup > 0 else None
+        if per_step is None:  # no warmup to size the timed region by: the mandatory config-2 leg only
+            deadline = time.time()
+        else:
+            deadline = budget_end - args.steps * per_step - POST_RESERVE_S
+        cpu.wait(deadline, required_by=time.time() + 180.0)
+
+    dt, video = timed(work, args.steps, args.warmup, world, dev, events=True, before_timed=collect_cpu)
     work.check(video)
     attn_ms, attn_share = work.attention_launch_ms()
     seq_len = work.seq_len
@@ -391,31 +512,46 @@ def run(args, world, rank, dev, work_factory=ClipWorkload):
         flops.vae_decode_flops(work.T, work.h, work.h)
     replicas = None
     if layout == "sp" and args.replica_steps > 0:
-        work.set_layout("replicas")
-        rdt, rvideo = timed(work, args.replica_steps, 0, world, dev)
-        work.check(rvideo)
-        replicas = {"value": round(world * work.out_frames * args.replica_steps / rdt, 4), "unit": "frames/s",
-                    "steps": args.replica_steps, "ms_per_step": round(rdt / args.replica_steps * 1e3, 1),
-                    "scaling": "weak", "parallelism": f"replicas{world}",
-                    "note": "one independent clip per rank in the same processes (no data-path collective)"}
+        # the layout switch changes the DiT's per-rank token count (workspaces, segment tables): untimed
+        # warmup clips first
+        est = (dt / args.steps) * world * (args.replica_steps + args.replica_warmup)
+        if time.time() + est < budget_end:
+            work.set_layout("replicas")
+            rdt, rvideo = timed(work, args.replica_steps, args.replica_warmup, world, dev)
+            work.check(rvideo)
+            replicas = {"value": round(world * work.out_frames * args.replica_steps / rdt, 4), "unit": "frames/s",
+                        "steps": args.replica_steps, "warmup": args.replica_warmup,
+                        "ms_per_step": round(rdt / args.replica_steps * 1e3, 1),
+                        "scaling": "weak", "parallelism": f"replicas{world}",
+                        "note": "one independent clip per rank in the same processes (no data-path collective)"}
+        else:
+            skipped.append("replicas (would not fit the time budget)")
     enc = None
     if not args.no_encode and rank == 0 and hasattr(work, "vae"):
-        enc = vae_encode_ms(work.vae, args.frames, args.size, dev)
+        if time.time() + 10.0 < budget_end:
+            enc = vae_encode_ms(work.vae, args.frames, args.size, dev)
+        else:
+            skipped.append("vae_encode (time budget)")
     dit14 = None
-    if world == 1 and not args.no_dit14 and hasattr(work, "dit"):
-        from stableavatar_amd.kbench import bench_dit14
-        dit14 = dict(bench_dit14(), note="BASELINE config 4's model (Wan-14B StableAvatar widths: dim 5120, 40 heads, "
-                                         "ffn 13824) at 720x1280, 81 frames (L = 75 600, B = 3) on one GPU: forwards "
-                                         "with 1 and 2 blocks, one block's time from their difference, the 40-block "
-                                         "forward projected; outside the timed region and the metric")
+    if world == 1 and args.dit14 and hasattr(work, "dit"):
+        if time.time() + 40.0 < budget_end:
+            from stableavatar_amd.kbench import bench_dit14
+            dit14 = dict(bench_dit14(), note="BASELINE config 4's model (Wan-14B StableAvatar widths: dim 5120, 40 "
+                                             "heads, ffn 13824) at 720x1280, 81 frames (L = 75 600, B = 3) on one "
+                                             "GPU: forwards with 1 and 2 blocks, one block's time from their "
+                                             "difference, the 40-block forward projected; outside the timed region "
+                                             "and the metric")
+        else:
+            skipped.append("config_4_dit14 (time budget)")
     if rank != 0:
         return None
     traffic, traffic_src = attn_traffic(seq_len, layout)
     achieved = attn_flop / (attn_ms * 1e-3) if attn_ms else None
-    cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.size, args.frames, args.sample_steps, n_fwd, work.out_frames,
-                           config1=not args.no_cpu_config1, config1_steps=args.cpu_config1_steps)
+    cpu_res = None
+    if cpu is not None:
+        cpu_res = cpu.result(n_fwd, work.out_frames, args.size)
+        if cpu_res.get("config_1", {}).get("value", 0) is None:
+            skipped.append("cpu_baseline.config_1 (" + cpu_res["config_1"]["skipped"] + ")")
     n_win = len(work.wins)
     out = {"metric": METRIC, "value": round(value, 4), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 1), "higher_is_better": True,
@@ -427,7 +563,9 @@ def run(args, world, rank, dev, work_factory=ClipWorkload):
                                      if work.out_frames != args.frames else "")
                                   + f", {args.sample_steps} steps, CFG x3, single audio clip, VAE decode",
                       "global_batch": 3 * (1 if shared else world), "seq_len": seq_len,
-                      "dit_forwards_per_clip": n_fwd, "parallelism": parallelism},
+                      "dit_forwards_per_clip": n_fwd, "parallelism": parallelism,
+                      "vae_decode": "split over the ranks" if (shared and world > 1 and args.vae_parallel)
+                      else "whole clip on every rank" if world > 1 else "one GPU"},
            "roofline": {"bound": "mfma", "kernel": f"{ATTN_KERNEL_NAME} (self-attention, flash, D=128)",
                         "achieved": round(achieved / 1e12, 1) if achieved else None, "peak": PEAK_BF16 / 1e12,
                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16, 4) if achieved else None,
@@ -436,7 +574,9 @@ def run(args, world, rank, dev, work_factory=ClipWorkload):
                         "launch_share_of_cfg_batch": round(attn_share, 4),
                         "launch_ms": round(attn_ms, 3) if attn_ms else None, "flop_per_launch": attn_flop},
            "path_mfma_frac": round(path_flop * args.steps / dt / PEAK_BF16 / (world if shared else 1), 4),
-           "cpu_baseline": cpu, "vae_encode": enc, "config_4_dit14": dit14}
+           "cpu_baseline": cpu_res, "vae_encode": enc, "config_4_dit14": dit14,
+           "time_budget": {"budget_s": args.time_budget, "elapsed_s": round(time.time() - T0, 1),
+                           "skipped": skipped}}
     if replicas is not None:
         out["replicas"] = replicas
     return out
@@ -445,6 +585,8 @@ def run(args, world, rank, dev, work_factory=ClipWorkload):
 def main(argv=None, work_factory=ClipWorkload, device=None):
     argv = sys.argv[1:] if argv is None else list(argv)
     args = parse(argv)
+    if args.cpu_child:
+        return cpu_child(args)
     if args.sp:
         args.mode = "sp"
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -454,25 +596,32 @@ def main(argv=None, work_factory=ClipWorkload, device=None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    if device is None:
-        dev = torch.device(f"cuda:{local}")
-        torch.cuda.set_device(dev)
-    else:
-        dev = torch.device(device)
-    if world > 1:
-        import torch.distributed as dist
-        if not dist.is_initialized():
-            if dev.type == "cuda":
-                dist.init_process_group("nccl", device_id=dev)
-            else:
-                dist.init_process_group("gloo")
-    out = run(args, world, rank, dev, work_factory)
-    if out is not None:
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-        dist.destroy_process_group()
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = CpuBaseline(args)  # started before this process touches the GPU (a plain child, no exec of ours)
+    try:
+        if device is None:
+            dev = torch.device(f"cuda:{local}")
+            torch.cuda.set_device(dev)
+        else:
+            dev = torch.device(device)
+        if world > 1:
+            import torch.distributed as dist
+            if not dist.is_initialized():
+                if dev.type == "cuda":
+                    dist.init_process_group("nccl", device_id=dev)
+                else:
+                    dist.init_process_group("gloo")
+        out = run(args, world, rank, dev, work_factory, cpu=cpu)
+        if out is not None:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+            dist.destroy_process_group()
+    finally:
+        if cpu is not None:
+            cpu.cleanup()
     return 0
 
 

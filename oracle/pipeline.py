@@ -75,7 +75,7 @@ def audio_window(index_start, index_end, infer_length, audio_token_per_frame, ma
 
 def denoise(dit, latents, y, context, clip_ctx, audio, audio_encoder, *, num_inference_steps, clip_length,
             num_frames, height, width, overlap, text_guide_scale, audio_guide_scale, sr=16000, fps=25,
-            scheme="uniform", shift=5.0, patch=(1, 2, 2), max_steps=None):
+            scheme="uniform", shift=5.0, patch=(1, 2, 2), max_steps=None, step_callback=None):
     """Restated loop of pipeline:703-790.  `dit(x, t, context, seq_len, y, clip_fea, vocal, n)` is the
     denoiser; `audio_encoder(samples [n]) -> [1, tokens, 768]`.  Returns latents_all (fp32 holding
     bf16-rounded values like the reference, :771,:776)."""
@@ -112,4 +112,6 @@ def denoise(dit, latents, y, context, clip_ctx, audio, audio_encoder, *, num_inf
             for k in range(nf):
                 pred[:, :, (s + k) % pred.shape[2]] = lat[:, :, k].to(pred.dtype)
         latents_all = pred
+        if step_callback is not None:  # progress of a timed run (bench.py's CPU baseline)
+            step_callback(i)
     return latents_all

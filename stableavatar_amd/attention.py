@@ -40,6 +40,8 @@ def attention(q, k, v, q_lens=None, k_lens=None, dropout_p=0., softmax_scale=Non
                       'impact on performance.')
     Lk = k.shape[1]
     out_dtype = q.dtype
+    if Lk == 0 or Lq == 0:  # SDPA over no keys returns zeros
+        return torch.zeros(B, Lq, N, D, device=q.device, dtype=out_dtype)
     qb, kb, vb = (t.to(torch.bfloat16).contiguous().view(-1, N * D) for t in (q, k, v))
     o = torch.empty(B * Lq, N * D, device=q.device, dtype=torch.bfloat16)
     segs = torch.tensor([[b * Lq, Lq, b * Lk, Lk] for b in range(B)], dtype=torch.int32).to(q.device)

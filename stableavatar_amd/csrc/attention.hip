@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* q, const bf
   }
   sum = wave_sum(sum);
   __builtin_amdgcn_wave_barrier();
-  const float inv = 1.f / sum;
+  const float inv = sum > 0.f ? 1.f / sum : 0.f;  // no keys: zeros, as SDPA
   bf16* op = o + (long)(q_row0 + qi) * os + h * D;
   for (int d = lane; d < D; d += 64) {
     float acc = 0.f;
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(256) void attn_small2_kernel(const bf16* q, const b
     for (int qq = 0; qq < 8; ++qq) {
       const int qi = q0 + w * 8 + qq;
       if (qi < q_len) {
-        const float inv = 1.f / l[qq];
+        const float inv = l[qq] > 0.f ? 1.f / l[qq] : 0.f;  // a segment with no keys: zeros, as SDPA
         *(bf16x4*)(o + (long)(q_row0 + qi) * os + h * D + 4 * lane) =
             (bf16x4){f2bf(O[qq][0] * inv), f2bf(O[qq][1] * inv), f2bf(O[qq][2] * inv), f2bf(O[qq][3] * inv)};
       }
@@ -518,8 +518,16 @@ __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
   const int qb = flat % nx, h = (flat / nx) % ny, seg = flat / (nx * ny);
   const int* sg = a.segs + seg * 4;
   const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
-  if (qb * QBW >= q_len || kv_len <= 0) return;
+  if (qb * QBW >= q_len) return;
   const int tid = threadIdx.x, lane = tid & 63;
+  if (kv_len <= 0) {  // a segment with no keys: zeros, as SDPA (nothing to add when accumulating)
+    if (!a.accumulate)
+      for (int i = tid; i < QBW * (D / 8); i += NW * 64) {
+        const int qi = qb * QBW + i / (D / 8);
+        if (qi < q_len) *(u32x4*)(a.o + (long)(q_row0 + qi) * a.os + h * D + (i % (D / 8)) * 8) = (u32x4){0u, 0u, 0u, 0u};
+      }
+    return;
+  }
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
 

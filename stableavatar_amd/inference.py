@@ -81,7 +81,32 @@ def parse_args(argv=None):
     p.add_argument("--window_parallel", action="store_true",
                    help="multi-GPU: spread the sliding windows of each step over the ranks instead of sequence "
                         "parallelism (long clips, SURVEY.md §8(e))")
-    return p.parse_args(argv)
+    p.add_argument("--vae_parallel", action="store_true",
+                   help="multi-GPU: split the VAE decode over the ranks (a wavefront of causal-cache hand-offs); "
+                        "off by default: every rank decodes the whole clip, as the reference does")
+    args = p.parse_args(argv)
+    if args.window_parallel and args.enable_teacache:
+        # checked before any model is loaded (the pipeline would raise at its first denoise step)
+        p.error("--window_parallel cannot be combined with --enable_teacache: TeaCache's skip decisions follow the "
+                "sequence of forwards one process runs (cache_utils.py:59-80), which window parallelism changes")
+    if args.window_parallel and (args.ulysses_degree > 1 or args.ring_degree > 1):
+        p.error("--window_parallel and --ulysses_degree/--ring_degree > 1 are alternative multi-GPU layouts")
+    return args
+
+
+def prompt_text(prompts):
+    """--validation_prompts uses nargs='+'.  The reference passes the list on as a batch of prompts
+    (inference.py:544-546 -> pipeline:608-611), but its context list then holds 3k entries against a CFG batch of 3
+    latents, which only works for k = 1 (one quoted prompt).  Several words given unquoted are joined into that
+    one prompt here, with a warning."""
+    if isinstance(prompts, str):
+        return prompts
+    prompts = list(prompts)
+    if len(prompts) > 1:
+        import warnings
+        warnings.warn(f"--validation_prompts got {len(prompts)} arguments; they are joined into one prompt (the "
+                      "reference's pipeline takes one prompt per audio clip: quote the prompt)")
+    return " ".join(prompts)
 
 
 def load_config(path):
@@ -215,6 +240,7 @@ def main(argv=None):
             pipeline.enable_window_parallel()
         else:
             transformer3d.enable_multi_gpus_inference()
+        pipeline.enable_vae_parallel(args.vae_parallel)
     if args.enable_teacache:
         coefficients = get_teacache_coefficients(root)
         if coefficients is not None:
@@ -230,8 +256,7 @@ def main(argv=None):
                        vae.config.temporal_compression_ratio) + 1 if clip_n != 1 else 1
     sr = 16000
     vocal_input, _ = load_audio(args.validation_driven_audio_path, sr=sr)
-    prompt = args.validation_prompts
-    prompt = " ".join(prompt) if isinstance(prompt, (list, tuple)) else prompt
+    prompt = prompt_text(args.validation_prompts)
     with torch.no_grad():
         sample = pipeline(prompt, num_frames=video_length, negative_prompt=NEGATIVE_PROMPT, height=args.height,
                           width=args.width, guidance_scale=6.0, generator=generator,

@@ -90,28 +90,39 @@ class WanI2VTalkingInferenceLongPipeline:
         import torch.distributed as dist
         self._check_window_parallel(self.transformer)
         self.window_group = group if group is not None else dist.group.WORLD
-        if self.vae is not None and hasattr(self.vae, "enable_multi_gpus_inference"):
-            self.vae.enable_multi_gpus_inference(self.window_group)  # each rank decodes its share of frames
         return self
 
     def disable_window_parallel(self):
         self.window_group = None
-        if self.vae is not None and hasattr(self.vae, "disable_multi_gpus_inference"):
-            self.vae.disable_multi_gpus_inference()
         return self
 
+    def enable_vae_parallel(self, on=True):
+        """Opt-in: decode the clip over the ranks the denoise loop runs on (window parallelism or the
+        transformer's sequence-parallel group) -- a wavefront of causal-cache hand-offs, 1/N of the frames per
+        rank + one gather, bit-identical to the single-GPU decode.  Off by default: every rank decodes the
+        whole clip, as the reference does (:793-796)."""
+        self.vae_parallel = bool(on)
+        return self
+
+    vae_parallel = False
+
     def _decode_group_sync(self):
-        """the VAE decodes over the ranks the transformer runs sequence parallel on (the reference decodes the
-        whole clip on every rank, :793-796): same result, 1/N of the frames per rank + one gather"""
+        """point the VAE's decode group at the ranks of the denoise loop when enable_vae_parallel() is on"""
         t = self.transformer
-        if self.vae is None or self.window_group is not None or not hasattr(self.vae, "decode_group"):
+        if self.vae is None or not hasattr(self.vae, "decode_group"):
             return
-        if getattr(t, "_sp_enabled", False):
-            if self.vae.decode_group is None:
-                import torch.distributed as dist
-                self.vae.enable_multi_gpus_inference(t.sp_group if t.sp_group is not None else dist.group.WORLD)
-        elif self.vae.decode_group is not None:
-            self.vae.disable_multi_gpus_inference()
+        grp = None
+        if self.vae_parallel:
+            import torch.distributed as dist
+            if self.window_group is not None:
+                grp = self.window_group
+            elif getattr(t, "_sp_enabled", False):
+                grp = t.sp_group if t.sp_group is not None else dist.group.WORLD
+        if grp is None:
+            if self.vae.decode_group is not None:
+                self.vae.disable_multi_gpus_inference()
+        elif self.vae.decode_group is not grp:
+            self.vae.enable_multi_gpus_inference(grp)
 
     @staticmethod
     def _check_window_parallel(transformer):
@@ -183,6 +194,8 @@ class WanI2VTalkingInferenceLongPipeline:
         window_features: {(start, end): [3, n_audio, 768]} (zero row first, :737).  Returns the
         final latents_all (bf16)."""
         dev = latents.device
+        if hasattr(self.transformer, "invalidate_context"):
+            self.transformer.invalidate_context()  # text / image K/V are rebuilt once for this call's inputs
         fpb = (clip_length - 1) // 4 + 1
         T = latents.shape[2]
         wins = window_schedule(T, fpb, overlap)

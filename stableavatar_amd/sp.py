@@ -281,14 +281,17 @@ def local_segments(B: int, Lc: int, kv_len: int):
     return [[b * Lc, Lc, b * kv_len, kv_len] for b in range(B)]
 
 
-def vocal_segments(B: int, Lp: int, Lc: int, rank: int, n_frames: int, nper: int):
+def vocal_segments(B: int, S: int, Lc: int, rank: int, n_frames: int, nper: int):
     """Per-frame vocal attention segments for this rank's chunk with single-GPU frame grouping:
-    global token t belongs to frame t // (Lp / n_frames) (1B:575-586 on the unsharded sequence)."""
-    G = Lp // n_frames
+    global token t < S belongs to frame t // (S / n_frames) (1B:575-586 on the unsharded sequence of S
+    tokens); SP pad tokens past S (queries whose outputs are never read) join the last frame's segment."""
+    G = S // n_frames
     t0, t1 = rank * Lc, (rank + 1) * Lc
     segs = []
     for b in range(B):
-        for f in range(t0 // G, (t1 - 1) // G + 1):
-            a, e = max(f * G, t0), min((f + 1) * G, t1)
-            segs.append([b * Lc + a - t0, e - a, (b * n_frames + f) * nper, nper])
+        for f in range(min(t0 // G, n_frames - 1), min((t1 - 1) // G, n_frames - 1) + 1):
+            a = max(f * G, t0)
+            e = min((f + 1) * G, t1) if f < n_frames - 1 else t1
+            if e > a:
+                segs.append([b * Lc + a - t0, e - a, (b * n_frames + f) * nper, nper])
     return segs

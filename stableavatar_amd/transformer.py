@@ -439,11 +439,25 @@ class WanTransformer3DFantasyModel(nn.Module):
 
     # ------------------------------------------------------------------ context (step-invariant)
 
+    def invalidate_context(self):
+        """drop the cached text / image K/V (the pipeline calls this at the start of every denoise)"""
+        self._ctx_cache = None
+
+    @staticmethod
+    def _ctx_key(context, clip_fea):
+        """(tensor, version) of every context input.  The cache holds the tensors themselves and matches
+        by identity, so a hit cannot come from a new tensor the caching allocator placed at a freed
+        address (an address key could return the previous call's prompt / image K/V)."""
+        return tuple((c, c._version) for c in context) + (((clip_fea, clip_fea._version),)
+                                                          if clip_fea is not None else ())
+
     def _context(self, pk, context, clip_fea, B, dev):
-        key = tuple((c.data_ptr(), c._version, tuple(c.shape)) for c in context)
-        key += ((clip_fea.data_ptr(), clip_fea._version, tuple(clip_fea.shape)) if clip_fea is not None else (),)
-        if self._ctx_cache is not None and self._ctx_cache[0] == key:
-            return self._ctx_cache[1]
+        key = self._ctx_key(context, clip_fea)
+        if self._ctx_cache is not None:
+            old = self._ctx_cache[0]
+            if len(old) == len(key) and all(a is c and va == vc for (a, va), (c, vc) in zip(old, key)):
+                return self._ctx_cache[1]
+            self._ctx_cache = None  # release the previous call's tensors and K/V before building new ones
         dim, tl = self.dim, self.text_len
         # text: pad each prompt to text_len with zeros (the pads are attended, 1B:993-999)
         tin = torch.zeros(B, tl, pk.text_kpad, device=dev, dtype=torch.bfloat16)
@@ -579,8 +593,9 @@ class WanTransformer3DFantasyModel(nn.Module):
         real = Fw * hp * wp
         NS, rank = self.sp_world_size, self.sp_world_rank
         SP = self._sp_enabled  # sequence-parallel path (NS ranks; at NS = 1 the exchanges are self-copies)
-        Lp = sp.padded_len(int(seq_len), NS)
-        assert real <= Lp, "seq_len smaller than the token count"
+        S = int(seq_len)  # the single-GPU sequence (1B:983): these keys are attended, SP's extra pads are not
+        Lp = sp.padded_len(S, NS)
+        assert real <= S, "seq_len smaller than the token count"
         Lc = Lp // NS  # tokens of each CFG row held by this rank (all of them without SP)
         ws = self._workspace(B * Lc, dev)
 
@@ -627,9 +642,9 @@ class WanTransformer3DFantasyModel(nn.Module):
             x_in = ws.x.clone() if tc is not None else None
             # vocal context (1B:1004-1009): projector on the last (full-condition) row only
             n_fr = (video_sample_n_frames - 1) // 4 + 1
-            if Lp % n_fr:
+            if S % n_fr:
                 raise ValueError("seq_len must split evenly into latent frames for the per-frame audio attention")
-            lat_row = torch.empty(Lp, dim, device=dev, dtype=torch.bfloat16)
+            lat_row = torch.empty(S, dim, device=dev, dtype=torch.bfloat16)
             if vocal_embeddings.shape[0] == 1 and B != 1:
                 raise ValueError("a single audio row drives a batch of 1 (1B:1008-1009); CFG batches pass 3 rows")
             # 1.3B: the projector runs on the last (full-condition) row only, the unconditional row gets
@@ -638,8 +653,8 @@ class WanTransformer3DFantasyModel(nn.Module):
             voc_rows = []
             for r in range(rows_v):
                 src = B - 1 if rows_v == 1 else r
-                ops.cast_bf16(xfull[src * Lp:(src + 1) * Lp], lat_row)
-                vv, Fn, nper = self._vocal(pk, vocal_embeddings[src], video_sample_n_frames, lat_row, Lp,
+                ops.cast_bf16(xfull[src * Lp:src * Lp + S], lat_row)
+                vv, Fn, nper = self._vocal(pk, vocal_embeddings[src], video_sample_n_frames, lat_row, S,
                                            e0[src:src + 1], e[src:src + 1], dev)
                 if self.vd != dim:
                     raise ValueError("vocal context width must equal the DiT width")
@@ -653,12 +668,15 @@ class WanTransformer3DFantasyModel(nn.Module):
                 vctx = torch.stack(voc_rows)
             vctx = vctx.view(B * Fn * nper, dim)
 
-            G = Lp // n_fr
+            G = S // n_fr
             if SP:
                 plan = sp.make_plan(NS, rank, H_)
                 exch = sp.UlyssesExchange(plan, self.sp_group)
                 Lq, hg = plan.G * Lc, plan.hg
-                segs_self = self._segs.get(("self_sp", B, Lp, Lq), [[b * Lq, Lq, b * Lp, Lp] for b in range(B)], dev)
+                # keys: the S tokens of the single-GPU sequence (the SP pads past S are queries only, their
+                # outputs are never read), so any degree reproduces the single-GPU forward
+                segs_self = self._segs.get(("self_sp", B, Lp, Lq, S), [[b * Lq, Lq, b * Lp, S] for b in range(B)],
+                                           dev)
                 o_sp = torch.empty(B * Lq, hg * self.d, device=dev, dtype=torch.bfloat16)
                 # per-row pipelining only when it adds no attention waves: a row's launch has
                 # ceil(Lq / 256) x hg workgroups; B serial launches must not need more rounds over the CUs
@@ -670,17 +688,17 @@ class WanTransformer3DFantasyModel(nn.Module):
                 if sp_rows:
                     q_sp = torch.empty(B * Lq, hg * self.d, device=dev, dtype=torch.bfloat16)
                     kv_sp = torch.empty(B * Lp, 2 * hg * self.d, device=dev, dtype=torch.bfloat16)
-                    segs_rows = [self._segs.get(("self_sp_row", b, Lp, Lq), [[b * Lq, Lq, b * Lp, Lp]], dev)
+                    segs_rows = [self._segs.get(("self_sp_row", b, Lp, Lq, S), [[b * Lq, Lq, b * Lp, S]], dev)
                                  for b in range(B)]
             else:
                 sp_rows = False
                 segs_self = self._segs.get(("self", B, Lp), [[b * Lp, Lp, b * Lp, Lp] for b in range(B)], dev)
             segs_txt = self._segs.get(("txt", B, Lc, ctx.text_len), sp.local_segments(B, Lc, ctx.text_len), dev)
             segs_img = self._segs.get(("img", B, Lc, ctx.img_len), sp.local_segments(B, Lc, ctx.img_len), dev)
-            voc_list = sp.vocal_segments(B, Lp, Lc, rank, n_fr, nper)
-            segs_voc = self._segs.get(("voc", B, Lp, Lc, rank, n_fr, nper), voc_list, dev)
+            voc_list = sp.vocal_segments(B, S, Lc, rank, n_fr, nper)
+            segs_voc = self._segs.get(("voc", B, S, Lc, rank, n_fr, nper), voc_list, dev)
             voc_n, voc_q = len(voc_list), max(s_[1] for s_ in voc_list)
-            use_cross3 = (ctx.img_len > 0 and G % 256 == 0 and (rank * Lc) % 256 == 0
+            use_cross3 = (ctx.img_len > 0 and G % 256 == 0 and (rank * Lc) % 256 == 0 and (rank + 1) * Lc <= S
                           and os.environ.get("SA_CROSS3", "1") != "0")
             x = ws.x
             kvv = torch.empty(B * n_fr * nper, 2 * dim, device=dev, dtype=torch.bfloat16)  # per-frame vocal K|V

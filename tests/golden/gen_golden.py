@@ -159,7 +159,7 @@ class _Obj(types.SimpleNamespace):
         return [self.last][i]
 
 
-def gen_pipeline(P=PIPE, name="pipeline_small"):
+def gen_pipeline(P=PIPE, name="pipeline_small", scheme="uniform"):
     import time
     from wan.pipeline.wan_inference_long_pipeline import WanI2VTalkingInferenceLongPipeline
     from _refstub import FlowMatchEulerDiscreteScheduler
@@ -198,12 +198,13 @@ def gen_pipeline(P=PIPE, name="pipeline_small"):
                  width=P["width"], guidance_scale=6.0, num_inference_steps=P["steps"], latents=fx["latents"],
                  text_guide_scale=P["text_guide"], audio_guide_scale=P["audio_guide"],
                  vocal_input_values=fx["audio"].numpy(), fps=25, sr=16000, cond_file_path=path,
-                 overlap_window_length=P["overlap"], clip_length=P["clip_length"]).videos
+                 overlap_window_length=P["overlap"], clip_length=P["clip_length"],
+                 overlapping_weight_scheme=scheme).videos
     out = {"video": video.numpy(), "latents": decoded["latents"].numpy(), "y": calls[0]["y"].numpy(),
            "win_F": np.array([c["F"] for c in calls]), "win_t": np.array([c["t"] for c in calls]),
            "win_seq_len": np.array([c["seq_len"] for c in calls]),
            "win_n_audio": np.array([c["n_audio"] for c in calls])}
-    if name != "pipeline_small":  # big video: keep a few decoded frames in fp16
+    if name == "pipeline_c1":  # big video: keep a few decoded frames in fp16
         from golden_cases import PIPE_C1_VIDEO_FRAMES
         out["video"] = out["video"][:, :, list(PIPE_C1_VIDEO_FRAMES)].astype(np.float16)
         out["video_frames"] = np.array(PIPE_C1_VIDEO_FRAMES)
@@ -220,6 +221,13 @@ def gen_pipeline_c1():
     256x256, clip 17, 5 steps, 2 windows per step (golden_cases.PIPE_C1)."""
     from golden_cases import PIPE_C1
     gen_pipeline(PIPE_C1, "pipeline_c1")
+
+
+def gen_pipeline_log():
+    """overlapping_weight_scheme="log" (pipeline:761-766) through the reference's __call__: PIPE with overlap 3
+    (at overlap 2 the log and uniform ramps are both [0, 1]), windows (0,5),(2,6) per step"""
+    from golden_cases import PIPE_LOG
+    gen_pipeline(PIPE_LOG, "pipeline_log", scheme="log")
 
 
 def gen_keys():

@@ -77,6 +77,10 @@ PIPE = dict(dit=dict(DIT_SMALL, num_layers=1, seed=31), vae=dict(dim=32, seed=32
             audio_frames=24)
 
 
+# the "log" overlap blend (pipeline:761-766) needs overlap >= 3 to differ from the uniform ramp
+PIPE_LOG = dict(PIPE, overlap=3)
+
+
 # BASELINE config 1: the full Wan-1.3B StableAvatar DiT (30 layers, dim 1536, ffn 8960,
 # text_dim 4096) and the full-width VAE (dim 96) at 256x256, clip 17 (5 latent frames), 5 sampling steps,
 # overlap 2, 24 video frames of audio -> T_lat 6 -> windows (0,5),(3,6) per step

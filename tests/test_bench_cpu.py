@@ -130,3 +130,37 @@ def test_bench_parse_defaults():
     assert a.gpus == 1 and a.mode == "sp" and a.steps >= 1
     assert bench.parse(["--window-dp"]).mode == "window-dp"
     assert bench.cpu_cores() >= 1 and isinstance(bench.cpu_model(), str)
+
+
+def test_bench_cpu_baseline_child_world1(capsys):
+    """N = 1: the CPU baseline runs in a child process started before the GPU work, is collected after the
+    warmup (never inside the timed region) and lands in the JSON with the thread count it used; the
+    JSON records the time budget."""
+    rc = bench.main(["--steps", "1", "--warmup", "1", "--size", "64", "--frames", "17", "--no-cpu-config1",
+                     "--no-encode"], work_factory=FakeClip, device="cpu")
+    assert rc == 0
+    j = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    c = j["cpu_baseline"]
+    assert c["value"] > 0 and c["kind"] == "port" and c["cores"] >= 1
+    assert "1 of 30 DiT blocks at B=3,L=80" in c["sample"]
+    assert c["config_1"]["value"] is None and c["config_1"]["skipped"] == "not run"
+    assert j["time_budget"]["budget_s"] == 540.0 and j["time_budget"]["elapsed_s"] > 0
+
+
+def test_bench_cpu_baseline_deadline(tmp_path):
+    """A child still running past the deadline is ended once its mandatory config-2 leg is in."""
+    import subprocess
+    import time as _t
+    cb = bench.CpuBaseline.__new__(bench.CpuBaseline)
+    cb.path, cb.log, cb.killed = str(tmp_path / "c.jsonl"), str(tmp_path / "c.log"), False
+    with open(cb.path, "w") as f:
+        f.write(json.dumps({"leg": "config2", "t_block": 1.0, "t_vae_frame": 0.5, "L": 80, "threads": 3}) + "\n")
+        f.write(json.dumps({"leg": "config1_step", "i": 0, "s": 2.0, "dit_forwards": 2}) + "\n")
+    cb.proc = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(60)"])
+    t0 = _t.time()
+    cb.wait(deadline=_t.time(), required_by=_t.time() + 30)
+    assert cb.killed and _t.time() - t0 < 15
+    r = cb.result(n_fwd=50, out_frames=81, size=512)
+    assert r["cores"] == 3 and abs(r["value"] - 81 / (50 * 30 * 1.0 + 81 * 0.5)) < 1e-5
+    assert r["config_1"]["skipped"] == "not finished within the time budget" and r["config_1"]["steps_done"] == 1
+    cb.cleanup()

@@ -232,8 +232,8 @@ def _drop_in_pipeline(P):
 def test_pipeline_call_vs_reference(case):
     """The drop-in __call__ with the reference's arguments (gen_golden.py): prompt -> fake T5, reference
     image -> fake CLIP + HIP VAE encode -> y, audio -> fake wav2vec per window, 2 windows x N steps,
-    HIP VAE decode.  y rel-L2 < 3e-2; latents rel-L2 < 3e-2 (small) / 5e-2 (config 1, 30 layers x 10
-    forwards of bf16 drift); video PSNR > 30 dB (small) / 28 dB (config 1) on [0, 1]."""
+    HIP VAE decode.  The SURVEY.md §8(d) contract for both cases (config 1: 30 layers x 10 forwards of bf16
+    drift; measured 7.9e-3 / 49 dB): y rel-L2 < 3e-2, latents rel-L2 <= 3e-2, video PSNR >= 30 dB on [0, 1]."""
     P, name = (PIPE, "pipeline_small.npz") if case == "small" else (PIPE_C1, "pipeline_c1.npz")
     g = np.load(os.path.join(HERE, "golden", name))
     pipe, fx = _drop_in_pipeline(P)
@@ -255,5 +255,5 @@ def test_pipeline_call_vs_reference(case):
     print(f"pipeline {case}: y rel {ey:.2e}, latents rel {el:.2e}, video PSNR {pv:.1f} dB")
     assert tuple(video.shape) == (1, 3, 1 + 4 * (g["latents"].shape[2] - 1), P["height"], P["width"])
     assert ey < 3e-2, ey
-    assert el < (3e-2 if case == "small" else 5e-2), el
-    assert pv > (30.0 if case == "small" else 28.0), pv
+    assert el <= 3e-2, el
+    assert pv >= 30.0, pv

@@ -1,7 +1,9 @@
 """Window-parallel denoising: the sliding windows of every step spread over
-the ranks, noise predictions all-gathered, blend replicated.  2 ranks sharing one MI355X (gloo,
-host-staged gather) must reproduce the single-GPU loop BIT-EXACTLY, with 3 windows per step (an
-uneven split: rank 1 idles in the second round)."""
+the ranks, noise predictions all-gathered, blend replicated.  Ranks sharing one MI355X (gloo, host-staged
+gather) must reproduce the single-GPU loop BIT-EXACTLY: 2 ranks x 3 windows per step (rank 1 idles in the
+second round) and 3 ranks x 8 windows per step (26 latent frames, uneven last round); the 8-window run is also
+checked against the CPU oracle's restatement of the reference loop (oracle/pipeline.py, pinned to the
+reference's __call__ goldens) at the pipeline tolerance (latents rel-L2 <= 3e-2)."""
 import math
 import os
 import socket
@@ -19,6 +21,8 @@ from mp_util import collect  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
+STEPS = 3
+
 
 def _free_port():
     s = socket.socket()
@@ -28,24 +32,33 @@ def _free_port():
     return port
 
 
-def _run(pipe, T, steps, window_parallel):
-    from stableavatar_amd import synthetic
-    from stableavatar_amd.pipeline import window_schedule
-    from stableavatar_amd.scheduler import FlowMatchEulerDiscreteScheduler
+def _inputs(T):
     from golden_cases import PIPE
-    P = PIPE
-    fpb = (P["clip_length"] - 1) // 4 + 1
+    fpb = (PIPE["clip_length"] - 1) // 4 + 1
     g = torch.Generator().manual_seed(5)
     lat = torch.randn(1, 16, T, 8, 8, generator=g)
     y = torch.randn(3, 20, fpb, 8, 8, generator=g)
     ctx = [torch.randn(12, 64, generator=g), torch.randn(12, 64, generator=g), torch.randn(9, 64, generator=g)]
+    ctx[1] = ctx[0]
     clip = torch.randn(1, 257, 1280, generator=g).expand(3, -1, -1).contiguous()
+    audio = 0.1 * torch.randn((1 + 4 * (T - 1)) * 640 + 320, generator=g)  # 1 + 4 (T - 1) video frames
+    return lat, y, ctx, clip, audio
+
+
+def _run(pipe, T, window_parallel):
+    from stableavatar_amd import synthetic
+    from stableavatar_amd.pipeline import audio_window, window_schedule
+    from stableavatar_amd.scheduler import FlowMatchEulerDiscreteScheduler
+    from golden_cases import PIPE
+    P = PIPE
+    fpb = (P["clip_length"] - 1) // 4 + 1
+    lat, y, ctx, clip, audio = _inputs(T)
     feats = {}
     for (s, e, _) in window_schedule(T, fpb, P["overlap"]):
-        a = synthetic.fake_wav2vec_features(torch.randn(1, 20 * 640, generator=g))
+        a = synthetic.fake_wav2vec_features(audio[audio_window(s, e, T, 640, audio.shape[0])][None])
         feats[(s, e)] = torch.cat([torch.zeros_like(a), a, a]).cuda()
     sched = FlowMatchEulerDiscreteScheduler(1000, shift=5.0)
-    sched.set_timesteps(steps, device="cuda")
+    sched.set_timesteps(STEPS, device="cuda")
     pipe.window_group = None
     if window_parallel:
         pipe.enable_window_parallel()
@@ -58,7 +71,7 @@ def _run(pipe, T, steps, window_parallel):
     return out.cpu()
 
 
-def _worker(rank, world, port, qret):
+def _worker(rank, world, port, T, qret):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -72,26 +85,56 @@ def _worker(rank, world, port, qret):
         dit = WanTransformer3DFantasyModel(**{k: v for k, v in dcfg.items() if k != "seed"})
         dit.load_state_dict(synthetic.fill_state_dict(param_shapes(dcfg), dcfg["seed"]))
         pipe = WanI2VTalkingInferenceLongPipeline(transformer=dit.cuda())
-        single = _run(pipe, 9, 3, False)
-        par = _run(pipe, 9, 3, True)
-        qret.put((rank, bool(torch.equal(single, par)), float((single.float() - par.float()).abs().max())))
+        single = _run(pipe, T, False)
+        par = _run(pipe, T, True)
+        qret.put((rank, bool(torch.equal(single, par)), float((single.float() - par.float()).abs().max()),
+                  par if rank == 0 else None))
     finally:
         dist.destroy_process_group()
 
 
-def test_window_parallel_bit_exact():
+def _oracle_loop(T):
+    """the reference loop (pipeline:703-790) restated on the CPU with the oracle DiT"""
+    from oracle import dit as odit
+    from oracle import pipeline as opipe
+    from stableavatar_amd import synthetic
+    from golden_cases import PIPE
+    P = PIPE
+    Pd = synthetic.fill_state_dict(odit.param_shapes(P["dit"]), P["dit"]["seed"])
+    lat, y, ctx, clip, audio = _inputs(T)
+
+    def dit(x, t, context, seq_len, yy, clip_fea, vocal, n):
+        return odit.forward(Pd, P["dit"], x.to(torch.bfloat16).float(), t, context, seq_len, clip_fea,
+                            yy.to(torch.bfloat16).float(), vocal, n)
+
+    enc = lambda s: synthetic.fake_wav2vec_features(torch.as_tensor(s)[None])  # noqa: E731
+    with torch.no_grad():
+        return opipe.denoise(dit, lat.to(torch.bfloat16).float(), y, ctx, clip, audio, enc,
+                             num_inference_steps=STEPS, clip_length=P["clip_length"], num_frames=P["clip_length"],
+                             height=64, width=64, overlap=P["overlap"], text_guide_scale=3.0, audio_guide_scale=5.0)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world,T", [(2, 9), (3, 26)])
+def test_window_parallel_bit_exact(world, T):
     from stableavatar_amd.pipeline import window_schedule
-    assert len(window_schedule(9, 5, 2)) == 3
-    world = 2
+    n_win = len(window_schedule(T, 5, 2))
+    assert n_win == (3 if T == 9 else 8)
     ctx = mp.get_context("spawn")
     qret = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, qret)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, T, qret)) for r in range(world)]
     for p in procs:
         p.start()
-    res = collect(procs, qret, world)
+    res = collect(procs, qret, world, timeout=540)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    for rank, same, mx in res:
+    for rank, same, mx, _ in res:
         assert same, (rank, mx)
+    if T == 26:
+        par = next(r[3] for r in res if r[0] == 0).float()
+        ref = _oracle_loop(T)
+        e = ((par - ref).norm() / ref.norm()).item()
+        print(f"window-parallel {world} ranks, {n_win} windows/step: vs oracle loop rel-L2 {e:.2e}")
+        assert e <= 3e-2, e

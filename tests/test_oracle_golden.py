@@ -97,11 +97,16 @@ def test_vae_encode_flops():
     assert abs(ovae.flops_encode(81, 512, 512) / 1e12 - 107.2) < 0.1
 
 
-def test_pipeline_vs_reference():
-    g = G("pipeline_small.npz")
-    Pd = synthetic.fill_state_dict(odit.param_shapes(PIPE["dit"]), PIPE["dit"]["seed"])
-    Pv = synthetic.fill_state_dict(ovae.param_shapes(dim=PIPE["vae"]["dim"]), PIPE["vae"]["seed"])
-    fx = pipe_fixed_inputs(PIPE)
+@pytest.mark.parametrize("case", ["uniform", "log"])
+def test_pipeline_vs_reference(case):
+    """the restated loop vs the reference's __call__; "log" = overlapping_weight_scheme="log" (pipeline:761-766)
+    at overlap 3, where its ramp differs from the uniform one"""
+    from golden_cases import PIPE_LOG
+    P = PIPE if case == "uniform" else PIPE_LOG
+    g = G("pipeline_small.npz" if case == "uniform" else "pipeline_log.npz")
+    Pd = synthetic.fill_state_dict(odit.param_shapes(P["dit"]), P["dit"]["seed"])
+    Pv = synthetic.fill_state_dict(ovae.param_shapes(dim=P["vae"]["dim"]), P["vae"]["seed"])
+    fx = pipe_fixed_inputs(P)
     ctx = [fx["neg_embeds"], fx["neg_embeds"], fx["pos_embeds"]]
     clip = torch.cat([fx["clip"]] * 3)
     y = torch.from_numpy(g["y"])
@@ -109,21 +114,33 @@ def test_pipeline_vs_reference():
 
     def dit(x, t, context, seq_len, yy, clip_fea, vocal, n):
         calls.append((x.shape[2], round(float(t[0]), 2), vocal.shape[1], seq_len))
-        return odit.forward(Pd, PIPE["dit"], x, t, context, seq_len, clip_fea, yy, vocal, n)
+        return odit.forward(Pd, P["dit"], x, t, context, seq_len, clip_fea, yy, vocal, n)
 
     enc = lambda s: synthetic.fake_wav2vec_features(torch.as_tensor(s)[None])  # noqa: E731
     with torch.no_grad():
-        lat = opipe.denoise(dit, fx["latents"], y, ctx, clip, fx["audio"], enc, num_inference_steps=PIPE["steps"],
-                            clip_length=PIPE["clip_length"], num_frames=PIPE["clip_length"], height=PIPE["height"],
-                            width=PIPE["width"], overlap=PIPE["overlap"], text_guide_scale=PIPE["text_guide"],
-                            audio_guide_scale=PIPE["audio_guide"])
-        video = ovae.decode(Pv, lat, dim=PIPE["vae"]["dim"])
+        lat = opipe.denoise(dit, fx["latents"], y, ctx, clip, fx["audio"], enc, num_inference_steps=P["steps"],
+                            clip_length=P["clip_length"], num_frames=P["clip_length"], height=P["height"],
+                            width=P["width"], overlap=P["overlap"], text_guide_scale=P["text_guide"],
+                            audio_guide_scale=P["audio_guide"], scheme=case)
+        video = ovae.decode(Pv, lat, dim=P["vae"]["dim"])
         video = (video / 2 + 0.5).clamp(0, 1)
     assert [c[0] for c in calls] == list(g["win_F"])
     assert [c[2] for c in calls] == list(g["win_n_audio"])
     assert np.allclose([c[1] for c in calls], g["win_t"], atol=1e-2)
     assert rel(lat, g["latents"]) < 1e-3
     assert rel(video, g["video"]) < 1e-3
+
+
+def test_log_overlap_weights_vs_reference_formula():
+    """pipeline.overlap_weights("log") == the reference's normalised log1p ramp (pipeline:761-766), and differs
+    from the uniform ramp at overlap >= 3"""
+    from stableavatar_amd.pipeline import overlap_weights
+    for n in (2, 3, 5, 15):
+        w = torch.linspace(0, 1, n)
+        w = torch.log1p(w * (torch.exp(torch.tensor(1.0)) - 1))
+        ref = (w - w.min()) / (w.max() - w.min())
+        assert torch.equal(overlap_weights(n, "log"), ref)
+    assert not torch.allclose(overlap_weights(3, "log"), overlap_weights(3, "uniform"))
 
 
 def test_teacache_state_machine_matches_reference_pattern():

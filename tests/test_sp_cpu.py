@@ -115,6 +115,27 @@ def test_vocal_segments_use_global_frames(world):
         assert k0 == (b * n_fr + gt // G) * nper and kl == nper
 
 
+@pytest.mark.parametrize("world,S,n_fr", [(8, 84, 21), (3, 80, 5), (8, 80, 5), (16, 84, 21)])
+def test_vocal_segments_with_sp_pads(world, S, n_fr):
+    """S not a multiple of the degree: the tokens < S keep the single-GPU frame t // (S / F); the pad tokens
+    past S (Lp - S of them, queries only) join the last frame; every local row is covered exactly once."""
+    B, nper = 3, 17
+    G = S // n_fr
+    Lp = sp.padded_len(S, world)
+    Lc = Lp // world
+    seen = {}
+    for r in range(world):
+        for q0, ql, k0, kl in sp.vocal_segments(B, S, Lc, r, n_fr, nper):
+            assert ql > 0 and kl == nper
+            b = q0 // Lc
+            for t in range(q0 - b * Lc, q0 - b * Lc + ql):
+                assert (b, r * Lc + t) not in seen
+                seen[(b, r * Lc + t)] = k0
+    assert len(seen) == B * Lp
+    for (b, gt), k0 in seen.items():
+        assert k0 == (b * n_fr + min(gt // G, n_fr - 1)) * nper
+
+
 def _slots_worker(rank, world, port, q_ret):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
