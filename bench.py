@@ -241,8 +241,13 @@ class CpuBaseline:
     def wait(self, deadline, required_by):
         """wait for the child to end; past `deadline` (time.time()) end it, but never before the config-2 leg
         is in (bounded by `required_by`)"""
+        last = 0.0
         while self.proc.poll() is None:
             now = time.time()
+            if now - last > 30:
+                legs = [r["leg"] for r in self.records()]
+                progress(f"waiting for the CPU baseline child ({len(legs)} records: {legs[-1] if legs else '-'})")
+                last = now
             if now > deadline and (self._has("config2") or now > required_by):
                 self.proc.terminate()
                 try:
@@ -398,6 +403,12 @@ class ClipWorkload:
         return self.args.sample_steps * len(self.wins)
 
 
+def progress(msg):
+    """one line on stderr (stdout carries only the JSON line): keeps a long run visibly alive"""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench {time.time() - T0:6.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def sync(dev):
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
@@ -416,9 +427,10 @@ def timed(work, steps, warmup, world, dev, events=False, before_timed=None):
     before_timed(warmup_seconds) runs after the warmup, before the opening barrier."""
     with torch.no_grad():
         tw = time.perf_counter()
-        for _ in range(warmup):
+        for i in range(warmup):
             work.step()
-        sync(dev)
+            sync(dev)
+            progress(f"warmup {i + 1}/{warmup} {time.perf_counter() - tw:.1f}s")
         tw = time.perf_counter() - tw
         if before_timed is not None:
             before_timed(tw)
@@ -427,10 +439,13 @@ def timed(work, steps, warmup, world, dev, events=False, before_timed=None):
             work.start_events()
         t0 = time.perf_counter()
         out = None
-        for _ in range(steps):
+        for i in range(steps):
             out = work.step()
+            if steps > 1 and i + 1 < steps:  # no sync: the clips stay queued back to back
+                progress(f"timed {i + 1}/{steps} queued {time.perf_counter() - t0:.1f}s")
         barrier(world, dev)
         dt = time.perf_counter() - t0
+        progress(f"timed {steps} steps {dt:.1f}s")
     if world > 1:
         import torch.distributed as dist
         tt = torch.tensor([dt], dtype=torch.float64, device=dev if dev.type == "cuda" else "cpu")

@@ -678,20 +678,27 @@ class WanTransformer3DFantasyModel(nn.Module):
                 segs_self = self._segs.get(("self_sp", B, Lp, Lq, S), [[b * Lq, Lq, b * Lp, S] for b in range(B)],
                                            dev)
                 o_sp = torch.empty(B * Lq, hg * self.d, device=dev, dtype=torch.bfloat16)
-                # per-row pipelining only when it adds no attention waves: a row's launch has
-                # ceil(Lq / 256) x hg workgroups; B serial launches must not need more rounds over the CUs
-                # than the batched one (N = 8: 63 workgroups per row would leave most CUs idle)
+                # exchange schedule (SA_SP_OVERLAP: 0 one synchronous batched exchange per direction; 2 per-row
+                # exchanges and per-row attention; 3 per-row Q/K/V exchanges, batched attention; 1 = auto:
+                # 2 when per-row attention launches add no waves over the CUs -- a row's launch has ceil(Lq /
+                # 256) x hg workgroups and B serial launches must not need more rounds than the batched one --
+                # else 3 (N = 8: 63 workgroups per row would leave most CUs idle, but the Q/K/V exchange of
+                # row b can still travel under the QKV GEMMs of rows b+1..; per-row GEMMs there take as many
+                # rounds over the CUs as the batched one)
                 n_cu = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 256
                 wg_row = -(-Lq // 256) * hg
-                ov = os.environ.get("SA_SP_OVERLAP", "1")  # 0 off, 1 when it adds no waves, 2 always
-                sp_rows = ov == "2" or (ov == "1" and B * -(-wg_row // n_cu) <= -(-(B * wg_row) // n_cu))
-                if sp_rows:
+                ov = os.environ.get("SA_SP_OVERLAP", "1")
+                if ov == "1":
+                    ov = "2" if B * -(-wg_row // n_cu) <= -(-(B * wg_row) // n_cu) else "3"
+                sp_rows, sp_rows_x = ov == "2", ov == "3" and B > 1
+                if sp_rows or sp_rows_x:
                     q_sp = torch.empty(B * Lq, hg * self.d, device=dev, dtype=torch.bfloat16)
                     kv_sp = torch.empty(B * Lp, 2 * hg * self.d, device=dev, dtype=torch.bfloat16)
+                if sp_rows:
                     segs_rows = [self._segs.get(("self_sp_row", b, Lp, Lq, S), [[b * Lq, Lq, b * Lp, S]], dev)
                                  for b in range(B)]
             else:
-                sp_rows = False
+                sp_rows = sp_rows_x = False
                 segs_self = self._segs.get(("self", B, Lp), [[b * Lp, Lp, b * Lp, Lp] for b in range(B)], dev)
             segs_txt = self._segs.get(("txt", B, Lc, ctx.text_len), sp.local_segments(B, Lc, ctx.text_len), dev)
             segs_img = self._segs.get(("img", B, Lc, ctx.img_len), sp.local_segments(B, Lc, ctx.img_len), dev)
@@ -734,10 +741,23 @@ class WanTransformer3DFantasyModel(nn.Module):
                         ops.linear(ws.att[rs], L.w_o, L.b_o, ops.EPI_RES_F32, out=x[rs], residual=x[rs],
                                    gate=em[b:b + 1, 2], rows_per_batch=Lc)
                 else:
-                    ops.linear(ws.mod, L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv)
-                    ops.qk_rmsnorm_rope(ws.qkv, 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
+                    if sp_rows_x:
+                        # per-row Q/K/V exchanges issued as each row's QKV GEMM + norm/RoPE lands (they travel
+                        # under the later rows' GEMMs), one batched attention once all have arrived
+                        pend = []
+                        for b in range(B):
+                            rs = slice(b * Lc, (b + 1) * Lc)
+                            ops.linear(ws.mod[rs], L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv[rs])
+                            ops.qk_rmsnorm_rope(ws.qkv[rs], 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
+                            pend.append(exch.to_heads_row(ws.qkv, b, B, Lc, self.d, q_sp, kv_sp))
+                        for p_ in pend:
+                            p_.wait()
+                    else:
+                        ops.linear(ws.mod, L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv)
+                        ops.qk_rmsnorm_rope(ws.qkv, 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
                     if SP:  # Ulysses: tokens -> heads, full-sequence attention, heads -> tokens
-                        q_sp, kv_sp = exch.to_heads(ws.qkv, B, Lc, self.d)
+                        if not sp_rows_x:
+                            q_sp, kv_sp = exch.to_heads(ws.qkv, B, Lc, self.d)
                         args_ = (q_sp, kv_sp[:, :hg * self.d], kv_sp[:, hg * self.d:], o_sp, segs_self, B, Lq, hg)
                     else:
                         args_ = (ws.qkv[:, :dim], ws.qkv[:, dim:2 * dim], ws.qkv[:, 2 * dim:], ws.att, segs_self, B, Lp,
