@@ -12,7 +12,7 @@ def main(path, top=40):
         for r in csv.DictReader(f):
             name = r.get("Kernel_Name", r.get("KernelName", ""))
             name = name.replace("(anonymous namespace)::", "")[:70]
-            grid = r.get("Grid_Size", r.get("Grid_Size_X", ""))
+            grid = r.get("Grid_Size") or "x".join(r.get(k, "") for k in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z"))
             wg = r.get("Workgroup_Size", r.get("Workgroup_Size_X", ""))
             lds = r.get("LDS_Block_Size", r.get("Lds_Size", ""))
             d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
