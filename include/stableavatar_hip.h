@@ -38,8 +38,7 @@ int sa_gemm_bf16(const void* A, int64_t lda, int64_t strideA, const void* W, int
 
 /* sa_gemm_bf16 with the kernel chosen per call (re-entrant A/B; no process-wide state):
  * kernel 0 = auto (the persistent one-wave-per-SIMD kernel where K % 128 == 0, else the 8-wave
- * ping-pong), 1 = ping-pong, 2 = persistent (rejected with 1 when K % 128 != 0), 3 = persistent without the
- * gated-residual epilogue's residual prefetch (A/B; same output);
+ * ping-pong), 1 = ping-pong, 2 = persistent (rejected with 1 when K % 128 != 0);
  * group_m = tile-raster run length (0 = per-kernel default, or env SA_GEMM_GROUP_M read once). */
 int sa_gemm_bf16_ex(const void* A, int64_t lda, int64_t strideA, const void* W, int64_t ldw, int64_t strideW,
                     const float* bias, void* C, int64_t ldc, int64_t strideC, int M, int N, int K, int batch,

@@ -421,12 +421,6 @@ struct S5Ctx {
   int aoff[8], woff[8];
   uint32_t lds_dma;          // wave-uniform LDS address of piece 0 (stage 0)
   uint32_t ard[2][2], wrd[2][2];  // [stage][k half] per-lane fragment read bases
-  // gated-residual kernels: the current tile's residual rows are pulled toward the GPU's caches during its K loop
-  // (RES_PF pieces of one 1-KB row segment per K-step pair, into a scratch LDS slot nothing reads), so the
-  // epilogue's residual loads do not all start from HBM at once
-  __amdgpu_buffer_rsrc_t rr;
-  int pf_row, pf_end, pf_stride;  // wave-uniform: next / end row of this wave's share, row stride in bytes
-  uint32_t pf_lds;
 };
 
 template <int STAGE, int PIECE>
@@ -652,31 +646,18 @@ __device__ __forceinline__ void s7_tile(const GemmArgs& g, int u, int total, int
 // seams, epilogue from a private strip above the ring) on the spread-DMA feed of variant 14: in the
 // last two K steps of a tile the DMA fetches K-tiles 0 and 1 of the next tile and the last step's
 // fragment reads take its first fragments, so a tile starts with no prologue.
-template <int PF>
-__device__ __forceinline__ void s8_prefetch(S5Ctx& c, int lane) {
-#pragma unroll
-  for (int i = 0; i < PF; ++i)
-    if (c.pf_row < c.pf_end) {  // wave-uniform
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rr, LDS_PTR((uintptr_t)c.pf_lds), 16, lane * 16, c.pf_row * c.pf_stride,
-                                               0, 0);
-      ++c.pf_row;
-    }
-}
-
-template <int S, int PF>
-__device__ __forceinline__ void s8_step(S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8], u32x4 (&b0)[8],
-                                        u32x4 (&a1)[8], u32x4 (&b1)[8], int ks, int lane) {
+template <int S>
+__device__ __forceinline__ void s8_step(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8], u32x4 (&b0)[8],
+                                        u32x4 (&a1)[8], u32x4 (&b1)[8], int ks) {
   s4_wait_frags(a0, b0);
   s5_half<S, 1, false, 0>(c, acc, a0, b0, a1, b1, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   s4_wait_frags(a1, b1);
   __builtin_amdgcn_s_barrier();
-  // residual prefetch right after the wait: a whole K-step pair before the next vmcnt(0) waits for it
-  if constexpr (PF > 0) s8_prefetch<PF>(c, lane);
   s5_half<S ^ 1, 0, true, S, true>(c, acc, a1, b1, a0, b0, ks);
 }
 
-template <int EPI, int PF>
+template <int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -741,27 +722,18 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
     int nm0 = m0, nn0 = n0;
     long nbz = bz;
     if (has_next) s7_tile(g, un, total, G, nm, nn, nm0, nn0, nbz, nra, nrw);
-    if constexpr (PF > 0) {  // this tile's residual rows, 64 per wave
-      const int rows = min(BM, g.M - m0);
-      c.rr = __builtin_amdgcn_make_buffer_rsrc((void*)(g.R + bz * g.sR + (long)m0 * g.ldr + n0), (short)0,
-                                               (int)(rows * g.ldr * 4), 0x00020000);
-      c.pf_row = wave * 64;
-      c.pf_end = wave * 64 + 64;
-      c.pf_stride = (int)g.ldr * 4;
-      c.pf_lds = __builtin_amdgcn_readfirstlane(lds0 + S7_LDS);
-    }
     for (int t = 0; t < nk; t += 2) {
       {
         const bool nx = t + 2 >= nk;  // DMA of the next tile's K-tile t+2-nk (or a re-read of the last)
         c.ra = nx ? nra : cra;
         c.rw = nx ? nrw : crw;
-        s8_step<0, PF>(c, acc, a0, b0, a1, b1, (nx ? (has_next ? t + 2 - nk : nk - 1) : t + 2) * 128, lane);
+        s8_step<0>(c, acc, a0, b0, a1, b1, (nx ? (has_next ? t + 2 - nk : nk - 1) : t + 2) * 128);
       }
       {
         const bool nx = t + 3 >= nk;
         c.ra = nx ? nra : cra;
         c.rw = nx ? nrw : crw;
-        s8_step<1, PF>(c, acc, a0, b0, a1, b1, (nx ? (has_next ? t + 3 - nk : nk - 1) : t + 3) * 128, lane);
+        s8_step<1>(c, acc, a0, b0, a1, b1, (nx ? (has_next ? t + 3 - nk : nk - 1) : t + 3) * 128);
       }
     }
     asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // MFMA -> v_accvgpr_read
@@ -781,8 +753,7 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 
-constexpr int KERNEL_AUTO = 0, KERNEL_PINGPONG = 1, KERNEL_PERSISTENT = 2, KERNEL_PERSISTENT_NOPF = 3;
-constexpr int S8_LDS_PF = S7_LDS + 1024;  // + the residual-prefetch scratch slot
+constexpr int KERNEL_AUTO = 0, KERNEL_PINGPONG = 1, KERNEL_PERSISTENT = 2;
 
 int num_cus() {
   // per device: the persistent grid is one workgroup per CU
@@ -809,16 +780,9 @@ int env_group_m() {
 
 template <int EPI>
 int launch(const GemmArgs& g_in, int batch, int kernel, hipStream_t st) {
-  constexpr bool RES = EPI == EPI_RES_F32;
   // one-time per epilogue instantiation: allow the dynamic LDS sizes (idempotent, thread-safe init)
   static const bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, S7_LDS);
-    if (RES) {
-      (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                S8_LDS_PF);
-      (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                S8_LDS_PF);
-    }
+    (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S7_LDS);
     (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
     return true;
@@ -830,27 +794,15 @@ int launch(const GemmArgs& g_in, int batch, int kernel, hipStream_t st) {
   // cross-Q +7-10 %, FFN-up +3-4 %, FFN-down +4 %, O-proj +-1 %), else the ping-pong kernel (e.g. the
   // K = 192 patch embedding)
   const bool persistent_ok = g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL && (long)BN * g.ldw * 2 < 0x7fffffffL;
-  if ((kernel == KERNEL_PERSISTENT || kernel == KERNEL_PERSISTENT_NOPF) && !persistent_ok) return SA_ERR_ARG;
-  const bool persistent = kernel == KERNEL_PERSISTENT || kernel == KERNEL_PERSISTENT_NOPF ||
-                          (kernel == KERNEL_AUTO && persistent_ok);
+  if (kernel == KERNEL_PERSISTENT && !persistent_ok) return SA_ERR_ARG;
+  const bool persistent = kernel == KERNEL_PERSISTENT || (kernel == KERNEL_AUTO && persistent_ok);
   constexpr bool BF16_OUT = EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16;
   if (g.group_m == 0) g.group_m = persistent ? (BF16_OUT ? 8 : 4) : (g.N >= 4096 ? 8 : 1);
   const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
-  if (persistent) {
-    const dim3 grid(min(nm * nn * batch, num_cus()));
-    // gated residual: the residual prefetch, 64 row segments per wave per tile over nk / 2 K-step pairs
-    // (8 per pair covers them within 8 pairs, K <= 2048; 2 per pair within 32 pairs)
-    const int pf = (RES && kernel != KERNEL_PERSISTENT_NOPF && (long)g.ldr * 4 < 0x7fffffffL / BM)
-                       ? (g.K / 128 <= 16 ? 8 : 2) : 0;
-    if (pf == 8)
-      hipLaunchKernelGGL((gemm_s8_kernel<EPI, RES ? 8 : 0>), grid, dim3(256), S8_LDS_PF, st, g, batch);
-    else if (pf == 2)
-      hipLaunchKernelGGL((gemm_s8_kernel<EPI, RES ? 2 : 0>), grid, dim3(256), S8_LDS_PF, st, g, batch);
-    else
-      hipLaunchKernelGGL((gemm_s8_kernel<EPI, 0>), grid, dim3(256), S7_LDS, st, g, batch);
-  } else {
+  if (persistent)
+    hipLaunchKernelGGL(gemm_s8_kernel<EPI>, dim3(min(nm * nn * batch, num_cus())), dim3(256), S7_LDS, st, g, batch);
+  else
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, true>), dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
-  }
   SA_LAUNCH_CHECK();
   return SA_OK;
 }
@@ -866,7 +818,7 @@ extern "C" int sa_gemm_bf16_ex(const void* A, int64_t lda, int64_t strideA, cons
   if (K % BK != 0 || lda % 8 != 0 || ldw % 8 != 0) return SA_ERR_ARG;
   if ((((uintptr_t)A) & 15) || (((uintptr_t)W) & 15)) return SA_ERR_ARG;
   if (epilogue == EPI_RES_F32 && (!residual || (gate && rows_per_batch <= 0))) return SA_ERR_ARG;
-  if (kernel < KERNEL_AUTO || kernel > KERNEL_PERSISTENT_NOPF || group_m < 0) return SA_ERR_ARG;
+  if (kernel < KERNEL_AUTO || kernel > KERNEL_PERSISTENT || group_m < 0) return SA_ERR_ARG;
   GemmArgs g{(const bf16*)A, lda, strideA, (const bf16*)W, ldw, strideW, bias, C, ldc, strideC,
              residual, ldr, strideR, gate, gate_bstride, rows_per_batch > 0 ? rows_per_batch : 1, M, N, K,
              group_m > 0 ? group_m : env_group_m()};
