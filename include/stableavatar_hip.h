@@ -45,6 +45,17 @@ int sa_gemm_bf16_ex(const void* A, int64_t lda, int64_t strideA, const void* W, 
                     int epilogue, const float* residual, int64_t ldr, int64_t strideR, const float* gate,
                     int64_t gate_bstride, int rows_per_batch, int kernel, int group_m, void* stream);
 
+/* sa_gemm_bf16_ex with A in column panels: A[m, k] = A[(k / a_panel_cols) * a_panel_stride + m * lda +
+ * k % a_panel_cols] (a_panel_cols % 64 == 0, batch 1, persistent kernel, EPI_RES_F32).  Reads the
+ * sequence-parallel head exchange's receive buffer (one panel per head group) as the O-projection input
+ * in place, replacing the all-gather of head outputs into token rows around wan/dist/wan_xfuser.py:72-115
+ * (1B:1150-1151 after the USP attention).  a_panel_cols == 0 is sa_gemm_bf16_ex. */
+int sa_gemm_bf16_panels(const void* A, int64_t lda, int64_t strideA, const void* W, int64_t ldw, int64_t strideW,
+                        const float* bias, void* C, int64_t ldc, int64_t strideC, int M, int N, int K, int batch,
+                        int epilogue, const float* residual, int64_t ldr, int64_t strideR, const float* gate,
+                        int64_t gate_bstride, int rows_per_batch, int kernel, int group_m, int64_t a_panel_cols,
+                        int64_t a_panel_stride, void* stream);
+
 /* attention(q,k,v,...) of wan/models/wan_fantasy_transformer3d_1B.py:158-207 (SDPA path, no mask,
  * q_lens/k_lens ignored) for head_dim 128.  Rows of q/k/v/o are flat [rows, stride] bf16 matrices,
  * head h at column h*head_dim.  segs = device int32 [nseg][4] = {q_row0, q_len, kv_row0, kv_len}:
@@ -60,6 +71,14 @@ int sa_attn_fwd(const void* q, const void* k, const void* v, void* o, const int3
 int sa_attn_fwd_ex(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
                    int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride, int64_t v_stride,
                    int64_t o_stride, float scale, int accumulate, int kernel, void* stream);
+
+/* sa_attn_fwd_ex with an output row map: query row r is written to row o_rows[r] of o (device int32 per
+ * query row; NULL = r).  The Ulysses path of usp_attn_forward (wan/dist/wan_xfuser.py:72-115) writes its
+ * own token chunk's head outputs straight into the O-projection's input panel and the other chunks into
+ * their send slabs. */
+int sa_attn_fwd_map(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
+                    int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride, int64_t v_stride,
+                    int64_t o_stride, float scale, int accumulate, int kernel, const int32_t* o_rows, void* stream);
 
 /* The three attentions of WanI2VTalkingCrossAttention.forward (1B:556-603) in one launch: per batch
  * row b, queries q[b*q_len + i] attend to text k/v rows [b*t_len, +t_len), image rows [b*i_len, +i_len)
@@ -94,6 +113,16 @@ int sa_layernorm_mod(const void* x, int64_t ldx, int in_dtype, void* out, int64_
 int sa_qk_rmsnorm_rope(void* x, int64_t ldx, int q_col, int k_col, const float* wq, const float* wk, int M, int C,
                        int head_dim, float eps, const float* rope, int rows_per_batch, int tok_offset, int F, int H,
                        int W, int n_frame_pairs, int n_height_pairs, void* stream);
+
+/* Sequence-parallel Q/K/V pack (usp_attn_forward's all-to-all input, wan/dist/wan_xfuser.py:72-115): the
+ * same RMSNorm + RoPE as sa_qk_rmsnorm_rope on the [M, 3C] QKV rows of this rank's token chunk (q at
+ * column 0, k at C, v at 2C), written with v into per-destination slabs instead of in place.  Head group g
+ * (C/G columns) of row (CFG row b = b_offset + row / rows_per_batch, token t = row % rows_per_batch) goes
+ * as q to destination my_part*G + g and as k|v to destinations r*G + g, r < R; table = device int64
+ * [G*R][6] {q_ptr, q_ld, q_bstride, kv_ptr, kv_ld, kv_bstride} in elements (v at k + C/G). */
+int sa_qkv_pack(const void* x, int64_t ldx, const float* wq, const float* wk, int M, int C, int head_dim, float eps,
+                const float* rope, int rows_per_batch, int tok_offset, int F, int H, int W, int n_frame_pairs,
+                int n_height_pairs, const int64_t* table, int G, int R, int my_part, int b_offset, void* stream);
 
 /* cat(x, y, dim=channels) -> Conv3d(k=s=(1,2,2)) im2col (1B:972-976); out = bf16 [B, Lpad, Kpad]. */
 int sa_patch_im2col(const void* x, int64_t xb, int64_t xc, int64_t xf, int xcn, const void* y, int64_t yb, int64_t yc,

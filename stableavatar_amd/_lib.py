@@ -17,10 +17,13 @@ HEADER = PKG.parent / "include" / "stableavatar_hip.h"
 SIGNATURES = {
     "sa_gemm_bf16": "pllpllpplliiiiipllplip",
     "sa_gemm_bf16_ex": "pllpllpplliiiiipllpliiip",
+    "sa_gemm_bf16_panels": "pllpllpplliiiiipllpliiillp",
     "sa_attn_fwd": "pppppiiiillllfip",
     "sa_attn_fwd_ex": "pppppiiiillllfiip",
+    "sa_attn_fwd_map": "pppppiiiillllfiipp",
     "sa_layernorm_mod": "pliplipppplpiiifp",
     "sa_qk_rmsnorm_rope": "pliippiiifpiiiiiiip",
+    "sa_qkv_pack": "plppiiifpiiiiiiipiiiip",
     "sa_patch_im2col": "plllipllliiiiipiip",
     "sa_unpatchify": "pliiiiiipip",
     "sa_timestep_embed": "piipp",

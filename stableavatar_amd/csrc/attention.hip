@@ -30,6 +30,7 @@ struct AttnArgs {
   long qs, ks, vs, os;
   float c;  // softmax scale * log2(e)
   int accumulate;
+  const int* orows;  // output row of query row r = orows[r] (null: r); the Ulysses exchange's receive layout
 };
 
 constexpr int D = 128;
@@ -524,7 +525,10 @@ __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
     if (!a.accumulate)
       for (int i = tid; i < QBW * (D / 8); i += NW * 64) {
         const int qi = qb * QBW + i / (D / 8);
-        if (qi < q_len) *(u32x4*)(a.o + (long)(q_row0 + qi) * a.os + h * D + (i % (D / 8)) * 8) = (u32x4){0u, 0u, 0u, 0u};
+        if (qi < q_len) {
+          const int orow = a.orows ? a.orows[q_row0 + qi] : q_row0 + qi;
+          *(u32x4*)(a.o + (long)orow * a.os + h * D + (i % (D / 8)) * 8) = (u32x4){0u, 0u, 0u, 0u};
+        }
       }
     return;
   }
@@ -623,7 +627,9 @@ __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
   for (int qt = 0; qt < 2; ++qt) {
     const float inv = 1.0f / st.L[qt][0];
     const int qi = qb * QBW + wave * 32 + qt * 16 + r16;
-    bf16* op = a.o + (long)(q_row0 + min(qi, q_len - 1)) * a.os + h * D + 4 * (g & ~1) + 16 * (g & 1);
+    const int qrow = q_row0 + min(qi, q_len - 1);
+    const int orow = a.orows ? a.orows[qrow] : qrow;
+    bf16* op = a.o + (long)orow * a.os + h * D + 4 * (g & ~1) + 16 * (g & 1);
 #pragma unroll
     for (int dt = 0; dt < 8; dt += 2) {
       const f32x4& A = st.O[dt][qt];
@@ -810,10 +816,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_v6_w4_kernel(AttnArgs a) { at
 // workgroup per CU: a 4-wave round holds two workgroups per CU and runs 3 % slower per FLOP; a last 4-wave
 // round of at most one workgroup per CU (one wave per SIMD) takes 0.75 of a round (measured,
 // profiles/r02/attn_sp_shapes.json: the Ulysses N = 8 shape, 378 / 756 workgroups, 1.036 vs 0.927 ms).
-extern "C" int sa_attn_fwd_ex(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
-                              int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride,
-                              int64_t v_stride, int64_t o_stride, float scale, int accumulate, int kernel,
-                              void* stream) {
+// o_rows (optional, device int32 indexed by query row): query row r's output goes to row o_rows[r] of o --
+// the sequence-parallel path writes this rank's own token chunk straight into the O-projection's input
+// panels and the other chunks into their send slabs (stableavatar_amd/sp.py)
+extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
+                               int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride,
+                               int64_t v_stride, int64_t o_stride, float scale, int accumulate, int kernel,
+                               const int32_t* o_rows, void* stream) {
   if (!q || !k || !v || !o || !segs || nseg <= 0 || max_q_len <= 0 || heads <= 0) return SA_ERR_ARG;
   if (head_dim != D) return SA_ERR_ARG;
   if ((q_stride | k_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
@@ -827,7 +836,7 @@ extern "C" int sa_attn_fwd_ex(const void* q, const void* k, const void* v, void*
   }();
   (void)attr;
   AttnArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, segs,
-             q_stride, k_stride, v_stride, o_stride, scale * 1.4426950408889634f, accumulate};
+             q_stride, k_stride, v_stride, o_stride, scale * 1.4426950408889634f, accumulate, o_rows};
   if (kernel == 0) {
     static int cus[64] = {0};  // per device, queried once
     int dev = 0, ncu = 256;
@@ -850,6 +859,14 @@ extern "C" int sa_attn_fwd_ex(const void* q, const void* k, const void* v, void*
   }
   SA_LAUNCH_CHECK();
   return SA_OK;
+}
+
+extern "C" int sa_attn_fwd_ex(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
+                              int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride,
+                              int64_t v_stride, int64_t o_stride, float scale, int accumulate, int kernel,
+                              void* stream) {
+  return sa_attn_fwd_map(q, k, v, o, segs, nseg, max_q_len, heads, head_dim, q_stride, k_stride, v_stride, o_stride,
+                         scale, accumulate, kernel, nullptr, stream);
 }
 
 extern "C" int sa_attn_fwd(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,

@@ -30,6 +30,10 @@ struct GemmArgs {
   int rows_per_batch;
   int M, N, K;
   int group_m;  // tile raster: runs of group_m tile rows, column-major inside a run (L2 reuse per XCD)
+  // A in column panels (persistent kernel only): K-tile T (64 columns) lives in panel (T * a_pmul) >> 20,
+  // each panel a_pdelta bytes further than contiguous columns would be (a_pmul 0: one plain matrix);
+  // a_pextra = the bytes past a tile's rows the buffer range must also cover
+  unsigned a_pmul; int a_pdelta; int a_pextra;
 };
 
 // flat tile id -> (tile row, tile col): consecutive ids walk down a column of group_m tile rows, then
@@ -424,11 +428,11 @@ struct S5Ctx {
 };
 
 template <int STAGE, int PIECE>
-__device__ __forceinline__ void s5_dma(const S5Ctx& c, int ks) {
+__device__ __forceinline__ void s5_dma(const S5Ctx& c, int ks, int ksa) {
   constexpr int i = PIECE & 7;
   if constexpr (PIECE < 8)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(c.ra, LDS_PTR((uintptr_t)(c.lds_dma + STAGE * S5_STAGE + i * 4096)), 16,
-                                             c.aoff[i], ks, 0, 0);
+                                             c.aoff[i], ksa, 0, 0);
   else
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
         c.rw, LDS_PTR((uintptr_t)(c.lds_dma + STAGE * S5_STAGE + 256 * 128 + i * 4096)), 16, c.woff[i], ks, 0, 0);
@@ -446,33 +450,33 @@ __device__ __forceinline__ void s5_read(const S5Ctx& c, u32x4 (&a)[8], u32x4 (&b
 // next fragments (stage RS, k half RK) and, when DMA, 4 DMA pieces each of tile ks into stage DS
 // DMA piece placement inside a half: packed (4 per MFMA row in rows 0-3) or SPREAD (2 per row, all 8)
 template <int DS, int Q, int POS, bool DMA, bool SPREAD>
-__device__ __forceinline__ void s5_dma_at(const S5Ctx& c, int ks) {
+__device__ __forceinline__ void s5_dma_at(const S5Ctx& c, int ks, int ksa) {
   if constexpr (DMA) {
     if constexpr (SPREAD) {
-      if constexpr (POS & 1) s5_dma<DS, 2 * Q + (POS >> 1)>(c, ks);
+      if constexpr (POS & 1) s5_dma<DS, 2 * Q + (POS >> 1)>(c, ks, ksa);
     } else if constexpr (Q < 4) {
-      s5_dma<DS, 4 * Q + POS>(c, ks);
+      s5_dma<DS, 4 * Q + POS>(c, ks, ksa);
     }
   }
 }
 
 template <int RS, int RK, bool DMA, int DS, bool SPREAD = false>
 __device__ __forceinline__ void s5_half(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&ac)[8], u32x4 (&bc)[8],
-                                        u32x4 (&an)[8], u32x4 (&bn)[8], int ks) {
+                                        u32x4 (&an)[8], u32x4 (&bn)[8], int ks, int ksa) {
 #define SA_S5_ROW(Q)                                                                        \
   {                                                                                         \
     s4_mma(acc[Q][0], bc[0], ac[Q]); s4_mma(acc[Q][1], bc[1], ac[Q]);                       \
     if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q>(c, an, bn); }                             \
-    s5_dma_at<DS, Q, 0, DMA, SPREAD>(c, ks);                               \
+    s5_dma_at<DS, Q, 0, DMA, SPREAD>(c, ks, ksa);                               \
     s4_mma(acc[Q][2], bc[2], ac[Q]); s4_mma(acc[Q][3], bc[3], ac[Q]);                       \
     if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 1>(c, an, bn); }                         \
-    s5_dma_at<DS, Q, 1, DMA, SPREAD>(c, ks);                           \
+    s5_dma_at<DS, Q, 1, DMA, SPREAD>(c, ks, ksa);                           \
     s4_mma(acc[Q][4], bc[4], ac[Q]); s4_mma(acc[Q][5], bc[5], ac[Q]);                       \
     if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 2>(c, an, bn); }                         \
-    s5_dma_at<DS, Q, 2, DMA, SPREAD>(c, ks);                           \
+    s5_dma_at<DS, Q, 2, DMA, SPREAD>(c, ks, ksa);                           \
     s4_mma(acc[Q][6], bc[6], ac[Q]); s4_mma(acc[Q][7], bc[7], ac[Q]);                       \
     if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 3>(c, an, bn); }                         \
-    s5_dma_at<DS, Q, 3, DMA, SPREAD>(c, ks);                           \
+    s5_dma_at<DS, Q, 3, DMA, SPREAD>(c, ks, ksa);                           \
   }
   SA_S5_ROW(0) SA_S5_ROW(1) SA_S5_ROW(2) SA_S5_ROW(3) SA_S5_ROW(4) SA_S5_ROW(5) SA_S5_ROW(6) SA_S5_ROW(7)
 #undef SA_S5_ROW
@@ -636,7 +640,7 @@ __device__ __forceinline__ void s7_tile(const GemmArgs& g, int u, int total, int
   n0 = nt * BN;
   const int rows_a = min(BM, g.M - m0), rows_w = min(BN, g.N - n0);
   ra = __builtin_amdgcn_make_buffer_rsrc((void*)(g.A + bz * g.sA + (long)m0 * g.lda), (short)0,
-                                         (int)(rows_a * g.lda * 2), 0x00020000);
+                                         (int)(rows_a * g.lda * 2) + g.a_pextra, 0x00020000);
   rw = __builtin_amdgcn_make_buffer_rsrc((void*)(g.W + bz * g.sW + (long)n0 * g.ldw), (short)0,
                                          (int)(rows_w * g.ldw * 2), 0x00020000);
 }
@@ -646,18 +650,25 @@ __device__ __forceinline__ void s7_tile(const GemmArgs& g, int u, int total, int
 // seams, epilogue from a private strip above the ring) on the spread-DMA feed of variant 14: in the
 // last two K steps of a tile the DMA fetches K-tiles 0 and 1 of the next tile and the last step's
 // fragment reads take its first fragments, so a tile starts with no prologue.
-template <int S>
-__device__ __forceinline__ void s8_step(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8], u32x4 (&b0)[8],
-                                        u32x4 (&a1)[8], u32x4 (&b1)[8], int ks) {
+// A's byte offset of K-tile ks / 128 (column panels: see GemmArgs)
+template <bool PANEL>
+__device__ __forceinline__ int s8_ksa(const GemmArgs& g, int ks) {
+  if constexpr (PANEL) return ks + (int)(((unsigned)(ks >> 7) * g.a_pmul) >> 20) * g.a_pdelta;
+  return ks;
+}
+
+template <int S, bool PANEL>
+__device__ __forceinline__ void s8_step(const GemmArgs& g, const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8],
+                                        u32x4 (&b0)[8], u32x4 (&a1)[8], u32x4 (&b1)[8], int ks) {
   s4_wait_frags(a0, b0);
-  s5_half<S, 1, false, 0>(c, acc, a0, b0, a1, b1, 0);
+  s5_half<S, 1, false, 0>(c, acc, a0, b0, a1, b1, 0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   s4_wait_frags(a1, b1);
   __builtin_amdgcn_s_barrier();
-  s5_half<S ^ 1, 0, true, S, true>(c, acc, a1, b1, a0, b0, ks);
+  s5_half<S ^ 1, 0, true, S, true>(c, acc, a1, b1, a0, b0, ks, s8_ksa<PANEL>(g, ks));
 }
 
-template <int EPI>
+template <int EPI, bool PANEL = false>
 __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -699,11 +710,13 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
   u32x4 a0[8], b0[8], a1[8], b1[8];
 #define SA_S8_DMA_ALL(STAGE, T)                                                                       \
   {                                                                                                   \
-    const int ks = (T) * 128;                                                                         \
-    s5_dma<STAGE, 0>(c, ks); s5_dma<STAGE, 1>(c, ks); s5_dma<STAGE, 2>(c, ks); s5_dma<STAGE, 3>(c, ks);     \
-    s5_dma<STAGE, 4>(c, ks); s5_dma<STAGE, 5>(c, ks); s5_dma<STAGE, 6>(c, ks); s5_dma<STAGE, 7>(c, ks);     \
-    s5_dma<STAGE, 8>(c, ks); s5_dma<STAGE, 9>(c, ks); s5_dma<STAGE, 10>(c, ks); s5_dma<STAGE, 11>(c, ks);   \
-    s5_dma<STAGE, 12>(c, ks); s5_dma<STAGE, 13>(c, ks); s5_dma<STAGE, 14>(c, ks); s5_dma<STAGE, 15>(c, ks); \
+    const int ks = (T) * 128, ksa = s8_ksa<PANEL>(g, ks);                                                  \
+    s5_dma<STAGE, 0>(c, ks, ksa); s5_dma<STAGE, 1>(c, ks, ksa); s5_dma<STAGE, 2>(c, ks, ksa);             \
+    s5_dma<STAGE, 3>(c, ks, ksa); s5_dma<STAGE, 4>(c, ks, ksa); s5_dma<STAGE, 5>(c, ks, ksa);             \
+    s5_dma<STAGE, 6>(c, ks, ksa); s5_dma<STAGE, 7>(c, ks, ksa); s5_dma<STAGE, 8>(c, ks, ksa);             \
+    s5_dma<STAGE, 9>(c, ks, ksa); s5_dma<STAGE, 10>(c, ks, ksa); s5_dma<STAGE, 11>(c, ks, ksa);           \
+    s5_dma<STAGE, 12>(c, ks, ksa); s5_dma<STAGE, 13>(c, ks, ksa); s5_dma<STAGE, 14>(c, ks, ksa);          \
+    s5_dma<STAGE, 15>(c, ks, ksa);                                                                    \
   }
   SA_S8_DMA_ALL(0, 0)
   SA_S8_DMA_ALL(1, 1)
@@ -727,13 +740,13 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
         const bool nx = t + 2 >= nk;  // DMA of the next tile's K-tile t+2-nk (or a re-read of the last)
         c.ra = nx ? nra : cra;
         c.rw = nx ? nrw : crw;
-        s8_step<0>(c, acc, a0, b0, a1, b1, (nx ? (has_next ? t + 2 - nk : nk - 1) : t + 2) * 128);
+        s8_step<0, PANEL>(g, c, acc, a0, b0, a1, b1, (nx ? (has_next ? t + 2 - nk : nk - 1) : t + 2) * 128);
       }
       {
         const bool nx = t + 3 >= nk;
         c.ra = nx ? nra : cra;
         c.rw = nx ? nrw : crw;
-        s8_step<1>(c, acc, a0, b0, a1, b1, (nx ? (has_next ? t + 3 - nk : nk - 1) : t + 3) * 128);
+        s8_step<1, PANEL>(g, c, acc, a0, b0, a1, b1, (nx ? (has_next ? t + 3 - nk : nk - 1) : t + 3) * 128);
       }
     }
     asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // MFMA -> v_accvgpr_read
@@ -783,6 +796,9 @@ int launch(const GemmArgs& g_in, int batch, int kernel, hipStream_t st) {
   // one-time per epilogue instantiation: allow the dynamic LDS sizes (idempotent, thread-safe init)
   static const bool attr = [] {
     (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S7_LDS);
+    if constexpr (EPI == EPI_RES_F32)
+      (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                S7_LDS);
     (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
     return true;
@@ -799,7 +815,13 @@ int launch(const GemmArgs& g_in, int batch, int kernel, hipStream_t st) {
   constexpr bool BF16_OUT = EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16;
   if (g.group_m == 0) g.group_m = persistent ? (BF16_OUT ? 8 : 4) : (g.N >= 4096 ? 8 : 1);
   const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
-  if (persistent)
+  if (g.a_pmul) {  // column-panel A: the O-projection of the sequence-parallel path only
+    if constexpr (EPI == EPI_RES_F32)
+      hipLaunchKernelGGL((gemm_s8_kernel<EPI, true>), dim3(min(nm * nn * batch, num_cus())), dim3(256), S7_LDS, st, g,
+                         batch);
+    else
+      return SA_ERR_ARG;
+  } else if (persistent)
     hipLaunchKernelGGL(gemm_s8_kernel<EPI>, dim3(min(nm * nn * batch, num_cus())), dim3(256), S7_LDS, st, g, batch);
   else
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, true>), dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
@@ -809,11 +831,16 @@ int launch(const GemmArgs& g_in, int batch, int kernel, hipStream_t st) {
 
 }  // namespace
 
-extern "C" int sa_gemm_bf16_ex(const void* A, int64_t lda, int64_t strideA, const void* W, int64_t ldw,
-                               int64_t strideW, const float* bias, void* C, int64_t ldc, int64_t strideC, int M, int N,
-                               int K, int batch, int epilogue, const float* residual, int64_t ldr, int64_t strideR,
-                               const float* gate, int64_t gate_bstride, int rows_per_batch, int kernel, int group_m,
-                               void* stream) {
+// a_panel_cols > 0: A is a_panel_cols-wide column panels a_panel_stride elements apart (lda = the panel
+// row stride), i.e. A[m, k] = A[(k / a_panel_cols) * a_panel_stride + m * lda + k % a_panel_cols] -- the
+// receive layout of the sequence-parallel head exchange, read by the O-projection in place (persistent
+// kernel only: a_panel_cols % 64 == 0, one panel per 64-column K-tile)
+extern "C" int sa_gemm_bf16_panels(const void* A, int64_t lda, int64_t strideA, const void* W, int64_t ldw,
+                                   int64_t strideW, const float* bias, void* C, int64_t ldc, int64_t strideC, int M,
+                                   int N, int K, int batch, int epilogue, const float* residual, int64_t ldr,
+                                   int64_t strideR, const float* gate, int64_t gate_bstride, int rows_per_batch,
+                                   int kernel, int group_m, int64_t a_panel_cols, int64_t a_panel_stride,
+                                   void* stream) {
   if (!A || !W || !C || M <= 0 || N <= 0 || K <= 0 || batch <= 0) return SA_ERR_ARG;
   if (K % BK != 0 || lda % 8 != 0 || ldw % 8 != 0) return SA_ERR_ARG;
   if ((((uintptr_t)A) & 15) || (((uintptr_t)W) & 15)) return SA_ERR_ARG;
@@ -821,7 +848,23 @@ extern "C" int sa_gemm_bf16_ex(const void* A, int64_t lda, int64_t strideA, cons
   if (kernel < KERNEL_AUTO || kernel > KERNEL_PERSISTENT || group_m < 0) return SA_ERR_ARG;
   GemmArgs g{(const bf16*)A, lda, strideA, (const bf16*)W, ldw, strideW, bias, C, ldc, strideC,
              residual, ldr, strideR, gate, gate_bstride, rows_per_batch > 0 ? rows_per_batch : 1, M, N, K,
-             group_m > 0 ? group_m : env_group_m()};
+             group_m > 0 ? group_m : env_group_m(), 0u, 0, 0};
+  if (a_panel_cols > 0) {
+    // panel p of K-tile T: (T * pmul) >> 20 == T / tpp for every T < K / 64 (checked), bytes in 32 bits
+    const long tpp = a_panel_cols / 64, np = (K + a_panel_cols - 1) / a_panel_cols;
+    if (a_panel_cols % 64 || lda < a_panel_cols || a_panel_stride < (long)M * lda || batch != 1 || K / 64 > 4096)
+      return SA_ERR_ARG;
+    if (kernel == KERNEL_PINGPONG) return SA_ERR_ARG;
+    const unsigned pmul = (unsigned)(((1L << 20) + tpp - 1) / tpp);
+    for (long T = 0; T < K / 64; ++T)
+      if ((long)((T * pmul) >> 20) != T / tpp) return SA_ERR_ARG;
+    const long delta = (a_panel_stride - a_panel_cols) * 2, extra = (np - 1) * a_panel_stride * 2;
+    if (delta >= 0x7fffffffL || extra + (long)BM * lda * 2 >= 0x7fffffffL) return SA_ERR_ARG;
+    g.a_pmul = pmul;
+    g.a_pdelta = (int)delta;
+    g.a_pextra = (int)extra;
+    kernel = KERNEL_PERSISTENT;
+  }
   hipStream_t st = (hipStream_t)stream;
   switch (epilogue) {
     case EPI_BF16: return launch<EPI_BF16>(g, batch, kernel, st);
@@ -832,6 +875,15 @@ extern "C" int sa_gemm_bf16_ex(const void* A, int64_t lda, int64_t strideA, cons
     case EPI_SILU_F32: return launch<EPI_SILU_F32>(g, batch, kernel, st);
     default: return SA_ERR_ARG;
   }
+}
+
+extern "C" int sa_gemm_bf16_ex(const void* A, int64_t lda, int64_t strideA, const void* W, int64_t ldw,
+                               int64_t strideW, const float* bias, void* C, int64_t ldc, int64_t strideC, int M, int N,
+                               int K, int batch, int epilogue, const float* residual, int64_t ldr, int64_t strideR,
+                               const float* gate, int64_t gate_bstride, int rows_per_batch, int kernel, int group_m,
+                               void* stream) {
+  return sa_gemm_bf16_panels(A, lda, strideA, W, ldw, strideW, bias, C, ldc, strideC, M, N, K, batch, epilogue,
+                             residual, ldr, strideR, gate, gate_bstride, rows_per_batch, kernel, group_m, 0, 0, stream);
 }
 
 extern "C" int sa_gemm_bf16(const void* A, int64_t lda, int64_t strideA, const void* W, int64_t ldw, int64_t strideW,

@@ -120,9 +120,17 @@ struct QkArgs {
   int nf, nh;         // pairs assigned to frame / height axes (rest: width)
 };
 
-template <int FIXED>
-__device__ __forceinline__ void rms_rope_one(bf16* p, const float* w, const QkArgs& a, int lane, int fi, int hi_,
-                                             int wi, bool rot) {
+// in-place store of one normalised 8-column chunk (c0 = column inside q or k)
+struct StoreInPlace {
+  bf16* p;
+  __device__ __forceinline__ void operator()(int c0, const float* y) const { store8<bf16>(p + c0, y); }
+};
+
+template <int FIXED, class Store>
+__device__ __forceinline__ void rms_rope_one(const bf16* p, const float* w, const QkArgs& a, int lane, int fi, int hi_,
+                                             int wi, bool rot, const Store& store) {
+  // explicit FMAs, no compiler contraction: the in-place and the SP pack instantiations round identically
+#pragma clang fp contract(off)
   const int nch = FIXED ? FIXED : (a.C + 511) / 512;
   float v[MAXV][8];
   float s = 0.f;
@@ -131,7 +139,7 @@ __device__ __forceinline__ void rms_rope_one(bf16* p, const float* w, const QkAr
     if (i < nch && (FIXED || i * 512 + lane * 8 < a.C)) {
       load8<bf16>(p + i * 512 + lane * 8, v[i]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += v[i][j] * v[i][j];
+      for (int j = 0; j < 8; ++j) s = fmaf(v[i][j], v[i][j], s);
     }
   const float r = rsqrtf(wave_sum(s) / a.C + a.eps);
 #pragma unroll
@@ -156,11 +164,11 @@ __device__ __forceinline__ void rms_rope_one(bf16* p, const float* w, const QkAr
           const float2 csn = *(const float2*)(a.rope + (pos * (a.head_dim / 2) + pi) * 2);
           const float cs = csn.x, sn = csn.y;
           const float re = y[j], im = y[j + 1];
-          y[j] = re * cs - im * sn;
-          y[j + 1] = re * sn + im * cs;
+          y[j] = fmaf(re, cs, -(im * sn));
+          y[j + 1] = fmaf(re, sn, im * cs);
         }
       }
-      store8<bf16>(p + c0, y);
+      store(c0, y);
     }
 }
 
@@ -181,8 +189,8 @@ __global__ __launch_bounds__(256) void qk_rmsnorm_rope_kernel(QkArgs a) {
     }
   }
   bf16* base = a.x + (long)row * a.ldx;
-  rms_rope_one<FIXED>(base + a.q_col, a.wq, a, lane, fi, hi_, wi, rot);
-  if (a.k_col >= 0) rms_rope_one<FIXED>(base + a.k_col, a.wk, a, lane, fi, hi_, wi, rot);
+  rms_rope_one<FIXED>(base + a.q_col, a.wq, a, lane, fi, hi_, wi, rot, StoreInPlace{base + a.q_col});
+  if (a.k_col >= 0) rms_rope_one<FIXED>(base + a.k_col, a.wk, a, lane, fi, hi_, wi, rot, StoreInPlace{base + a.k_col});
 }
 
 // Self-attention case (C = 1536 = 3 x 512, head_dim 128, q and k, 3-D RoPE): one wave per token row
@@ -198,13 +206,13 @@ __device__ __forceinline__ float2 wave_sum2(float2 v) {
   return v;
 }
 
-__global__ __launch_bounds__(256) void qk_rmsnorm_rope_pair_kernel(QkArgs a) {
+// store(i, yq, yk): chunk i (columns i*512 + lane*8 .. +7) of the normalised, rotated q and k
+template <class Store>
+__device__ __forceinline__ void qk_pair_row(const QkArgs& a, int row, int lane, const Store& store) {
+#pragma clang fp contract(off)  // explicit FMAs only (as rms_rope_one)
   constexpr int NCH = 3, HD = 128;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (row >= a.M) return;
-  bf16* qp = a.x + (long)row * a.ldx + a.q_col + lane * 8;
-  bf16* kp = a.x + (long)row * a.ldx + a.k_col + lane * 8;
+  const bf16* qp = a.x + (long)row * a.ldx + a.q_col + lane * 8;
+  const bf16* kp = a.x + (long)row * a.ldx + a.k_col + lane * 8;
   float q[NCH][8], k[NCH][8];
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
@@ -230,8 +238,8 @@ __global__ __launch_bounds__(256) void qk_rmsnorm_rope_pair_kernel(QkArgs a) {
   for (int i = 0; i < NCH; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      ss.x += q[i][j] * q[i][j];
-      ss.y += k[i][j] * k[i][j];
+      ss.x = fmaf(q[i][j], q[i][j], ss.x);
+      ss.y = fmaf(k[i][j], k[i][j], ss.y);
     }
   ss = wave_sum2(ss);
   const float rq = rsqrtf(ss.x / (NCH * 512) + a.eps), rk = rsqrtf(ss.y / (NCH * 512) + a.eps);
@@ -249,14 +257,102 @@ __global__ __launch_bounds__(256) void qk_rmsnorm_rope_pair_kernel(QkArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float qr = yq[2 * j], qi = yq[2 * j + 1], kr = yk[2 * j], ki = yk[2 * j + 1];
-      yq[2 * j] = qr * cs[j] - qi * sn[j];
-      yq[2 * j + 1] = qr * sn[j] + qi * cs[j];
-      yk[2 * j] = kr * cs[j] - ki * sn[j];
-      yk[2 * j + 1] = kr * sn[j] + ki * cs[j];
+      yq[2 * j] = fmaf(qr, cs[j], -(qi * sn[j]));
+      yq[2 * j + 1] = fmaf(qr, sn[j], qi * cs[j]);
+      yk[2 * j] = fmaf(kr, cs[j], -(ki * sn[j]));
+      yk[2 * j + 1] = fmaf(kr, sn[j], ki * cs[j]);
     }
+    store(i, yq, yk);
+  }
+}
+
+__global__ __launch_bounds__(256) void qk_rmsnorm_rope_pair_kernel(QkArgs a) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= a.M) return;
+  bf16* qp = a.x + (long)row * a.ldx + a.q_col + lane * 8;
+  bf16* kp = a.x + (long)row * a.ldx + a.k_col + lane * 8;
+  qk_pair_row(a, row, lane, [&](int i, const float* yq, const float* yk) {
     store8<bf16>(qp + i * 512, yq);
     store8<bf16>(kp + i * 512, yk);
+  });
+}
+
+// ---- the Ulysses send-slab pack (replaces the torch.cat packing around
+// wan/dist/wan_xfuser.py:72-115): the same per-row q/k RMSNorm + RoPE as above on the fused QKV GEMM
+// output of this rank's token chunk, written -- with v -- straight into per-destination slabs instead of
+// back in place.  Head group g (columns g*C/G .. of q, k and v) of token t in CFG row b goes to
+//   q:    destination my_part*G + g (the rank that runs attention for this chunk's query part), and
+//   k, v: destinations r*G + g for every query part r (each of them attends over all keys),
+// entry d of the device table {q_ptr, q_ld, q_bstride, kv_ptr, kv_ld, kv_bstride} (elements; q_ptr 0 =
+// no query slab for d): q row at q_ptr + b*q_bstride + t*q_ld, k at kv_ptr + b*kv_bstride + t*kv_ld, v at
+// k + C/G.  The entry of this rank itself points into its own attention inputs, the others into the send
+// buffers of the point-to-point exchange, so the pack is the only copy of Q/K/V on the way.
+struct PackArgs {
+  QkArgs qk;             // x = the [M, 3C] QKV rows (q at column 0, k at C, v at 2C)
+  const long* table;     // [G*R][6]
+  int G, R, my_part;
+  int b_offset;          // CFG row of launch row 0 is b_offset + row / rows_per_batch
+};
+
+struct PackStore {
+  const long* table;
+  int G, R, my_part, hgd;
+  long b, t;
+  const bf16* vrow;  // this row's v
+  template <bool Q>
+  __device__ __forceinline__ void put(int c0, const float* y) const {
+    const int g = c0 / hgd, w = c0 - g * hgd;
+    if (Q) {
+      const long* e = table + (long)(my_part * G + g) * 6;
+      store8<bf16>((bf16*)e[0] + b * e[2] + t * e[1] + w, y);
+    } else {
+      const u32x4 vv = *(const u32x4*)(vrow + c0);
+      for (int r = 0; r < R; ++r) {
+        const long* e = table + (long)(r * G + g) * 6;
+        bf16* kd = (bf16*)e[3] + b * e[5] + t * e[4] + w;
+        store8<bf16>(kd, y);
+        *(u32x4*)(kd + hgd) = vv;
+      }
+    }
   }
+};
+
+template <bool Q>
+struct PackOne {
+  const PackStore* ps;
+  __device__ __forceinline__ void operator()(int c0, const float* y) const { ps->put<Q>(c0, y); }
+};
+
+template <int FIXED, bool PAIR>
+__global__ __launch_bounds__(256) void qkv_pack_kernel(PackArgs pa) {
+  const QkArgs& a = pa.qk;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= a.M) return;
+  const bf16* base = a.x + (long)row * a.ldx;
+  const PackStore ps{pa.table, pa.G, pa.R, pa.my_part, a.C / pa.G, (long)(pa.b_offset + row / a.rows_per_batch),
+                     (long)(row % a.rows_per_batch), base + 2 * a.C};
+  if (PAIR && a.rope && a.head_dim == 128) {  // the 1.3B shape: the pair path, as the in-place launcher takes
+    qk_pair_row(a, row, lane, [&](int i, const float* yq, const float* yk) {
+      ps.put<true>(i * 512 + lane * 8, yq);
+      ps.put<false>(i * 512 + lane * 8, yk);
+    });
+    return;
+  }
+  bool rot = false;
+  int fi = 0, hi_ = 0, wi = 0;
+  if (a.rope) {
+    const int t = a.tok_offset + row % a.rows_per_batch;
+    if (t < a.F * a.H * a.W) {
+      rot = true;
+      fi = t / (a.H * a.W);
+      hi_ = (t / a.W) % a.H;
+      wi = t % a.W;
+    }
+  }
+  rms_rope_one<FIXED>(base, a.wq, a, lane, fi, hi_, wi, rot, PackOne<true>{&ps});
+  rms_rope_one<FIXED>(base + a.C, a.wk, a, lane, fi, hi_, wi, rot, PackOne<false>{&ps});
 }
 
 template <typename TI, typename TO>
@@ -310,6 +406,31 @@ extern "C" int sa_qk_rmsnorm_rope(void* x, int64_t ldx, int q_col, int k_col, co
     hipLaunchKernelGGL(qk_rmsnorm_rope_kernel<10>, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(qk_rmsnorm_rope_kernel<0>, dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
+  SA_LAUNCH_CHECK();
+  return SA_OK;
+}
+
+extern "C" int sa_qkv_pack(const void* x, int64_t ldx, const float* wq, const float* wk, int M, int C, int head_dim,
+                           float eps, const float* rope, int rows_per_batch, int tok_offset, int F, int H, int W,
+                           int n_frame_pairs, int n_height_pairs, const int64_t* table, int G, int R, int my_part,
+                           int b_offset, void* stream) {
+  if (!x || !wq || !wk || !table || M <= 0 || C <= 0 || C % 512 || C > 512 * MAXV || ldx % 8 || ldx < 3 * C)
+    return SA_ERR_ARG;
+  if (G <= 0 || R <= 0 || my_part < 0 || my_part >= R || b_offset < 0 || rows_per_batch <= 0) return SA_ERR_ARG;
+  if (C % G || (C / G) % 8) return SA_ERR_ARG;
+  if (rope && (head_dim % 8 || F <= 0 || H <= 0 || W <= 0)) return SA_ERR_ARG;
+  PackArgs pa{QkArgs{(bf16*)x, ldx, 0, C, wq, wk, M, C, head_dim, eps, rope, rows_per_batch, tok_offset, F, H, W,
+                     n_frame_pairs, n_height_pairs},
+              (const long*)table, G, R, my_part, b_offset};
+  static const bool generic = getenv("SA_QK_GENERIC") != nullptr;  // the in-place launcher's A/B switch
+  if (C == 1536 && !generic)
+    hipLaunchKernelGGL((qkv_pack_kernel<3, true>), dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, pa);
+  else if (C == 1536)
+    hipLaunchKernelGGL((qkv_pack_kernel<3, false>), dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, pa);
+  else if (C == 5120)
+    hipLaunchKernelGGL((qkv_pack_kernel<10, false>), dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, pa);
+  else
+    hipLaunchKernelGGL((qkv_pack_kernel<0, false>), dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, pa);
   SA_LAUNCH_CHECK();
   return SA_OK;
 }

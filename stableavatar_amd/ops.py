@@ -39,14 +39,26 @@ GEMM_AUTO, GEMM_PINGPONG, GEMM_PERSISTENT = 0, 1, 2
 
 
 def linear(x, weight, bias=None, epilogue=EPI_BF16, out=None, residual=None, gate=None, rows_per_batch=0,
-           kernel=GEMM_AUTO, group_m=0):
+           kernel=GEMM_AUTO, group_m=0, a_panels=None):
     """y = epi(x @ weight^T + bias).  x: bf16 [M, K] (row stride may exceed K), weight: bf16 [N, K].
     EPI_RES_F32: out(f32) = residual + y * gate[row // rows_per_batch] (gate f32 [B, N] view).
-    kernel / group_m: per-call GEMM schedule selection (A/B benchmarks and tests; default auto)."""
+    kernel / group_m: per-call GEMM schedule selection (A/B benchmarks and tests; default auto).
+    a_panels = (panel_cols, panel_stride): x is the first of K / panel_cols column panels [M, panel_cols],
+    panel p starting panel_stride elements after x (sa_gemm_bf16_panels; EPI_RES_F32 only)."""
     _check(x, torch.bfloat16, "linear.x")
     _check(weight, torch.bfloat16, "linear.weight")
     M, K = x.shape
     N = weight.shape[0]
+    pc = ps = 0
+    if a_panels is not None:
+        pc, ps = a_panels
+        if K != pc or weight.shape[1] % pc or epilogue != EPI_RES_F32:
+            raise ValueError("linear: a_panels needs x = the first [M, panel_cols] panel and EPI_RES_F32")
+        K = weight.shape[1]
+        base = x.untyped_storage().data_ptr()
+        end = x.data_ptr() + ((K // pc - 1) * ps + (M - 1) * x.stride(0) + pc) * 2
+        if end > base + x.untyped_storage().nbytes():
+            raise ValueError("linear: the column panels run past x's storage")
     assert weight.shape[1] == K and x.stride(1) == 1 and weight.stride(1) == 1
     f32_out = epilogue in (EPI_F32, EPI_RES_F32, EPI_SILU_F32)
     if out is None:
@@ -64,9 +76,9 @@ def linear(x, weight, bias=None, epilogue=EPI_BF16, out=None, residual=None, gat
         if gate is not None:
             assert gate.dtype == torch.float32 and gate.stride(-1) == 1
             gstride = gate.stride(0)
-    call("sa_gemm_bf16_ex", x.data_ptr(), x.stride(0), 0, weight.data_ptr(), weight.stride(0), 0, _p(bias),
+    call("sa_gemm_bf16_panels", x.data_ptr(), x.stride(0), 0, weight.data_ptr(), weight.stride(0), 0, _p(bias),
          out.data_ptr(), out.stride(0), 0, M, N, K, 1, epilogue, _p(residual), ldr, 0, _p(gate), gstride,
-         rows_per_batch, kernel, group_m, _stream())
+         rows_per_batch, kernel, group_m, pc, ps, _stream())
     return out
 
 
@@ -83,18 +95,21 @@ ATTN_AUTO = 0
 
 
 def attention(q, k, v, out, segs, nseg, max_q_len, heads, head_dim=128, scale=None, accumulate=False,
-              kernel=ATTN_AUTO):
+              kernel=ATTN_AUTO, o_rows=None):
     """Flash attention over row-segment table `segs` (int32 [nseg,4] on device); kernel = per-call
-    schedule selection (sa_attn_fwd_ex; 0 = auto)."""
+    schedule selection (sa_attn_fwd_ex; 0 = auto); o_rows = int32 device map query row -> output row of
+    `out` (sa_attn_fwd_map)."""
     for t, n in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
         _check(t, torch.bfloat16, f"attention.{n}")
         assert t.stride(-1) == 1
     assert segs.dtype == torch.int32 and segs.is_cuda
+    if o_rows is not None:
+        assert o_rows.dtype == torch.int32 and o_rows.is_cuda and o_rows.is_contiguous()
     if scale is None:
         scale = head_dim ** -0.5
-    call("sa_attn_fwd_ex", q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), segs.data_ptr(), nseg,
+    call("sa_attn_fwd_map", q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), segs.data_ptr(), nseg,
          max_q_len, heads, head_dim, q.stride(0), k.stride(0), v.stride(0), out.stride(0), float(scale),
-         int(accumulate), kernel, _stream())
+         int(accumulate), kernel, _p(o_rows), _stream())
     return out
 
 
@@ -133,6 +148,19 @@ def qk_rmsnorm_rope(x, q_col, k_col, wq, wk, C, eps, rope=None, rows_per_batch=0
     call("sa_qk_rmsnorm_rope", x.data_ptr(), x.stride(0), q_col, k_col, wq.data_ptr(), _p(wk), M, C, head_dim,
          float(eps), _p(rope), rows_per_batch, tok_offset, F, H, W, n_frame_pairs, n_height_pairs, _stream())
     return x
+
+
+def qkv_pack(x, wq, wk, C, eps, table, G, R, my_part, rope=None, rows_per_batch=0, tok_offset=0, grid=(1, 1, 1),
+             head_dim=128, n_frame_pairs=0, n_height_pairs=0, b_offset=0):
+    """RMSNorm + RoPE of the q / k columns of the [M, 3C] QKV rows x, written with v into the sequence-parallel
+    send slabs / attention inputs that the int64 device `table` [G*R, 6] names (sa_qkv_pack)."""
+    _check(x, torch.bfloat16, "qkv_pack.x")
+    assert x.stride(1) == 1 and x.shape[1] >= 3 * C
+    assert table.dtype == torch.int64 and table.is_cuda and tuple(table.shape) == (G * R, 6)
+    F, H, W = grid
+    call("sa_qkv_pack", x.data_ptr(), x.stride(0), wq.data_ptr(), wk.data_ptr(), x.shape[0], C, head_dim, float(eps),
+         _p(rope), rows_per_batch, tok_offset, F, H, W, n_frame_pairs, n_height_pairs, table.data_ptr(), G, R, my_part,
+         b_offset, _stream())
 
 
 def patch_im2col(x, y, B, F, H, W, out, Kpad, Lpad, x_frame_offset=0, x_batch_broadcast=False):

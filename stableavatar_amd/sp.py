@@ -20,9 +20,10 @@ Here, one process per GPU (torch.distributed; backend "nccl" = RCCL over xGMI):
 * the head output is all-gathered so every rank holds the full noise prediction and runs the same
   sampler step (bit-identical latents on every rank).
 
-Everything in this module is data movement (torch copies + collectives); the attention itself is the
-HIP kernel, called by the transformer.  The exchange is written against torch.distributed only, so
-the same code runs under gloo on CPU (tests/test_sp_cpu.py) and RCCL on MI355X.
+This module holds the layout and the transfers (torch.distributed point-to-point: RCCL on MI355X, gloo on
+CPU in tests/test_sp_cpu.py); the pack (RMSNorm + RoPE writing send slabs), the attention (writing its
+output by row map) and the O-projection (reading column panels) are HIP kernels called by the transformer,
+so no copy pass runs on the way in or out.
 """
 from __future__ import annotations
 
@@ -69,183 +70,144 @@ def padded_len(seq_len: int, world: int) -> int:
     return int(math.ceil(seq_len / world)) * world
 
 
-def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group) -> None:
-    """all_to_all_single on flat buffers; gloo cannot move device tensors, so they are staged
-    through host memory there (test configuration: several ranks sharing one GPU)."""
-    if inp.is_cuda and dist.get_backend(group) == "gloo":
-        o = torch.empty(out.shape, dtype=out.dtype)
-        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=group)
-        out.copy_(o)
-    else:
-        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
-
-
 class Pending:
-    """An issued all-to-all and the unpack that runs once it has landed.
+    """Issued point-to-point transfers and the host-staged copies (gloo only) that finish them.
 
-    On RCCL the collective runs on ProcessGroupNCCL's own stream; ``wait()`` makes the caller's
-    current stream wait for it (no host sync) and then enqueues the unpack copies there, so compute
-    queued on the current stream between issue and ``wait()`` overlaps the transfer."""
+    On RCCL the transfers run on ProcessGroupNCCL's own stream; ``wait()`` makes the caller's current
+    stream wait for them (no host sync), so compute queued on the current stream between issue and
+    ``wait()`` overlaps the transfer."""
 
-    def __init__(self, work, finish):
-        self.work, self.finish = work, finish
+    def __init__(self, works, finish=None, keep=None):
+        self.works, self.finish, self.keep = works, finish, keep
 
     def wait(self):
-        if self.work is not None:
-            self.work.wait()
-            self.work = None
+        for w in self.works or ():
+            w.wait()
+        self.works = None
         if self.finish is not None:
             self.finish()
             self.finish = None
+        self.keep = None
 
 
-def _a2a_async(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group):
-    if inp.is_cuda and dist.get_backend(group) == "gloo":
-        _a2a(out, inp, out_splits, in_splits, group)  # host-staged: completes here
-        return None
-    return dist.all_to_all_single(out, inp, out_splits, in_splits, group=group, async_op=True)
+def _p2p(sends, recvs, group):
+    """sends / recvs: lists of (contiguous tensor, peer rank inside ``group``).  RCCL: one coalesced group of sends and
+    receives landing in place.  gloo cannot move device tensors, so there (several ranks sharing one GPU in
+    the tests) they are staged through host memory and the device receive views are filled on wait()."""
+    if not sends and not recvs:
+        return Pending(None)
+    t0 = (sends or recvs)[0][0]
+    if dist.get_backend(group) != "gloo":
+        ops = [dist.P2POp(dist.isend, t, group=group, group_peer=peer) for t, peer in sends]
+        ops += [dist.P2POp(dist.irecv, t, group=group, group_peer=peer) for t, peer in recvs]
+        return Pending(dist.batch_isend_irecv(ops), keep=(sends, recvs))
+    staged = t0.is_cuda
+    works, keep, back = [], [], []
+    for t, peer in sends:
+        h = t.cpu() if staged else t
+        keep.append(h)
+        works.append(dist.isend(h, group=group, group_dst=peer))
+    for t, peer in recvs:
+        h = torch.empty(t.shape, dtype=t.dtype) if staged else t
+        keep.append(h)
+        works.append(dist.irecv(h, group=group, group_src=peer))
+        if staged:
+            back.append((t, h))
+
+    def finish():
+        for t, h in back:
+            t.copy_(h)
+
+    return Pending(works, finish if back else None, keep)
 
 
 class UlyssesExchange:
-    """The two all-to-alls around one sequence-parallel self-attention.
+    """The data layout and the point-to-point transfers around one sequence-parallel self-attention
+    (usp_attn_forward, wan/dist/wan_xfuser.py:72-115), for B CFG rows of Lc tokens per rank.
 
-    ``to_heads`` / ``to_tokens`` move all CFG rows in one collective each.  ``to_heads_row`` /
-    ``to_tokens_row`` move one CFG row and return a ``Pending``: the transformer issues the three
-    rows' Q/K/V exchanges up front and runs row b's attention while rows b+1.. are in flight and row
-    b-1's output travels back (comm/compute overlap on separate HIP streams)."""
+    There is no pack or unpack pass: every tensor lands where its consumer reads it.
+      * ``q`` [B*Lq, hg*D] (rows b*Lq + j*Lc + t: token t of chunk j of this rank's query part) and ``kv``
+        [B*Lp, 2*hg*D] (rows b*Lp + r*Lc + t, k | v) are the attention inputs; this rank's own chunk is
+        written into them by ``ops.qkv_pack`` (through ``table``), the other chunks arrive into them;
+      * ``sq[d]`` [B, Lc, hg*D] and ``skv[d]`` [B, Lc, 2*hg*D] are the send slabs of remote destination d,
+        also written by ``ops.qkv_pack``;
+      * ``obuf`` [2*G*B*Lc, hg*D]: the attention writes query chunk j's head outputs to rows (j*B + b)*Lc + t
+        of the first half (the send slab of chunk j's owner) -- except this rank's own chunk, which goes to
+        the second half, ``pan``, whose panel j (rows j*B*Lc ..) receives head group j of this rank's tokens
+        from the other ranks of the query part: ``pan`` is the O-projection's input in column panels
+        (``ops.linear(..., a_panels=(hg*D, B*Lc*hg*D))``).  ``omap`` is that attention output row map."""
 
-    def __init__(self, plan: SPPlan, group=None):
-        self.plan = plan
-        self.group = group
-
-    # tokens -> heads ---------------------------------------------------------------------------
-    def to_heads(self, qkv: torch.Tensor, B: int, Lc: int, D: int):
-        """qkv: [B*Lc, 3*H*D] (q | k | v, head h at column h*D) of this rank's chunk.
-        Returns q [B*Lq, hg*D] (Lq = G*Lc query rows of this rank's part, batch-major) and
-        kv [B*Lp, 2*hg*D] (k | v of this rank's head group for the full sequence)."""
-        p = self.plan
-        N, G, hg = p.world, p.G, p.hg
-        H = p.heads
-        x = qkv.view(B, Lc, 3, G, hg * D)
-        q_el = B * Lc * hg * D
-        kv_el = 2 * q_el
-        sends, in_splits = [], []
-        my_part = p.part_of_chunk(p.rank)
-        for j in range(N):
-            gj, pj = j % G, j // G
-            blk = []
-            if pj == my_part:
-                blk.append(x[:, :, 0, gj].reshape(-1))
-            blk.append(x[:, :, 1:3, gj].reshape(-1))  # [B, Lc, 2, hg*D]
-            sends.extend(blk)
-            in_splits.append(sum(t.numel() for t in blk))
-        send = torch.cat(sends)
-        out_splits = []
-        for r in range(N):
-            out_splits.append((q_el if p.part_of_chunk(r) == p.part else 0) + kv_el)
-        recv = torch.empty(sum(out_splits), dtype=qkv.dtype, device=qkv.device)
-        _a2a(recv, send, out_splits, in_splits, self.group)
-        # unpack: per source rank r, [Q (if r in my part)] [KV]
-        qs, kvs = [], []
-        off = 0
-        for r in range(N):
-            if p.part_of_chunk(r) == p.part:
-                qs.append(recv[off:off + q_el].view(B, Lc, hg * D))
-                off += q_el
-            kvs.append(recv[off:off + kv_el].view(B, Lc, 2 * hg * D))
-            off += kv_el
-        q = torch.stack(qs, 1).reshape(B * len(qs) * Lc, hg * D)        # [B, G*Lc, hg*D]
-        kv = torch.stack(kvs, 1).reshape(B * N * Lc, 2 * hg * D)         # [B, Lp, (k|v) hg*D]
-        del H
-        return q, kv
-
-    # heads -> tokens ---------------------------------------------------------------------------
-    def to_tokens(self, o: torch.Tensor, B: int, Lc: int, D: int, out: torch.Tensor) -> torch.Tensor:
-        """o: [B*G*Lc, hg*D] attention output of this rank's (part, head group); out: [B*Lc, H*D]
-        receives this rank's chunk for all heads."""
-        p = self.plan
-        N, G, hg = p.world, p.G, p.hg
-        el = B * Lc * hg * D
-        ov = o.view(B, G, Lc, hg * D)
-        sends, in_splits = [], []
-        for r in range(N):
-            if p.part_of_chunk(r) == p.part:
-                sends.append(ov[:, r - p.part * G].reshape(-1))
-                in_splits.append(el)
+    def __init__(self, plan: SPPlan, B: int, Lc: int, D: int, device, group=None, dtype=torch.bfloat16):
+        self.plan, self.group, self.B, self.Lc, self.D = plan, group, B, Lc, D
+        p = plan
+        N, G, g = p.world, p.G, p.group
+        self.hgd = hgd = p.hg * D
+        self.Lq, self.Lp = G * Lc, N * Lc
+        self.q = torch.empty(B * self.Lq, hgd, device=device, dtype=dtype)
+        self.kv = torch.empty(B * self.Lp, 2 * hgd, device=device, dtype=dtype)
+        self.obuf = torch.empty(2 * G * B * Lc, hgd, device=device, dtype=dtype)
+        self.pan = self.obuf[G * B * Lc:]
+        self.remote = [d for d in range(N) if d != p.rank]
+        self.sq = {d: torch.empty(B, Lc, hgd, device=device, dtype=dtype) for d in self.remote if d // G == p.part}
+        self.skv = {d: torch.empty(B, Lc, 2 * hgd, device=device, dtype=dtype) for d in self.remote}
+        qv = self.q.view(B, self.Lq, hgd)
+        kvv = self.kv.view(B, self.Lp, 2 * hgd)
+        rows = []
+        for d in range(N):
+            if d == p.rank:
+                qd, kd = qv[:, g * Lc:(g + 1) * Lc], kvv[:, p.rank * Lc:(p.rank + 1) * Lc]
             else:
-                in_splits.append(0)
-        send = torch.cat(sends)
-        out_splits = [el if (j // G) == p.part_of_chunk(p.rank) else 0 for j in range(N)]
-        recv = torch.empty(sum(out_splits), dtype=o.dtype, device=o.device)
-        _a2a(recv, send, out_splits, in_splits, self.group)
-        # sources j with part == my chunk's part, in j order = head group order
-        parts = recv.view(G, B, Lc, hg * D)
-        out.view(B, Lc, G, hg * D).copy_(parts.permute(1, 2, 0, 3))
-        return out
+                qd, kd = self.sq.get(d), self.skv[d]
+            rows.append([0, 0, 0] if qd is None else [qd.data_ptr(), qd.stride(1), qd.stride(0)])
+            rows[-1] += [kd.data_ptr(), kd.stride(1), kd.stride(0)]
+        self.slabs = {d: (self.sq.get(d), self.skv[d]) for d in self.remote}
+        self.slabs[p.rank] = (qv[:, g * Lc:(g + 1) * Lc], kvv[:, p.rank * Lc:(p.rank + 1) * Lc])
+        self.table = torch.tensor(rows, dtype=torch.int64).to(device)
+        j = torch.arange(G).view(1, G, 1)
+        b = torch.arange(B).view(B, 1, 1)
+        t = torch.arange(Lc).view(1, 1, Lc)
+        omap = (j == g).to(torch.int64) * (G * B * Lc) + (j * B + b) * Lc + t  # [B, G, Lc] = q row order
+        self.omap = omap.reshape(-1).to(torch.int32).to(device)
 
-    # one CFG row at a time, asynchronous ----------------------------------------------------------
-    def to_heads_row(self, qkv: torch.Tensor, b: int, B: int, Lc: int, D: int,
-                     q_dst: torch.Tensor, kv_dst: torch.Tensor) -> Pending:
-        """Row b of ``to_heads``: q_dst [B*G*Lc, hg*D] and kv_dst [B*Lp, 2*hg*D] (the layouts
-        ``to_heads`` returns) receive row b once the returned Pending is waited on."""
+    def heads(self, rows) -> Pending:
+        """Q/K/V of CFG rows ``rows`` to the ranks that attend over them (after ``ops.qkv_pack``)."""
         p = self.plan
-        N, G, hg = p.world, p.G, p.hg
-        x = qkv.view(B, Lc, 3, G, hg * D)[b]
-        q_el = Lc * hg * D
-        kv_el = 2 * q_el
-        my_part = p.part_of_chunk(p.rank)
-        sends, in_splits = [], []
-        for j in range(N):
-            gj, pj = j % G, j // G
-            n = 0
-            if pj == my_part:
-                sends.append(x[:, 0, gj].reshape(-1))
-                n += q_el
-            sends.append(x[:, 1:3, gj].reshape(-1))  # [Lc, 2, hg*D]
-            in_splits.append(n + kv_el)
-        send = torch.cat(sends)
-        src_q = [p.part_of_chunk(r) == p.part for r in range(N)]
-        out_splits = [(q_el if src_q[r] else 0) + kv_el for r in range(N)]
-        recv = torch.empty(sum(out_splits), dtype=qkv.dtype, device=qkv.device)
-        work = _a2a_async(recv, send, out_splits, in_splits, self.group)
-        Lq = G * Lc
+        G, Lc, Lq, Lp = p.G, self.Lc, self.Lq, self.Lp
+        sends, recvs = [], []
+        for b in rows:
+            for d in self.remote:
+                if d in self.sq:
+                    sends.append((self.sq[d][b], d))
+                sends.append((self.skv[d][b], d))
+            for r in self.remote:
+                if r // G == p.part:
+                    q0 = b * Lq + (r % G) * Lc
+                    recvs.append((self.q[q0:q0 + Lc], r))
+                recvs.append((self.kv[b * Lp + r * Lc:b * Lp + (r + 1) * Lc], r))
+        return _p2p(sends, recvs, self.group)
 
-        def finish():
-            qv = q_dst.view(B, Lq, hg * D)[b]
-            kvv = kv_dst.view(B, N * Lc, 2 * hg * D)[b]
-            off, qi = 0, 0
-            for r in range(N):
-                if src_q[r]:
-                    qv[qi * Lc:(qi + 1) * Lc].copy_(recv[off:off + q_el].view(Lc, hg * D))
-                    qi += 1
-                    off += q_el
-                kvv[r * Lc:(r + 1) * Lc].copy_(recv[off:off + kv_el].view(Lc, 2 * hg * D))
-                off += kv_el
-
-        return Pending(work, finish)
-
-    def to_tokens_row(self, o: torch.Tensor, b: int, B: int, Lc: int, D: int, out: torch.Tensor) -> Pending:
-        """Row b of ``to_tokens``: o [B*G*Lc, hg*D]; out [B*Lc, H*D] receives row b on wait()."""
+    def tokens(self, rows) -> Pending:
+        """Head outputs of CFG rows ``rows`` back to the owners of their tokens (after the attention)."""
         p = self.plan
-        N, G, hg = p.world, p.G, p.hg
-        el = Lc * hg * D
-        ov = o.view(B, G, Lc, hg * D)[b]
-        sends, in_splits = [], []
-        for r in range(N):
-            if p.part_of_chunk(r) == p.part:
-                sends.append(ov[r - p.part * G].reshape(-1))
-                in_splits.append(el)
-            else:
-                in_splits.append(0)
-        send = torch.cat(sends)
-        out_splits = [el if (j // G) == p.part_of_chunk(p.rank) else 0 for j in range(N)]
-        recv = torch.empty(sum(out_splits), dtype=o.dtype, device=o.device)
-        work = _a2a_async(recv, send, out_splits, in_splits, self.group)
+        G, B, Lc = p.G, self.B, self.Lc
+        sends, recvs = [], []
+        for b in rows:
+            for j in range(G):
+                if j != p.group:
+                    r0 = (j * B + b) * Lc
+                    sends.append((self.obuf[r0:r0 + Lc], p.part * G + j))
+            for j in range(G):
+                if j != p.group:
+                    r0 = (j * B + b) * Lc
+                    recvs.append((self.pan[r0:r0 + Lc], p.part * G + j))
+        return _p2p(sends, recvs, self.group)
 
-        def finish():
-            out.view(B, Lc, G, hg * D)[b].copy_(recv.view(G, Lc, hg * D).permute(1, 0, 2))
-
-        return Pending(work, finish)
+    def panels(self, rows=None):
+        """(first panel [M, hg*D], (panel_cols, panel_stride)) of the O-projection input for CFG rows
+        ``rows`` (a range; None = all)"""
+        B, Lc = self.B, self.Lc
+        b0, nb = (0, B) if rows is None else (rows.start, len(rows))
+        return self.pan[b0 * Lc:(b0 + nb) * Lc], (self.hgd, B * Lc * self.hgd)
 
 
 def all_gather_slots(buf: torch.Tensor, rank: int, group=None) -> Pending:

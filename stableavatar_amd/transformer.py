@@ -229,6 +229,7 @@ class WanTransformer3DFantasyModel(nn.Module):
         self._ws = {}
         self._ctx_cache = None
         self._segs = _Seg()
+        self._sp_ex = None
         self._split_cache = {}
         self._events = None  # optional list to record (start, end) events around self-attention
         self._sp_enabled = False
@@ -322,7 +323,7 @@ class WanTransformer3DFantasyModel(nn.Module):
         self.sp_group = group
         self.sp_world_size = dist.get_world_size(group)
         self.sp_world_rank = dist.get_rank(group)
-        self._sp_enabled = True  # the exchange path runs even at degree 1 (a self all-to-all)
+        self._sp_enabled = True  # the exchange path runs even at degree 1 (pack + row-mapped attention + panels)
 
     def disable_multi_gpus_inference(self):
         """back to single-GPU forwards (every rank its own clip)"""
@@ -442,6 +443,16 @@ class WanTransformer3DFantasyModel(nn.Module):
     def invalidate_context(self):
         """drop the cached text / image K/V (the pipeline calls this at the start of every denoise)"""
         self._ctx_cache = None
+
+    def _sp_exchange(self, plan, B, Lc, dev):
+        """the sequence-parallel exchange buffers (attention inputs, send slabs, output / panel buffer, pack
+        table, output row map) for this shape, kept across layers, steps and calls (one shape at a time)"""
+        key = (plan, B, Lc, self.d, str(dev), id(self.sp_group))
+        ex = self._sp_ex
+        if ex is None or ex[0] != key:
+            self._sp_ex = None  # free the previous shape's buffers first
+            ex = self._sp_ex = (key, sp.UlyssesExchange(plan, B, Lc, self.d, dev, self.sp_group))
+        return ex[1]
 
     @staticmethod
     def _ctx_key(context, clip_fea):
@@ -592,7 +603,7 @@ class WanTransformer3DFantasyModel(nn.Module):
         hp, wp = Hh // 2, Ww // 2
         real = Fw * hp * wp
         NS, rank = self.sp_world_size, self.sp_world_rank
-        SP = self._sp_enabled  # sequence-parallel path (NS ranks; at NS = 1 the exchanges are self-copies)
+        SP = self._sp_enabled  # sequence-parallel path (NS ranks; at NS = 1 no transfer, the same kernels)
         S = int(seq_len)  # the single-GPU sequence (1B:983): these keys are attended, SP's extra pads are not
         Lp = sp.padded_len(S, NS)
         assert real <= S, "seq_len smaller than the token count"
@@ -671,13 +682,13 @@ class WanTransformer3DFantasyModel(nn.Module):
             G = S // n_fr
             if SP:
                 plan = sp.make_plan(NS, rank, H_)
-                exch = sp.UlyssesExchange(plan, self.sp_group)
-                Lq, hg = plan.G * Lc, plan.hg
+                ex = self._sp_exchange(plan, B, Lc, dev)
+                Lq, hg, hgd = plan.G * Lc, plan.hg, plan.hg * self.d
+                pack_kw = dict(table=ex.table, G=plan.G, R=plan.R, my_part=plan.part)
                 # keys: the S tokens of the single-GPU sequence (the SP pads past S are queries only, their
                 # outputs are never read), so any degree reproduces the single-GPU forward
                 segs_self = self._segs.get(("self_sp", B, Lp, Lq, S), [[b * Lq, Lq, b * Lp, S] for b in range(B)],
                                            dev)
-                o_sp = torch.empty(B * Lq, hg * self.d, device=dev, dtype=torch.bfloat16)
                 # exchange schedule (SA_SP_OVERLAP: 0 one synchronous batched exchange per direction; 2 per-row
                 # exchanges and per-row attention; 3 per-row Q/K/V exchanges, batched attention; 1 = auto:
                 # 2 when per-row attention launches add no waves over the CUs -- a row's launch has ceil(Lq /
@@ -691,9 +702,6 @@ class WanTransformer3DFantasyModel(nn.Module):
                 if ov == "1":
                     ov = "2" if B * -(-wg_row // n_cu) <= -(-(B * wg_row) // n_cu) else "3"
                 sp_rows, sp_rows_x = ov == "2", ov == "3" and B > 1
-                if sp_rows or sp_rows_x:
-                    q_sp = torch.empty(B * Lq, hg * self.d, device=dev, dtype=torch.bfloat16)
-                    kv_sp = torch.empty(B * Lp, 2 * hg * self.d, device=dev, dtype=torch.bfloat16)
                 if sp_rows:
                     segs_rows = [self._segs.get(("self_sp_row", b, Lp, Lq, S), [[b * Lq, Lq, b * Lp, S]], dev)
                                  for b in range(B)]
@@ -718,55 +726,62 @@ class WanTransformer3DFantasyModel(nn.Module):
                                n_frame_pairs=self.d // 2 - 2 * (self.d // 6), n_height_pairs=self.d // 6)
                 if SP and sp_rows:
                     # Ulysses pipelined over the CFG rows: row b's Q/K/V exchange is issued right after its
-                    # QKV GEMM + norm/RoPE (so it travels under rows b+1..'s GEMMs), row b's attention waits
+                    # QKV GEMM + pack (so it travels under rows b+1..'s GEMMs), row b's attention waits
                     # only on it, and row b's output exchange travels under the next rows' attention and
                     # the earlier rows' O-projections
                     pend = []
                     for b in range(B):
                         rs = slice(b * Lc, (b + 1) * Lc)
                         ops.linear(ws.mod[rs], L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv[rs])
-                        ops.qk_rmsnorm_rope(ws.qkv[rs], 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
-                        pend.append(exch.to_heads_row(ws.qkv, b, B, Lc, self.d, q_sp, kv_sp))
+                        ops.qkv_pack(ws.qkv[rs], L.nq, L.nk, dim, self.eps, b_offset=b, **pack_kw, **rope_kw)
+                        pend.append(ex.heads([b]))
                     back = []
                     for b in range(B):
                         pend[b].wait()
                         ev0 = self._record_event()
-                        ops.attention(q_sp, kv_sp[:, :hg * self.d], kv_sp[:, hg * self.d:], o_sp, segs_rows[b], 1, Lq,
-                                      hg, kernel=self.attn_kernel)
+                        ops.attention(ex.q, ex.kv[:, :hgd], ex.kv[:, hgd:], ex.obuf, segs_rows[b], 1, Lq, hg,
+                                      kernel=self.attn_kernel, o_rows=ex.omap)
                         self._record_span(ev0, rows=1, batch=B)
-                        back.append(exch.to_tokens_row(o_sp, b, B, Lc, self.d, ws.att))
+                        back.append(ex.tokens([b]))
                     for b in range(B):
                         rs = slice(b * Lc, (b + 1) * Lc)
                         back[b].wait()
-                        ops.linear(ws.att[rs], L.w_o, L.b_o, ops.EPI_RES_F32, out=x[rs], residual=x[rs],
-                                   gate=em[b:b + 1, 2], rows_per_batch=Lc)
-                else:
+                        a0, pnl = ex.panels(range(b, b + 1))
+                        ops.linear(a0, L.w_o, L.b_o, ops.EPI_RES_F32, out=x[rs], residual=x[rs],
+                                   gate=em[b:b + 1, 2], rows_per_batch=Lc, a_panels=pnl)
+                elif SP:
                     if sp_rows_x:
-                        # per-row Q/K/V exchanges issued as each row's QKV GEMM + norm/RoPE lands (they travel
+                        # per-row Q/K/V exchanges issued as each row's QKV GEMM + pack lands (they travel
                         # under the later rows' GEMMs), one batched attention once all have arrived
                         pend = []
                         for b in range(B):
                             rs = slice(b * Lc, (b + 1) * Lc)
                             ops.linear(ws.mod[rs], L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv[rs])
-                            ops.qk_rmsnorm_rope(ws.qkv[rs], 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
-                            pend.append(exch.to_heads_row(ws.qkv, b, B, Lc, self.d, q_sp, kv_sp))
+                            ops.qkv_pack(ws.qkv[rs], L.nq, L.nk, dim, self.eps, b_offset=b, **pack_kw, **rope_kw)
+                            pend.append(ex.heads([b]))
                         for p_ in pend:
                             p_.wait()
-                    else:
+                    else:  # one exchange per direction for all rows
                         ops.linear(ws.mod, L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv)
-                        ops.qk_rmsnorm_rope(ws.qkv, 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
-                    if SP:  # Ulysses: tokens -> heads, full-sequence attention, heads -> tokens
-                        if not sp_rows_x:
-                            q_sp, kv_sp = exch.to_heads(ws.qkv, B, Lc, self.d)
-                        args_ = (q_sp, kv_sp[:, :hg * self.d], kv_sp[:, hg * self.d:], o_sp, segs_self, B, Lq, hg)
-                    else:
-                        args_ = (ws.qkv[:, :dim], ws.qkv[:, dim:2 * dim], ws.qkv[:, 2 * dim:], ws.att, segs_self, B, Lp,
-                                 H_)
+                        ops.qkv_pack(ws.qkv, L.nq, L.nk, dim, self.eps, **pack_kw, **rope_kw)
+                        ex.heads(range(B)).wait()
+                    # Ulysses: full-sequence attention of this rank's (query part, head group), outputs written
+                    # to the owners' send slabs / this rank's own O-projection panel, then heads -> tokens
                     ev0 = self._record_event()
-                    ops.attention(*args_, kernel=self.attn_kernel)
+                    ops.attention(ex.q, ex.kv[:, :hgd], ex.kv[:, hgd:], ex.obuf, segs_self, B, Lq, hg,
+                                  kernel=self.attn_kernel, o_rows=ex.omap)
                     self._record_span(ev0, rows=B, batch=B)
-                    if SP:
-                        exch.to_tokens(o_sp, B, Lc, self.d, ws.att)
+                    ex.tokens(range(B)).wait()
+                    a0, pnl = ex.panels()
+                    ops.linear(a0, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2],
+                               rows_per_batch=Lc, a_panels=pnl)
+                else:
+                    ops.linear(ws.mod, L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv)
+                    ops.qk_rmsnorm_rope(ws.qkv, 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
+                    ev0 = self._record_event()
+                    ops.attention(ws.qkv[:, :dim], ws.qkv[:, dim:2 * dim], ws.qkv[:, 2 * dim:], ws.att, segs_self, B,
+                                  Lp, H_, kernel=self.attn_kernel)
+                    self._record_span(ev0, rows=B, batch=B)
                     ops.linear(ws.att, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2],
                                rows_per_batch=Lc)
                 # cross-attention: text + image + per-frame vocal (1B:534-605, 684)

@@ -72,6 +72,7 @@ def _worker(rank, world, port, model, qret):
         for name, inp, gold in cases:
             m.disable_multi_gpus_inference()
             single = run(m, inp)
+            es_gold, _ = _stats(single, gold)
             m.enable_multi_gpus_inference()
             # one batched exchange / per-row exchanges + per-row attention / per-row Q/K/V exchanges + batched attention
             for ov in ("0", "2", "3"):
@@ -80,7 +81,7 @@ def _worker(rank, world, port, model, qret):
                 e_single = ((par - single).norm() / single.norm()).item()
                 e_gold, c_gold = _stats(par, gold)
                 res.append((name, ov, e_single, e_gold, c_gold, bool(torch.isfinite(par).all()),
-                            tuple(par.shape) == tuple(gold.shape)))
+                            tuple(par.shape) == tuple(gold.shape), es_gold))
         qret.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -100,11 +101,12 @@ def test_sp_matches_reference_golden(world, model):
         p.join(timeout=120)
         assert p.exitcode == 0
     for rank, rows in res:
-        for name, ov, e_single, e_gold, c_gold, finite, shape_ok in rows:
+        for name, ov, e_single, e_gold, c_gold, finite, shape_ok, es_gold in rows:
             print(f"world {world} {model} rank {rank} {name} overlap {ov}: vs golden rel {e_gold:.2e} cos "
-                  f"{c_gold:.6f}, vs single-GPU {e_single:.1e}")
+                  f"{c_gold:.6f}, vs single-GPU {e_single:.1e} (single-GPU vs golden {es_gold:.2e})")
             assert finite and shape_ok, (rank, name)
             assert e_gold < 2e-2 and c_gold > 0.9995, (rank, name, ov, e_gold, c_gold)
+            assert es_gold < 2e-2, (rank, name, es_gold)
             assert e_single < 1e-3, (rank, name, ov, e_single)
 
 
