@@ -1,0 +1,34 @@
+"""One RCCL rank with the sequence-parallel path on (argv[1] == "sp") or off ("single"): two DiT forwards of
+the small golden model, for a rocprofv3 kernel trace of each mode -- the SP run must add no copy kernels
+(the exchange is pack / row-mapped attention / column-panel O-projection only).
+usage: rocprofv3 --kernel-trace --stats -d <dir> -o run -- python scripts/sp_trace.py sp|single"""
+import os
+import socket
+import sys
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+from test_gpu_dit import make_model, run  # noqa: E402
+from golden_cases import DIT_SMALL, dit_inputs  # noqa: E402
+
+s = socket.socket()
+s.bind(("127.0.0.1", 0))
+port = s.getsockname()[1]
+s.close()
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                        device_id=torch.device("cuda:0"))
+try:
+    m = make_model(DIT_SMALL)
+    if sys.argv[1] == "sp":
+        m.enable_multi_gpus_inference()
+    inp = dit_inputs(DIT_SMALL, "full")
+    outs = [run(m, inp) for _ in range(2)]
+    print(sys.argv[1], "sp_enabled", m._sp_enabled, "checksum", outs[1].double().abs().sum().item())
+finally:
+    dist.destroy_process_group()
