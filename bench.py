@@ -480,7 +480,7 @@ def attn_traffic(seq_len, layout):
         return None, None
     with open(tpath) as f:
         tj = json.load(f)
-    if not tj.get("kernel", "").startswith(ATTN_KERNEL_NAME):
+    if ATTN_KERNEL_NAME not in tj.get("kernel", ""):
         return None, None
     return tj["hbm_bytes_per_launch"], f"profiles/pmc_attn_traffic.json ({tj.get('source', 'rocprofv3 --pmc')})"
 
