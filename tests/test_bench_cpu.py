@@ -163,4 +163,10 @@ def test_bench_cpu_baseline_deadline(tmp_path):
     r = cb.result(n_fwd=50, out_frames=81, size=512)
     assert r["cores"] == 3 and abs(r["value"] - 81 / (50 * 30 * 1.0 + 81 * 0.5)) < 1e-5
     assert r["config_1"]["skipped"] == "not finished within the time budget" and r["config_1"]["steps_done"] == 1
+    # with the (first-timed) config-1 decode in, k measured steps give a partial, extrapolated config-1 number
+    with open(cb.path, "a") as f:
+        f.write(json.dumps({"leg": "config1_decode", "s": 3.0, "frames": 21}) + "\n")
+        f.write(json.dumps({"leg": "config1_step", "i": 1, "s": 4.2, "dit_forwards": 4}) + "\n")
+    c1 = cb.result(n_fwd=50, out_frames=81, size=512)["config_1"]
+    assert c1["steps_run"] == 2 and abs(c1["value"] - 21 / (5 * 2.1 + 3.0)) < 1e-4 and "2 of 5" in c1["partial"]
     cb.cleanup()
