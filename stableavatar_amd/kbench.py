@@ -196,6 +196,9 @@ def main(which=("gemm", "attn")):
     if "dit14" in which:
         res.append(bench_dit14())
         print(json.dumps(res[-1]), flush=True)
+    if "dit14full" in which:  # BASELINE config 4's model: one whole 40-layer forward at 720p x 81 frames
+        res.append(bench_dit14(layer_counts=(40,)))
+        print(json.dumps(res[-1]), flush=True)
     if "ditvar" in which:  # in-situ A/B of attention variants inside full DiT forwards (interleaved)
         import os
         avars = tuple(int(v) for v in os.environ.get("SA_KB_AVARS", "1").split(","))
@@ -228,10 +231,16 @@ def bench_dit14(layer_counts=(1, 2)):
         m = WanTransformer3DFantasy14BModel(**cfg, num_layers=nl).to(dev)
         m.load_state_dict(synthetic.fill_state_dict(param_shapes(dict(cfg, num_layers=nl, vocal="14B")), 0,
                                                     backend="torch", device=dev))
+        print(f"[kbench] dit14: {nl}-layer model loaded, timing", file=sys.stderr, flush=True)
         with torch.no_grad():
             ms[nl] = _time(lambda: m.forward_window(lat, 0, True, 3, t, ctx, L, clip, y, voc, 81), iters=2, warmup=1)
         del m
         torch.cuda.empty_cache()
+    if tuple(layer_counts) == (40,):  # the whole 40-layer forward, measured
+        fl_fwd = dit_forward_flops(B=3, L=L, dim=5120, ffn=13824, layers=40)
+        return {"kernel": "dit14_forward_720p_40_layers", "L": L, "ms_forward": round(ms[40], 0),
+                "tflop_per_forward": round(fl_fwd / 1e12, 0), "tflops": round(fl_fwd / ms[40] / 1e9, 1),
+                "clip_s_projected_50_steps": round(50 * ms[40] / 1e3, 0)}
     per_layer = ms[2] - ms[1]
     fl_layer = dit_forward_flops(B=3, L=L, dim=5120, ffn=13824, layers=1) - dit_forward_flops(
         B=3, L=L, dim=5120, ffn=13824, layers=0)
