@@ -201,7 +201,9 @@ class WanI2VTalkingInferenceLongPipeline:
         wins = window_schedule(T, fpb, overlap)
         wts = overlap_weights(overlap, scheme).to(dev) if overlap and overlap > 1 else None
         cfg = y.shape[0] == 3
-        lat = latents.to(torch.bfloat16).contiguous()
+        # a copy: the two ping-pong buffers are written in turn, and the caller's noise tensor must survive the
+        # call (the reference's scheduler.step returns new tensors, :754)
+        lat = latents.to(torch.bfloat16, copy=True).contiguous()
         pred = torch.empty_like(lat)
         yb = y.to(device=dev, dtype=torch.bfloat16).contiguous()
         sig = [float(s) for s in sigmas]

@@ -125,13 +125,16 @@ def test_pipeline_vs_reference(scheme):
         feats[(s, e)] = torch.cat([torch.zeros_like(a), a, a])
     ctx = [fx["neg_embeds"].cuda(), fx["neg_embeds"].cuda(), fx["pos_embeds"].cuda()]
     seq_len = math.ceil(P["width"] // 8 * P["height"] // 8 / 4 * fpb)
+    noise = fx["latents"].cuda().bfloat16()  # bf16 already: denoise must still leave the caller's tensor alone
+    keep = noise.clone()
     with torch.no_grad():
-        lat = pipe.denoise(fx["latents"].cuda(), torch.from_numpy(g["y"]).cuda(), ctx,
+        lat = pipe.denoise(noise, torch.from_numpy(g["y"]).cuda(), ctx,
                            torch.cat([fx["clip"]] * 3).cuda(), feats, sched.timesteps, sched.sigmas,
                            clip_length=P["clip_length"], seq_len=seq_len, overlap=P["overlap"],
                            text_guide_scale=P["text_guide"], audio_guide_scale=P["audio_guide"], scheme=scheme)
         video = vae.decode_clip(lat[0].float(), post=True)[None]
     torch.cuda.synchronize()
+    assert torch.equal(noise, keep), "denoise overwrote its input latents"
     assert rel(lat.float(), g["latents"]) < 3e-2, rel(lat.float(), g["latents"])
     assert psnr(video, g["video"], 1.0) > 30.0, psnr(video, g["video"], 1.0)
 
