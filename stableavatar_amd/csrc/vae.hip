@@ -14,6 +14,8 @@
 //  sa_transpose_bf16   : batched 2-D transpose (V -> V^T for the P·V GEMM)
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 struct ConvArgs {
@@ -40,7 +42,7 @@ constexpr int BM = 128, BK = 32;
 __device__ __forceinline__ int swz64(int r, int c) { return r * 64 + ((c ^ ((r >> 1) & 3)) << 4); }
 
 template <int NT>
-__global__ __launch_bounds__(256) void conv3d_cl_kernel(ConvArgs a) {
+__global__ __launch_bounds__(256, 2) void conv3d_cl_kernel(ConvArgs a) {
   constexpr int BN = NT * 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int SBYTES = BM * 64 + BN * 64;  // one stage: A tile then B tile
@@ -71,7 +73,15 @@ __global__ __launch_bounds__(256) void conv3d_cl_kernel(ConvArgs a) {
   constexpr int BCH = BN * 4;  // 16-B chunks of the B tile
   constexpr int BPT = (BCH + 255) / 256;
 
-  u32x4 ra[2], rb[BPT];
+#ifndef SA_CONV_DEPTH
+#define SA_CONV_DEPTH 2
+#endif
+  // register staging ring: the loads of step ks + 1 are in flight while step ks is stored and multiplied,
+  // so a step's loads have a whole step of MFMAs behind them before their LDS write (depth 2, with
+  // __launch_bounds__(256, 2) holding the 192-wide tile at 202 VGPRs: decode 283.0 vs 288.4 ms,
+  // bit-identical, profiles/r03/README.md r3y)
+  constexpr int NS = SA_CONV_DEPTH;
+  u32x4 ra[NS][2], rb[NS][BPT];
   // The K loop walks (tap, channel chunk) in order; the A-row source pointers are recomputed only
   // when the tap changes (every Cin/BK steps) and the chunk offset advances in between, so the
   // im2col index arithmetic is off the per-step path (Cin % BK == 0 is checked by the launcher).
@@ -112,17 +122,17 @@ __global__ __launch_bounds__(256) void conv3d_cl_kernel(ConvArgs a) {
       }
     }
   };
-  auto load = [&]() {  // loads step (ld_tap, ld_ci) and advances to the next one
+  auto load = [&](int s) {  // loads step (ld_tap, ld_ci) into ring slot s and advances to the next one
     if (ld_ci == 0) set_tap(ld_tap);
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      ra[j] = asrc[j] ? *(const u32x4*)(asrc[j] + ld_ci) : (u32x4){0u, 0u, 0u, 0u};
+      ra[s][j] = asrc[j] ? *(const u32x4*)(asrc[j] + ld_ci) : (u32x4){0u, 0u, 0u, 0u};
 #pragma unroll
     for (int j = 0; j < BPT; ++j) {
       const int idx = tid + j * 256;
       if (idx < BCH) {
         const int r = idx >> 2, c = idx & 3;
-        rb[j] = *(const u32x4*)(a.w + (long)(n0 + r) * K + ld_k0 + c * 8);
+        rb[s][j] = *(const u32x4*)(a.w + (long)(n0 + r) * K + ld_k0 + c * 8);
       }
     }
     ld_k0 += BK;
@@ -132,13 +142,13 @@ __global__ __launch_bounds__(256) void conv3d_cl_kernel(ConvArgs a) {
       ++ld_tap;
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, int s) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) *(u32x4*)(smem + buf * SBYTES + swz64(ar[j], ac[j])) = ra[j];
+    for (int j = 0; j < 2; ++j) *(u32x4*)(smem + buf * SBYTES + swz64(ar[j], ac[j])) = ra[s][j];
 #pragma unroll
     for (int j = 0; j < BPT; ++j) {
       const int idx = tid + j * 256;
-      if (idx < BCH) *(u32x4*)(smem + buf * SBYTES + BM * 64 + swz64(idx >> 2, idx & 3)) = rb[j];
+      if (idx < BCH) *(u32x4*)(smem + buf * SBYTES + BM * 64 + swz64(idx >> 2, idx & 3)) = rb[s][j];
     }
   };
 
@@ -153,11 +163,12 @@ __global__ __launch_bounds__(256) void conv3d_cl_kernel(ConvArgs a) {
 #pragma unroll
     for (int n = 0; n < NB; ++n) acc[i][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  load();
-  for (int ks = 0; ks < nk; ++ks) {
+  // one K step: store slot S of step ks, refill it with step ks + NS, barrier, MFMAs
+  auto kstep = [&](int ks, auto sc) {
+    constexpr int S = decltype(sc)::value;
     const int buf = ks & 1;
-    store(buf);
-    if (ks + 1 < nk) load();  // issued before the barrier: the wait at the barrier hides part of its latency
+    store(buf, S);
+    if (ks + NS < nk) load(S);  // issued before the barrier: the wait at the barrier hides part of its latency
     __syncthreads();
     const int c = lane >> 4;
     bf16x8 af[AI];
@@ -170,6 +181,20 @@ __global__ __launch_bounds__(256) void conv3d_cl_kernel(ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < AI; ++i) acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][n], 0, 0, 0);
     }
+  };
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (s < nk) load(s);
+  if constexpr (NS == 1) {
+    for (int ks = 0; ks < nk; ++ks) kstep(ks, std::integral_constant<int, 0>{});
+  } else {
+    static_assert(NS == 2, "register ring depth 1 or 2");
+    int ks = 0;
+    for (; ks + 1 < nk; ks += 2) {
+      kstep(ks, std::integral_constant<int, 0>{});
+      kstep(ks + 1, std::integral_constant<int, 1>{});
+    }
+    if (ks < nk) kstep(ks, std::integral_constant<int, 0>{});
   }
   __syncthreads();
 
