@@ -37,8 +37,9 @@ int sa_gemm_bf16(const void* A, int64_t lda, int64_t strideA, const void* W, int
                  int64_t gate_bstride, int rows_per_batch, void* stream);
 
 /* sa_gemm_bf16 with the kernel chosen per call (re-entrant A/B; no process-wide state):
- * kernel 0 = auto (the persistent one-wave-per-SIMD kernel where K % 128 == 0, else the 8-wave
- * ping-pong), 1 = ping-pong, 2 = persistent (rejected with 1 when K % 128 != 0);
+ * kernel 0 = auto (the persistent one-wave-per-SIMD kernel where K % 128 == 0 -- 256- or 192-row tiles,
+ * whichever takes fewer rounds over the CUs -- else the 8-wave ping-pong), 1 = ping-pong, 2 = persistent
+ * 256-row tiles, 3 = persistent 192-row tiles (2 and 3 rejected with 1 when K % 128 != 0);
  * group_m = tile-raster run length (0 = per-kernel default, or env SA_GEMM_GROUP_M read once). */
 int sa_gemm_bf16_ex(const void* A, int64_t lda, int64_t strideA, const void* W, int64_t ldw, int64_t strideW,
                     const float* bias, void* C, int64_t ldc, int64_t strideC, int M, int N, int K, int batch,

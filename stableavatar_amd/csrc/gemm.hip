@@ -49,6 +49,10 @@ __device__ __forceinline__ void tile_coords(int wg, int nm, int nn, int gm, int&
 }
 
 constexpr int BM = 256, BN = 256, BK = 64;
+// per-FLOP cost of the 192-row persistent tile relative to the 256-row one (auto tile choice; measured r3t2)
+#ifndef SA_T192_COST
+#define SA_T192_COST 1.06  // QKV 1.025, O-proj 1.087, cross-Q 1.05, FFN-up 1.023, FFN-down 1.095 at M = 64 512
+#endif
 constexpr int HALF_BYTES = 128 * BK * 2;        // 16 KB
 constexpr int STAGE_BYTES = 4 * HALF_BYTES;     // 64 KB: A0 A1 B0 B1
 constexpr int LDS_BYTES = 2 * STAGE_BYTES;      // 128 KB
@@ -409,9 +413,13 @@ __device__ __forceinline__ void s4_ds(u32x4& d, uint32_t addr) {
 __device__ __forceinline__ void s4_mma(f32x4& c, const u32x4& w, const u32x4& x) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(w), "v"(x) : "memory");
 }
+template <int MI = 8>
 __device__ __forceinline__ void s4_wait_frags(u32x4 (&a)[8], u32x4 (&b)[8]) {
-  asm volatile("s_waitcnt lgkmcnt(0)"
-               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]));
+  if constexpr (MI == 8)
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]));
+  else
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]));
   asm volatile("" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]), "+v"(b[6]), "+v"(b[7]));
 }
 
@@ -430,56 +438,64 @@ struct S5Ctx {
   uint32_t ard[2][2], wrd[2][2];  // [stage][k half] per-lane fragment read bases
 };
 
-template <int STAGE, int PIECE>
+// MI = A fragments (16-row groups) per wave: 8 for the 256-row tile, 6 for the 192-row one (the A region of a
+// stage keeps its 256-row size; a 192-row tile uses the first 24 KB of it).  Pieces 0..MI-1 are A, then 8 of W
+template <int STAGE, int PIECE, int MI = 8>
 __device__ __forceinline__ void s5_dma(const S5Ctx& c, int ks, int ksa) {
-  constexpr int i = PIECE & 7;
-  if constexpr (PIECE < 8)
+  if constexpr (PIECE < MI) {
+    constexpr int i = PIECE;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(c.ra, LDS_PTR((uintptr_t)(c.lds_dma + STAGE * S5_STAGE + i * 4096)), 16,
                                              c.aoff[i], ksa, 0, 0);
-  else
+  } else {
+    constexpr int i = PIECE - MI;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
         c.rw, LDS_PTR((uintptr_t)(c.lds_dma + STAGE * S5_STAGE + 256 * 128 + i * 4096)), 16, c.woff[i], ks, 0, 0);
+  }
 }
 
-template <int STAGE, int KH, int R>
+template <int STAGE, int KH, int R, int MI = 8>
 __device__ __forceinline__ void s5_read(const S5Ctx& c, u32x4 (&a)[8], u32x4 (&b)[8]) {
-  if constexpr (R < 8)
-    s4_ds<(R & 7) * 2048>(a[R], c.ard[STAGE][KH]);
-  else
-    s4_ds<(R & 7) * 2048>(b[R & 7], c.wrd[STAGE][KH]);
+  if constexpr (R < MI)
+    s4_ds<R * 2048>(a[R], c.ard[STAGE][KH]);
+  else if constexpr (R < MI + 8)
+    s4_ds<(R - MI) * 2048>(b[R - MI], c.wrd[STAGE][KH]);
 }
 
 // one 64-MFMA half: MFMA row Q uses (ac[Q], bc[0..7]); the first 4 rows carry the reads of the
 // next fragments (stage RS, k half RK) and, when DMA, 4 DMA pieces each of tile ks into stage DS
 // DMA piece placement inside a half: packed (4 per MFMA row in rows 0-3) or SPREAD (2 per row, all 8)
-template <int DS, int Q, int POS, bool DMA, bool SPREAD>
+// (MI = 6: the 14 pieces as 2 per MFMA row plus one more in rows 0-1)
+template <int DS, int Q, int POS, bool DMA, bool SPREAD, int MI = 8>
 __device__ __forceinline__ void s5_dma_at(const S5Ctx& c, int ks, int ksa) {
   if constexpr (DMA) {
     if constexpr (SPREAD) {
-      if constexpr (POS & 1) s5_dma<DS, 2 * Q + (POS >> 1)>(c, ks, ksa);
+      if constexpr (POS & 1)
+        s5_dma<DS, 2 * Q + (POS >> 1), MI>(c, ks, ksa);
+      else if constexpr (POS == 2 && Q < 8 - MI)
+        s5_dma<DS, 2 * MI + Q, MI>(c, ks, ksa);
     } else if constexpr (Q < 4) {
-      s5_dma<DS, 4 * Q + POS>(c, ks, ksa);
+      s5_dma<DS, 4 * Q + POS, MI>(c, ks, ksa);
     }
   }
 }
 
-template <int RS, int RK, bool DMA, int DS, bool SPREAD = false>
+template <int RS, int RK, bool DMA, int DS, bool SPREAD = false, int MI = 8>
 __device__ __forceinline__ void s5_half(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&ac)[8], u32x4 (&bc)[8],
                                         u32x4 (&an)[8], u32x4 (&bn)[8], int ks, int ksa) {
 #define SA_S5_ROW(Q)                                                                        \
-  {                                                                                         \
+  if constexpr (Q < MI) {                                                                   \
     s4_mma(acc[Q][0], bc[0], ac[Q]); s4_mma(acc[Q][1], bc[1], ac[Q]);                       \
-    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q>(c, an, bn); }                             \
-    s5_dma_at<DS, Q, 0, DMA, SPREAD>(c, ks, ksa);                               \
+    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q, MI>(c, an, bn); }                         \
+    s5_dma_at<DS, Q, 0, DMA, SPREAD, MI>(c, ks, ksa);                                       \
     s4_mma(acc[Q][2], bc[2], ac[Q]); s4_mma(acc[Q][3], bc[3], ac[Q]);                       \
-    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 1>(c, an, bn); }                         \
-    s5_dma_at<DS, Q, 1, DMA, SPREAD>(c, ks, ksa);                           \
+    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 1, MI>(c, an, bn); }                     \
+    s5_dma_at<DS, Q, 1, DMA, SPREAD, MI>(c, ks, ksa);                                       \
     s4_mma(acc[Q][4], bc[4], ac[Q]); s4_mma(acc[Q][5], bc[5], ac[Q]);                       \
-    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 2>(c, an, bn); }                         \
-    s5_dma_at<DS, Q, 2, DMA, SPREAD>(c, ks, ksa);                           \
+    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 2, MI>(c, an, bn); }                     \
+    s5_dma_at<DS, Q, 2, DMA, SPREAD, MI>(c, ks, ksa);                                       \
     s4_mma(acc[Q][6], bc[6], ac[Q]); s4_mma(acc[Q][7], bc[7], ac[Q]);                       \
-    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 3>(c, an, bn); }                         \
-    s5_dma_at<DS, Q, 3, DMA, SPREAD>(c, ks, ksa);                           \
+    if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 3, MI>(c, an, bn); }                     \
+    s5_dma_at<DS, Q, 3, DMA, SPREAD, MI>(c, ks, ksa);                                       \
   }
   SA_S5_ROW(0) SA_S5_ROW(1) SA_S5_ROW(2) SA_S5_ROW(3) SA_S5_ROW(4) SA_S5_ROW(5) SA_S5_ROW(6) SA_S5_ROW(7)
 #undef SA_S5_ROW
@@ -501,14 +517,14 @@ constexpr int S7_LDS = S5_LDS + 4 * S7_STRIP;     // 145 KB
 // box, interleaved, profiles/r02/gemm_epilogue_study.md): O-proj 0.440 vs 0.447 ms, FFN-down 1.474 vs
 // 1.486 ms, 30-layer DiT forward 396.7 vs 398.7 ms; for bf16 outputs the strip path's 16-byte row
 // segments stay faster (QKV 0.80 vs 0.94 ms), so those keep it.
-template <int EPI, bool TILE_GATE>
+template <int EPI, bool TILE_GATE, int MI = 8>
 __device__ __forceinline__ void s7_f32_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8], int wm, int wn, int fr, int fc,
                                                 int m0, int n0, long bz) {
   constexpr bool RES = EPI == EPI_RES_F32;
   constexpr bool PER_ROW_GATE = RES && !TILE_GATE;
   constexpr int AH = RES ? (PER_ROW_GATE ? 4 : 8) : 1;
   const int col = n0 + wn * 128 + fc * 4;  // + j * 16
-  const int row0 = m0 + wm * 128 + fr;     // + i * 16
+  const int row0 = m0 + wm * 16 * MI + fr;  // + i * 16
   const float* tgate = (TILE_GATE && RES && g.gate) ? g.gate + (long)(m0 / g.rows_per_batch) * g.gate_bstride : nullptr;
   f32x4 bj[3], gj[3], rb[AH], gb[PER_ROW_GATE ? AH : 1];
   auto fetch_col = [&](int j) {
@@ -516,7 +532,7 @@ __device__ __forceinline__ void s7_f32_epilogue(const GemmArgs& g, f32x4 (&acc)[
     if constexpr (RES && TILE_GATE) gj[j % 3] = tgate ? *(const f32x4*)(tgate + col + j * 16) : (f32x4){1.f, 1.f, 1.f, 1.f};
   };
   auto fetch = [&](int st) {
-    const int i = st & 7, j = st >> 3;
+    const int i = st % MI, j = st / MI;
     if constexpr (RES) rb[st % AH] = *(const f32x4*)(g.R + bz * g.sR + (long)(row0 + i * 16) * g.ldr + col + j * 16);
     if constexpr (PER_ROW_GATE)
       gb[st % AH] = *(const f32x4*)(g.gate + (long)((row0 + i * 16) / g.rows_per_batch) * g.gate_bstride + col + j * 16);
@@ -532,11 +548,15 @@ __device__ __forceinline__ void s7_f32_epilogue(const GemmArgs& g, f32x4 (&acc)[
     if (j + 2 < 8) fetch_col(j + 2);
     // one column group at a time: its accumulators are read from the AGPRs only here (keeps the
     // compiler from hoisting all 256 reads into VGPRs) and no store crosses this point
-    asm volatile("" : "+a"(acc[0][j]), "+a"(acc[1][j]), "+a"(acc[2][j]), "+a"(acc[3][j]), "+a"(acc[4][j]),
-                      "+a"(acc[5][j]), "+a"(acc[6][j]), "+a"(acc[7][j])::"memory");
+    if constexpr (MI == 8)
+      asm volatile("" : "+a"(acc[0][j]), "+a"(acc[1][j]), "+a"(acc[2][j]), "+a"(acc[3][j]), "+a"(acc[4][j]),
+                        "+a"(acc[5][j]), "+a"(acc[6][j]), "+a"(acc[7][j])::"memory");
+    else
+      asm volatile("" : "+a"(acc[0][j]), "+a"(acc[1][j]), "+a"(acc[2][j]), "+a"(acc[3][j]), "+a"(acc[4][j]),
+                        "+a"(acc[5][j])::"memory");
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int st = j * 8 + i;
+    for (int i = 0; i < MI; ++i) {
+      const int st = j * MI + i;
       f32x4 v = acc[i][j];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -550,24 +570,25 @@ __device__ __forceinline__ void s7_f32_epilogue(const GemmArgs& g, f32x4 (&acc)[
       }
       *(f32x4*)((float*)g.C + bz * g.sC + (long)(row0 + i * 16) * g.ldc + col + j * 16) = v;
       if constexpr (RES) {
-        if (st + AH < 64) fetch(st + AH);
+        if (st + AH < 8 * MI) fetch(st + AH);
       }
     }
   }
 }
 
-template <int EPI>
+template <int EPI, int MI = 8>
 __device__ __forceinline__ void s7_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8], char* smem, int wave, int lane,
                                             int m0, int n0, long bz) {
+  constexpr int BMT = 32 * MI;  // tile rows
   const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fc = lane >> 4;
   float* strip = (float*)(smem + S5_LDS + wave * S7_STRIP);
   const int er = lane >> 2, ec = (lane & 3) * 16;
   if constexpr (EPI == EPI_RES_F32 || EPI == EPI_F32 || EPI == EPI_SILU_F32) {
-    if (m0 + BM <= g.M && n0 + BN <= g.N) {  // interior tile (wave-uniform)
-      if (EPI != EPI_RES_F32 || !g.gate || m0 / g.rows_per_batch == (m0 + BM - 1) / g.rows_per_batch)
-        s7_f32_epilogue<EPI, true>(g, acc, wm, wn, fr, fc, m0, n0, bz);
+    if (m0 + BMT <= g.M && n0 + BN <= g.N) {  // interior tile (wave-uniform)
+      if (EPI != EPI_RES_F32 || !g.gate || m0 / g.rows_per_batch == (m0 + BMT - 1) / g.rows_per_batch)
+        s7_f32_epilogue<EPI, true, MI>(g, acc, wm, wn, fr, fc, m0, n0, bz);
       else
-        s7_f32_epilogue<EPI, false>(g, acc, wm, wn, fr, fc, m0, n0, bz);
+        s7_f32_epilogue<EPI, false, MI>(g, acc, wm, wn, fr, fc, m0, n0, bz);
       return;
     }
   }
@@ -603,8 +624,8 @@ __device__ __forceinline__ void s7_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8
   asm volatile("" ::"v"(bias4[0][0]), "v"(bias4[0][1]), "v"(bias4[0][2]), "v"(bias4[0][3]), "v"(bias4[1][0]),
                "v"(bias4[1][1]), "v"(bias4[1][2]), "v"(bias4[1][3]));
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int grow = m0 + wm * 128 + i * 16 + er;
+  for (int i = 0; i < MI; ++i) {
+    const int grow = m0 + wm * 16 * MI + i * 16 + er;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -629,8 +650,10 @@ __device__ __forceinline__ void s7_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8
   }
 }
 
+template <int MI = 8>
 __device__ __forceinline__ void s7_tile(const GemmArgs& g, int u, int total, int G, int nm, int nn, int& m0, int& n0,
                                         long& bz, __amdgpu_buffer_rsrc_t& ra, __amdgpu_buffer_rsrc_t& rw) {
+  constexpr int BMT = 32 * MI;
   // rounds of G tiles; within a round the XCD remap hands each XCD a contiguous run of tile ids
   const int per = nm * nn;
   const int round = u / G;
@@ -639,9 +662,9 @@ __device__ __forceinline__ void s7_tile(const GemmArgs& g, int u, int total, int
   bz = w / per;
   int mt, nt;
   tile_coords(w - (int)bz * per, nm, nn, g.group_m, mt, nt);
-  m0 = mt * BM;
+  m0 = mt * BMT;
   n0 = nt * BN;
-  const int rows_a = min(BM, g.M - m0), rows_w = min(BN, g.N - n0);
+  const int rows_a = min(BMT, g.M - m0), rows_w = min(BN, g.N - n0);
   ra = __builtin_amdgcn_make_buffer_rsrc((void*)(g.A + bz * g.sA + (long)m0 * g.lda), (short)0,
                                          (int)(rows_a * g.lda * 2) + g.a_pextra, 0x00020000);
   rw = __builtin_amdgcn_make_buffer_rsrc((void*)(g.W + bz * g.sW + (long)n0 * g.ldw), (short)0,
@@ -660,30 +683,34 @@ __device__ __forceinline__ int s8_ksa(const GemmArgs& g, int ks) {
   return ks;
 }
 
-template <int S, bool PANEL>
+template <int S, bool PANEL, int MI = 8>
 __device__ __forceinline__ void s8_step(const GemmArgs& g, const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8],
                                         u32x4 (&b0)[8], u32x4 (&a1)[8], u32x4 (&b1)[8], int ks) {
-  s4_wait_frags(a0, b0);
-  s5_half<S, 1, false, 0>(c, acc, a0, b0, a1, b1, 0, 0);
+  s4_wait_frags<MI>(a0, b0);
+  s5_half<S, 1, false, 0, false, MI>(c, acc, a0, b0, a1, b1, 0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  s4_wait_frags(a1, b1);
+  s4_wait_frags<MI>(a1, b1);
   __builtin_amdgcn_s_barrier();
-  s5_half<S ^ 1, 0, true, S, true>(c, acc, a1, b1, a0, b0, ks, s8_ksa<PANEL>(g, ks));
+  s5_half<S ^ 1, 0, true, S, true, MI>(c, acc, a1, b1, a0, b0, ks, s8_ksa<PANEL>(g, ks));
 }
 
-template <int EPI, bool PANEL = false>
+// MI = 6: 192 x 256 tiles (4 waves x 96 x 128), for launches whose 256-row tile count leaves the last round over
+// the CUs mostly empty (the per-rank GEMMs of sequence parallelism: 8 064 rows at N = 8 fill 0.74 of a round of
+// 256 x 256 tiles, 0.98 of a round of 192 x 256)
+template <int EPI, bool PANEL = false, int MI = 8>
 __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) {
+  constexpr int BMT = 32 * MI;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
+  const int nm = (g.M + BMT - 1) / BMT, nn = (g.N + BN - 1) / BN;
   const int total = nm * nn * batch, G = gridDim.x;
   int u = blockIdx.x;
   S5Ctx c;
   int m0, n0;
   long bz;
-  s7_tile(g, u, total, G, nm, nn, m0, n0, bz, c.ra, c.rw);
+  s7_tile<MI>(g, u, total, G, nm, nn, m0, n0, bz, c.ra, c.rw);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int row = (i * 4 + wave) * 8 + (lane >> 3);
@@ -699,7 +726,7 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh) {
       const int sw = ((4 * kh + fc) ^ ((fr >> 1) & 7)) << 4;
-      c.ard[st][kh] = lds0 + st * S5_STAGE + (wm * 128 + fr) * 128 + sw;
+      c.ard[st][kh] = lds0 + st * S5_STAGE + (wm * 16 * MI + fr) * 128 + sw;
       c.wrd[st][kh] = lds0 + st * S5_STAGE + 256 * 128 + (wn * 128 + fr) * 128 + sw;
     }
   const int nk = g.K / 64;  // even (launcher: K % 128 == 0)
@@ -711,25 +738,33 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
     for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   u32x4 a0[8], b0[8], a1[8], b1[8];
+#define SA_S8_DMA(STAGE, P) \
+  if constexpr (P < MI + 8) s5_dma<STAGE, P, MI>(c, ks, ksa);
 #define SA_S8_DMA_ALL(STAGE, T)                                                                       \
   {                                                                                                   \
     const int ks = (T) * 128, ksa = s8_ksa<PANEL>(g, ks);                                                  \
-    s5_dma<STAGE, 0>(c, ks, ksa); s5_dma<STAGE, 1>(c, ks, ksa); s5_dma<STAGE, 2>(c, ks, ksa);             \
-    s5_dma<STAGE, 3>(c, ks, ksa); s5_dma<STAGE, 4>(c, ks, ksa); s5_dma<STAGE, 5>(c, ks, ksa);             \
-    s5_dma<STAGE, 6>(c, ks, ksa); s5_dma<STAGE, 7>(c, ks, ksa); s5_dma<STAGE, 8>(c, ks, ksa);             \
-    s5_dma<STAGE, 9>(c, ks, ksa); s5_dma<STAGE, 10>(c, ks, ksa); s5_dma<STAGE, 11>(c, ks, ksa);           \
-    s5_dma<STAGE, 12>(c, ks, ksa); s5_dma<STAGE, 13>(c, ks, ksa); s5_dma<STAGE, 14>(c, ks, ksa);          \
-    s5_dma<STAGE, 15>(c, ks, ksa);                                                                    \
+    SA_S8_DMA(STAGE, 0) SA_S8_DMA(STAGE, 1) SA_S8_DMA(STAGE, 2) SA_S8_DMA(STAGE, 3) SA_S8_DMA(STAGE, 4)   \
+    SA_S8_DMA(STAGE, 5) SA_S8_DMA(STAGE, 6) SA_S8_DMA(STAGE, 7) SA_S8_DMA(STAGE, 8) SA_S8_DMA(STAGE, 9)   \
+    SA_S8_DMA(STAGE, 10) SA_S8_DMA(STAGE, 11) SA_S8_DMA(STAGE, 12) SA_S8_DMA(STAGE, 13)                   \
+    SA_S8_DMA(STAGE, 14) SA_S8_DMA(STAGE, 15)                                                         \
   }
   SA_S8_DMA_ALL(0, 0)
   SA_S8_DMA_ALL(1, 1)
 #undef SA_S8_DMA_ALL
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+#undef SA_S8_DMA
+  // K-tile 0 landed; K-tile 1's MI + 8 pieces may still fly
+  if constexpr (MI == 8)
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+  static_assert(MI == 8 || MI == 6, "tile rows: 256 or 192");
   __builtin_amdgcn_s_barrier();
-  s5_read<0, 0, 0>(c, a0, b0); s5_read<0, 0, 1>(c, a0, b0); s5_read<0, 0, 2>(c, a0, b0); s5_read<0, 0, 3>(c, a0, b0);
-  s5_read<0, 0, 4>(c, a0, b0); s5_read<0, 0, 5>(c, a0, b0); s5_read<0, 0, 6>(c, a0, b0); s5_read<0, 0, 7>(c, a0, b0);
-  s5_read<0, 0, 8>(c, a0, b0); s5_read<0, 0, 9>(c, a0, b0); s5_read<0, 0, 10>(c, a0, b0); s5_read<0, 0, 11>(c, a0, b0);
-  s5_read<0, 0, 12>(c, a0, b0); s5_read<0, 0, 13>(c, a0, b0); s5_read<0, 0, 14>(c, a0, b0); s5_read<0, 0, 15>(c, a0, b0);
+  s5_read<0, 0, 0, MI>(c, a0, b0); s5_read<0, 0, 1, MI>(c, a0, b0); s5_read<0, 0, 2, MI>(c, a0, b0);
+  s5_read<0, 0, 3, MI>(c, a0, b0); s5_read<0, 0, 4, MI>(c, a0, b0); s5_read<0, 0, 5, MI>(c, a0, b0);
+  s5_read<0, 0, 6, MI>(c, a0, b0); s5_read<0, 0, 7, MI>(c, a0, b0); s5_read<0, 0, 8, MI>(c, a0, b0);
+  s5_read<0, 0, 9, MI>(c, a0, b0); s5_read<0, 0, 10, MI>(c, a0, b0); s5_read<0, 0, 11, MI>(c, a0, b0);
+  s5_read<0, 0, 12, MI>(c, a0, b0); s5_read<0, 0, 13, MI>(c, a0, b0); s5_read<0, 0, 14, MI>(c, a0, b0);
+  s5_read<0, 0, 15, MI>(c, a0, b0);
 
   while (true) {
     const int un = u + G;
@@ -737,23 +772,23 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
     __amdgpu_buffer_rsrc_t cra = c.ra, crw = c.rw, nra = c.ra, nrw = c.rw;
     int nm0 = m0, nn0 = n0;
     long nbz = bz;
-    if (has_next) s7_tile(g, un, total, G, nm, nn, nm0, nn0, nbz, nra, nrw);
+    if (has_next) s7_tile<MI>(g, un, total, G, nm, nn, nm0, nn0, nbz, nra, nrw);
     for (int t = 0; t < nk; t += 2) {
       {
         const bool nx = t + 2 >= nk;  // DMA of the next tile's K-tile t+2-nk (or a re-read of the last)
         c.ra = nx ? nra : cra;
         c.rw = nx ? nrw : crw;
-        s8_step<0, PANEL>(g, c, acc, a0, b0, a1, b1, (nx ? (has_next ? t + 2 - nk : nk - 1) : t + 2) * 128);
+        s8_step<0, PANEL, MI>(g, c, acc, a0, b0, a1, b1, (nx ? (has_next ? t + 2 - nk : nk - 1) : t + 2) * 128);
       }
       {
         const bool nx = t + 3 >= nk;
         c.ra = nx ? nra : cra;
         c.rw = nx ? nrw : crw;
-        s8_step<1, PANEL>(g, c, acc, a0, b0, a1, b1, (nx ? (has_next ? t + 3 - nk : nk - 1) : t + 3) * 128);
+        s8_step<1, PANEL, MI>(g, c, acc, a0, b0, a1, b1, (nx ? (has_next ? t + 3 - nk : nk - 1) : t + 3) * 128);
       }
     }
     asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // MFMA -> v_accvgpr_read
-    s7_epilogue<EPI>(g, acc, smem, wave, lane, m0, n0, bz);
+    s7_epilogue<EPI, MI>(g, acc, smem, wave, lane, m0, n0, bz);
     if (!has_next) break;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -769,7 +804,8 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 
-constexpr int KERNEL_AUTO = 0, KERNEL_PINGPONG = 1, KERNEL_PERSISTENT = 2;
+constexpr int KERNEL_AUTO = 0, KERNEL_PINGPONG = 1, KERNEL_PERSISTENT = 2, KERNEL_PERSISTENT192 = 3;
+constexpr int KERNEL_PERSISTENT_AUTO = 4;  // internal: the persistent kernel with the tile rows chosen as by auto
 
 int num_cus() {
   // per device: the persistent grid is one workgroup per CU
@@ -799,9 +835,14 @@ int launch(const GemmArgs& g_in, int batch, int kernel, hipStream_t st) {
   // one-time per epilogue instantiation: allow the dynamic LDS sizes (idempotent, thread-safe init)
   static const bool attr = [] {
     (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S7_LDS);
-    if constexpr (EPI == EPI_RES_F32)
+    (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI, false, 6>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              S7_LDS);
+    if constexpr (EPI == EPI_RES_F32) {
       (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 S7_LDS);
+      (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI, true, 6>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                S7_LDS);
+    }
     (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
     return true;
@@ -813,19 +854,33 @@ int launch(const GemmArgs& g_in, int batch, int kernel, hipStream_t st) {
   // cross-Q +7-10 %, FFN-up +3-4 %, FFN-down +4 %, O-proj +-1 %), else the ping-pong kernel (e.g. the
   // K = 192 patch embedding)
   const bool persistent_ok = g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL && (long)BN * g.ldw * 2 < 0x7fffffffL;
-  if (kernel == KERNEL_PERSISTENT && !persistent_ok) return SA_ERR_ARG;
-  const bool persistent = kernel == KERNEL_PERSISTENT || (kernel == KERNEL_AUTO && persistent_ok);
+  const bool forced = kernel == KERNEL_PERSISTENT || kernel == KERNEL_PERSISTENT192 || kernel == KERNEL_PERSISTENT_AUTO;
+  if (forced && !persistent_ok) return SA_ERR_ARG;
+  const bool persistent = forced || (kernel == KERNEL_AUTO && persistent_ok);
   constexpr bool BF16_OUT = EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16;
   if (g.group_m == 0) g.group_m = persistent ? (BF16_OUT ? 8 : 4) : (g.N >= 4096 ? 8 : 1);
-  const int nm = (g.M + BM - 1) / BM, nn = (g.N + BN - 1) / BN;
+  const int nn = (g.N + BN - 1) / BN, ncu = num_cus();
+  const long n256 = (long)((g.M + 255) / 256) * nn * batch, n192 = (long)((g.M + 191) / 192) * nn * batch;
+  // persistent tile rows: 192 where its rounds over the CUs, at 0.75 of a 256-row tile's work and a measured
+  // per-FLOP cost of SA_T192_COST, finish first (the per-rank shapes of sequence parallelism)
+  bool t192 = kernel == KERNEL_PERSISTENT192;
+  if ((kernel == KERNEL_AUTO || kernel == KERNEL_PERSISTENT_AUTO) && persistent)
+    t192 = (double)((n192 + ncu - 1) / ncu) * 0.75 * SA_T192_COST < (double)((n256 + ncu - 1) / ncu);
+  const int nm = t192 ? (g.M + 191) / 192 : (g.M + BM - 1) / BM;
+  const dim3 pgrid(min(nm * nn * batch, ncu));
   if (g.a_pmul) {  // column-panel A: the O-projection of the sequence-parallel path only
-    if constexpr (EPI == EPI_RES_F32)
-      hipLaunchKernelGGL((gemm_s8_kernel<EPI, true>), dim3(min(nm * nn * batch, num_cus())), dim3(256), S7_LDS, st, g,
-                         batch);
-    else
+    if constexpr (EPI == EPI_RES_F32) {
+      if (t192)
+        hipLaunchKernelGGL((gemm_s8_kernel<EPI, true, 6>), pgrid, dim3(256), S7_LDS, st, g, batch);
+      else
+        hipLaunchKernelGGL((gemm_s8_kernel<EPI, true>), pgrid, dim3(256), S7_LDS, st, g, batch);
+    } else {
       return SA_ERR_ARG;
-  } else if (persistent)
-    hipLaunchKernelGGL(gemm_s8_kernel<EPI>, dim3(min(nm * nn * batch, num_cus())), dim3(256), S7_LDS, st, g, batch);
+    }
+  } else if (persistent && t192)
+    hipLaunchKernelGGL((gemm_s8_kernel<EPI, false, 6>), pgrid, dim3(256), S7_LDS, st, g, batch);
+  else if (persistent)
+    hipLaunchKernelGGL(gemm_s8_kernel<EPI>, pgrid, dim3(256), S7_LDS, st, g, batch);
   else
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, true>), dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
   SA_LAUNCH_CHECK();
@@ -848,7 +903,7 @@ extern "C" int sa_gemm_bf16_panels(const void* A, int64_t lda, int64_t strideA, 
   if (K % BK != 0 || lda % 8 != 0 || ldw % 8 != 0) return SA_ERR_ARG;
   if ((((uintptr_t)A) & 15) || (((uintptr_t)W) & 15)) return SA_ERR_ARG;
   if (epilogue == EPI_RES_F32 && (!residual || (gate && rows_per_batch <= 0))) return SA_ERR_ARG;
-  if (kernel < KERNEL_AUTO || kernel > KERNEL_PERSISTENT || group_m < 0) return SA_ERR_ARG;
+  if (kernel < KERNEL_AUTO || kernel > KERNEL_PERSISTENT192 || group_m < 0) return SA_ERR_ARG;
   GemmArgs g{(const bf16*)A, lda, strideA, (const bf16*)W, ldw, strideW, bias, C, ldc, strideC,
              residual, ldr, strideR, gate, gate_bstride, rows_per_batch > 0 ? rows_per_batch : 1, M, N, K,
              group_m > 0 ? group_m : env_group_m(), 0u, 0, 0};
@@ -866,7 +921,7 @@ extern "C" int sa_gemm_bf16_panels(const void* A, int64_t lda, int64_t strideA, 
     g.a_pmul = pmul;
     g.a_pdelta = (int)delta;
     g.a_pextra = (int)extra;
-    kernel = KERNEL_PERSISTENT;
+    if (kernel == KERNEL_AUTO) kernel = KERNEL_PERSISTENT_AUTO;  // persistent, tile rows by the rounds model
   }
   hipStream_t st = (hipStream_t)stream;
   switch (epilogue) {

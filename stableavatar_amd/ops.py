@@ -35,7 +35,7 @@ def _check(t, dtype, name):
         raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
 
 
-GEMM_AUTO, GEMM_PINGPONG, GEMM_PERSISTENT = 0, 1, 2
+GEMM_AUTO, GEMM_PINGPONG, GEMM_PERSISTENT, GEMM_PERSISTENT192 = 0, 1, 2, 3
 
 
 def linear(x, weight, bias=None, epilogue=EPI_BF16, out=None, residual=None, gate=None, rows_per_batch=0,

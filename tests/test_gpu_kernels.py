@@ -50,7 +50,7 @@ def test_gemm_epilogues(M, N, K):
     assert rel(out, res + ref.bfloat16().float() * g_rows) < 2e-3
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 2], ids=["auto", "pingpong", "persistent"])
+@pytest.mark.parametrize("kernel", [0, 1, 2, 3], ids=["auto", "pingpong", "persistent", "persistent192"])
 @pytest.mark.parametrize("M,N,K", [(300, 520, 256), (257, 130, 128), (1000, 1536, 1536), (600, 300, 2304)])
 def test_gemm_kernels(kernel, M, N, K):
     """Both shipped GEMM schedules (per-call selection, sa_gemm_bf16_ex) on ragged M/N tiles, every
