@@ -154,7 +154,9 @@ def cpu_child(args):
     T = (frames - 1) // 4 + 1
     L = T * (h // 2) ** 2
     cfg = dict(odit.CONFIG_1_3B, num_layers=1)
-    P = synthetic.fill_state_dict({k: v for k, v in odit.param_shapes(cfg).items() if k.startswith("blocks.0.")}, 0)
+    # timing-only weights (synthetic.timing_state_dict: the rule's scales, tiled from one seeded block), so that the
+    # 1.7 G-parameter fills do not eat into the time the child has before the timed region starts
+    P = synthetic.timing_state_dict({k: v for k, v in odit.param_shapes(cfg).items() if k.startswith("blocks.0.")}, 0)
     g = torch.Generator().manual_seed(0)
     x = torch.randn(3, L, 1536, generator=g)
     e0 = torch.randn(3, 6, 1536, generator=g) * 0.1
@@ -165,7 +167,7 @@ def cpu_child(args):
         t0 = time.time()
         odit.block(P, "blocks.0", x, e0, grid, odit.model_freqs(128), ctx, voc, T, 12)
         t_block = time.time() - t0
-        Pv = synthetic.fill_state_dict(ovae.param_shapes(), 1)
+        Pv = synthetic.timing_state_dict(ovae.param_shapes(), 1)
         z = torch.randn(1, 16, 1, h, h, generator=g)
         t0 = time.time()
         ovae.decode(Pv, z)
@@ -177,7 +179,7 @@ def cpu_child(args):
     # config 1: the 30-layer DiT (synthetic weights) through the restated sliding-window loop + the full decode;
     # encoders excluded (once per call)
     cfg = dict(odit.CONFIG_1_3B)
-    Pd = synthetic.fill_state_dict(odit.param_shapes(cfg), 41)
+    Pd = synthetic.timing_state_dict(odit.param_shapes(cfg), 41)
     size1, clip_length, steps, overlap, audio_frames = 256, 17, 5, 2, 24
     run_steps = max(1, min(steps, args.cpu_config1_steps))
     T1 = (audio_frames - 1) // 4 + 1
@@ -288,8 +290,8 @@ class CpuBaseline:
         out = {"value": round(out_frames / t_clip, 6), "unit": "frames/s", "cores": th, "kind": "port",
                "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
                "sample": f"oracle fp32 (oracle/dit.py, oracle/vae.py) on {th} threads (one core of this process's "
-                         f"share left to the GPU launch thread; run during the untimed warmup clips, ended before "
-                         f"the timed region): 1 of 30 DiT blocks at B=3,L={c2['L']} ({c2['t_block']:.1f}s) + VAE "
+                         f"share left to the GPU launch thread; run during the untimed warmup clips, so it shares the "
+                         f"host with the GPU process's launch thread, and ended before the timed region): 1 of 30 DiT blocks at B=3,L={c2['L']} ({c2['t_block']:.1f}s) + VAE "
                          f"decode of 1 latent frame at {size}x{size} ({c2['t_vae_frame']:.1f}s), extrapolated to "
                          f"{n_fwd} forwards x 30 blocks + {out_frames} frames = {t_clip:.0f}s per clip"}
         c1 = next((r for r in recs if r["leg"] == "config1"), None)
@@ -409,6 +411,35 @@ class ClipWorkload:
     def check(self, video):
         assert video.shape[1] == self.out_frames and torch.isfinite(video).all()
 
+    def _forward_once(self):
+        s, e, _ = self.wins[0]
+        tt = torch.as_tensor(self.sched.timesteps[0], dtype=torch.float32, device=self.dev).reshape(1)
+        return self.dit.forward_window(self.latents, s, True, 3, tt, self.ctx, self.seq_len, self.clip,
+                                       self.y[:, :, :e - s], self.feats[(s, e)], self.args.frames)
+
+    def sp_check(self):
+        """The N > 1 sequence-parallel run checks itself: one DiT forward of the clip's first window (B = 3, the
+        full sequence) through the Ulysses exchange and through the single-GPU layout on every rank, which must
+        agree bit for bit (the SP path reproduces the single-GPU forward); plus the SP output's
+        checksum must be the same on every rank (every rank holds the whole noise prediction)."""
+        import torch.distributed as dist
+        with torch.no_grad():
+            o_sp = self._forward_once().clone()
+            self.dit.disable_multi_gpus_inference()
+            o1 = self._forward_once()
+            self.dit.enable_multi_gpus_inference()
+            sync(self.dev)
+            eq = bool(torch.equal(o_sp, o1))
+            rel = ((o_sp.float() - o1.float()).norm() / o1.float().norm()).item()
+            ck = o_sp.view(torch.int16).to(torch.float64).sum()
+            t = torch.tensor([0.0 if eq else 1.0, rel, ck.item(), -ck.item()], dtype=torch.float64, device=self.dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return {"forward_bit_identical_to_single_gpu": t[0].item() == 0.0, "max_rel_l2_vs_single_gpu": t[1].item(),
+                "ranks_agree": t[2].item() == -t[3].item(),
+                "note": "one DiT forward of the clip's first window (B=3, L=%d) via the Ulysses exchange vs the "
+                        "single-GPU layout, on every rank (max over ranks); ranks_agree: the SP outputs' checksums "
+                        "are equal on all ranks" % self.seq_len}
+
     def start_events(self):
         self.dit._events = []
 
@@ -509,7 +540,7 @@ def attn_traffic(seq_len, layout):
     return tj["hbm_bytes_per_launch"], f"profiles/pmc_attn_traffic.json ({tj.get('source', 'rocprofv3 --pmc')})"
 
 
-POST_RESERVE_S = 15.0  # after the timed region: result assembly, JSON, process-group teardown
+POST_RESERVE_S = 6.0  # after the timed region: result assembly, JSON, process-group teardown (~1 s measured, r03)
 
 
 def run(args, world, rank, dev, work_factory=ClipWorkload, cpu=None):
@@ -549,6 +580,10 @@ def run(args, world, rank, dev, work_factory=ClipWorkload, cpu=None):
     n_fwd = work.n_fwd()
     path_flop = n_fwd * flops.dit_forward_flops(B=3, L=seq_len, n_frames=work.fpb) + \
         flops.vae_decode_flops(work.T, work.h, work.h)
+    sp_check = None
+    if layout == "sp" and world > 1 and hasattr(work, "sp_check"):
+        sp_check = work.sp_check()
+        progress(f"sp check: {sp_check}")
     replicas = None
     if layout == "sp" and args.replica_steps > 0:
         # the layout switch changes the DiT's per-rank token count (workspaces, segment tables): untimed
@@ -621,6 +656,8 @@ def run(args, world, rank, dev, work_factory=ClipWorkload, cpu=None):
                            "skipped": skipped}}
     if replicas is not None:
         out["replicas"] = replicas
+    if sp_check is not None:
+        out["sp_check"] = sp_check
     return out
 
 

@@ -50,7 +50,9 @@ int sa_gemm_bf16_ex(const void* A, int64_t lda, int64_t strideA, const void* W, 
  * k % a_panel_cols] (a_panel_cols % 64 == 0, batch 1, persistent kernel, EPI_RES_F32).  Reads the
  * sequence-parallel head exchange's receive buffer (one panel per head group) as the O-projection input
  * in place, replacing the all-gather of head outputs into token rows around wan/dist/wan_xfuser.py:72-115
- * (1B:1150-1151 after the USP attention).  a_panel_cols == 0 is sa_gemm_bf16_ex. */
+ * (1B:1150-1151 after the USP attention).  a_panel_cols == 0 is sa_gemm_bf16_ex.
+ * The buffer must stay readable for 256 rows (256 * lda elements) past the last panel's row M - 1: the last
+ * panel's tail tile reads those rows (their products are never stored). */
 int sa_gemm_bf16_panels(const void* A, int64_t lda, int64_t strideA, const void* W, int64_t ldw, int64_t strideW,
                         const float* bias, void* C, int64_t ldc, int64_t strideC, int M, int N, int K, int batch,
                         int epilogue, const float* residual, int64_t ldr, int64_t strideR, const float* gate,

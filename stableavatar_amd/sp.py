@@ -92,8 +92,10 @@ class Pending:
 
 def _p2p(sends, recvs, group):
     """sends / recvs: lists of (contiguous tensor, peer rank inside ``group``).  RCCL: one coalesced group of sends and
-    receives landing in place.  gloo cannot move device tensors, so there (several ranks sharing one GPU in
-    the tests) they are staged through host memory and the device receive views are filled on wait()."""
+    receives landing in place (a peer may be this rank itself: loopback, matched in order like any peer's).  gloo
+    cannot move device tensors, so there (several ranks sharing one GPU in the tests) they are staged through host
+    memory and the device receive views are filled on wait(); gloo has no pair to the own rank, so loopback
+    transfers are matched in order and copied locally."""
     if not sends and not recvs:
         return Pending(None)
     t0 = (sends or recvs)[0][0]
@@ -101,6 +103,15 @@ def _p2p(sends, recvs, group):
         ops = [dist.P2POp(dist.isend, t, group=group, group_peer=peer) for t, peer in sends]
         ops += [dist.P2POp(dist.irecv, t, group=group, group_peer=peer) for t, peer in recvs]
         return Pending(dist.batch_isend_irecv(ops), keep=(sends, recvs))
+    me = dist.get_rank(group)
+    self_s = [t for t, peer in sends if peer == me]
+    self_r = [t for t, peer in recvs if peer == me]
+    if len(self_s) != len(self_r):
+        raise RuntimeError(f"loopback: {len(self_s)} sends to this rank but {len(self_r)} receives from it")
+    for s_, r_ in zip(self_s, self_r):
+        r_.copy_(s_)
+    sends = [(t, peer) for t, peer in sends if peer != me]
+    recvs = [(t, peer) for t, peer in recvs if peer != me]
     staged = t0.is_cuda
     works, keep, back = [], [], []
     for t, peer in sends:
@@ -135,38 +146,48 @@ class UlyssesExchange:
         of the first half (the send slab of chunk j's owner) -- except this rank's own chunk, which goes to
         the second half, ``pan``, whose panel j (rows j*B*Lc ..) receives head group j of this rank's tokens
         from the other ranks of the query part: ``pan`` is the O-projection's input in column panels
-        (``ops.linear(..., a_panels=(hg*D, B*Lc*hg*D))``).  ``omap`` is that attention output row map."""
+        (``ops.linear(..., a_panels=(hg*D, B*Lc*hg*D))``).  ``omap`` is that attention output row map.
 
-    def __init__(self, plan: SPPlan, B: int, Lc: int, D: int, device, group=None, dtype=torch.bfloat16):
+    ``loopback=True`` sends this rank's own chunk through the transport as well (its Q/K/V through send slabs of
+    its own, its head outputs through the first half of ``obuf``), a point-to-point transfer to itself: at degree 1
+    on RCCL that runs every send / receive of the exchange on the GPU the box has, with a bit-identical result."""
+
+    def __init__(self, plan: SPPlan, B: int, Lc: int, D: int, device, group=None, dtype=torch.bfloat16,
+                 loopback=False):
         self.plan, self.group, self.B, self.Lc, self.D = plan, group, B, Lc, D
+        self.loopback = bool(loopback)
         p = plan
         N, G, g = p.world, p.G, p.group
         self.hgd = hgd = p.hg * D
         self.Lq, self.Lp = G * Lc, N * Lc
         self.q = torch.empty(B * self.Lq, hgd, device=device, dtype=dtype)
         self.kv = torch.empty(B * self.Lp, 2 * hgd, device=device, dtype=dtype)
-        self.obuf = torch.empty(2 * G * B * Lc, hgd, device=device, dtype=dtype)
-        self.pan = self.obuf[G * B * Lc:]
-        self.remote = [d for d in range(N) if d != p.rank]
+        # + 256 rows of slack: the O-projection's last tile reads up to 256 rows past the last panel
+        # (sa_gemm_bf16_panels; the buffer range check does not cover the panel offset)
+        self.obuf = torch.empty(2 * G * B * Lc + 256, hgd, device=device, dtype=dtype)
+        self.pan = self.obuf[G * B * Lc:2 * G * B * Lc]
+        self.remote = [d for d in range(N) if d != p.rank or self.loopback]
         self.sq = {d: torch.empty(B, Lc, hgd, device=device, dtype=dtype) for d in self.remote if d // G == p.part}
         self.skv = {d: torch.empty(B, Lc, 2 * hgd, device=device, dtype=dtype) for d in self.remote}
         qv = self.q.view(B, self.Lq, hgd)
         kvv = self.kv.view(B, self.Lp, 2 * hgd)
         rows = []
         for d in range(N):
-            if d == p.rank:
+            if d == p.rank and not self.loopback:
                 qd, kd = qv[:, g * Lc:(g + 1) * Lc], kvv[:, p.rank * Lc:(p.rank + 1) * Lc]
             else:
                 qd, kd = self.sq.get(d), self.skv[d]
             rows.append([0, 0, 0] if qd is None else [qd.data_ptr(), qd.stride(1), qd.stride(0)])
             rows[-1] += [kd.data_ptr(), kd.stride(1), kd.stride(0)]
         self.slabs = {d: (self.sq.get(d), self.skv[d]) for d in self.remote}
-        self.slabs[p.rank] = (qv[:, g * Lc:(g + 1) * Lc], kvv[:, p.rank * Lc:(p.rank + 1) * Lc])
+        if not self.loopback:
+            self.slabs[p.rank] = (qv[:, g * Lc:(g + 1) * Lc], kvv[:, p.rank * Lc:(p.rank + 1) * Lc])
         self.table = torch.tensor(rows, dtype=torch.int64).to(device)
         j = torch.arange(G).view(1, G, 1)
         b = torch.arange(B).view(B, 1, 1)
         t = torch.arange(Lc).view(1, 1, Lc)
-        omap = (j == g).to(torch.int64) * (G * B * Lc) + (j * B + b) * Lc + t  # [B, G, Lc] = q row order
+        own = (j == g).to(torch.int64) * (0 if self.loopback else 1)  # own chunk straight into its panel
+        omap = own * (G * B * Lc) + (j * B + b) * Lc + t  # [B, G, Lc] = q row order
         self.omap = omap.reshape(-1).to(torch.int32).to(device)
 
     def heads(self, rows) -> Pending:
@@ -193,11 +214,11 @@ class UlyssesExchange:
         sends, recvs = [], []
         for b in rows:
             for j in range(G):
-                if j != p.group:
+                if j != p.group or self.loopback:
                     r0 = (j * B + b) * Lc
                     sends.append((self.obuf[r0:r0 + Lc], p.part * G + j))
             for j in range(G):
-                if j != p.group:
+                if j != p.group or self.loopback:
                     r0 = (j * B + b) * Lc
                     recvs.append((self.pan[r0:r0 + Lc], p.part * G + j))
         return _p2p(sends, recvs, self.group)

@@ -52,6 +52,25 @@ def fill_state_dict(shapes: dict, seed: int = 0, backend: str = "numpy", device=
     return {n: param_tensor(n, s, seed, backend, device) for n, s in shapes.items()}
 
 
+def timing_state_dict(shapes: dict, seed: int = 0) -> dict:
+    """{name: shape} -> fp32 tensors with the rule's mean / std per name, but tiled from ONE seeded block of 2^20
+    normals instead of a generator per tensor: for runs that only time the arithmetic (bench.py's CPU baseline),
+    where filling 1.7 G parameters one generator at a time would take longer than the measured work.  The values
+    are normal floats of the same scale (no denormals), so the timing is that of real weights."""
+    base = torch.from_numpy(np.random.Generator(np.random.PCG64(seed)).standard_normal(1 << 20, dtype=np.float32))
+    out = {}
+    for n, shp in shapes.items():
+        mean, std = _std_for(n, tuple(shp))
+        cnt = int(np.prod(shp)) if len(shp) else 1
+        nb = base.numel()
+        reps = -(-cnt // nb)
+        src = base[:min(cnt, nb)] * std + mean
+        t = torch.empty(reps * src.numel())
+        t.view(reps, src.numel()).copy_(src.expand(reps, -1))  # one (threaded) write pass
+        out[n] = t[:cnt].view(tuple(shp))
+    return out
+
+
 def seeded_normal(shape, seed: int, scale: float = 1.0) -> torch.Tensor:
     rng = np.random.Generator(np.random.PCG64(seed))
     return torch.from_numpy(rng.standard_normal(size=tuple(shape), dtype=np.float32) * np.float32(scale))

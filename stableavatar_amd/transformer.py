@@ -233,6 +233,7 @@ class WanTransformer3DFantasyModel(nn.Module):
         self._split_cache = {}
         self._events = None  # optional list to record (start, end) events around self-attention
         self._sp_enabled = False
+        self._sp_loopback = False
 
     # ------------------------------------------------------------------ loading
 
@@ -316,14 +317,17 @@ class WanTransformer3DFantasyModel(nn.Module):
     def disable_teacache(self):
         self.teacache = None
 
-    def enable_multi_gpus_inference(self, group=None):
+    def enable_multi_gpus_inference(self, group=None, loopback=None):
         """Ulysses sequence parallelism over torch.distributed (RCCL); replaces the xfuser path
-        installed at 1B:918-923 with single-GPU semantics."""
+        installed at 1B:918-923 with single-GPU semantics.  loopback=True (default: env
+        SA_SP_LOOPBACK=1) also sends this rank's own token chunk through the point-to-point transport (a transfer
+        to itself), so at degree 1 every exchange of the layer runs on RCCL; the output is unchanged."""
         import torch.distributed as dist
         self.sp_group = group
         self.sp_world_size = dist.get_world_size(group)
         self.sp_world_rank = dist.get_rank(group)
         self._sp_enabled = True  # the exchange path runs even at degree 1 (pack + row-mapped attention + panels)
+        self._sp_loopback = (os.environ.get("SA_SP_LOOPBACK", "0") == "1") if loopback is None else bool(loopback)
 
     def disable_multi_gpus_inference(self):
         """back to single-GPU forwards (every rank its own clip)"""
@@ -447,11 +451,12 @@ class WanTransformer3DFantasyModel(nn.Module):
     def _sp_exchange(self, plan, B, Lc, dev):
         """the sequence-parallel exchange buffers (attention inputs, send slabs, output / panel buffer, pack
         table, output row map) for this shape, kept across layers, steps and calls (one shape at a time)"""
-        key = (plan, B, Lc, self.d, str(dev), id(self.sp_group))
+        key = (plan, B, Lc, self.d, str(dev), id(self.sp_group), self._sp_loopback)
         ex = self._sp_ex
         if ex is None or ex[0] != key:
             self._sp_ex = None  # free the previous shape's buffers first
-            ex = self._sp_ex = (key, sp.UlyssesExchange(plan, B, Lc, self.d, dev, self.sp_group))
+            ex = self._sp_ex = (key, sp.UlyssesExchange(plan, B, Lc, self.d, dev, self.sp_group,
+                                                        loopback=self._sp_loopback))
         return ex[1]
 
     @staticmethod

@@ -249,6 +249,41 @@ class _ChainState:
         self.sends = []
 
 
+class _LoopbackChain(_ChainState):
+    """Virtual rank v of n decoded in turn on ONE rank (degree-1 RCCL test of the wavefront): every cache hand-off is a
+    point-to-point send to this rank itself with its matching receive in one coalesced group (sp._p2p), the
+    received copy queued for virtual rank v + 1."""
+
+    def __init__(self, group, v, n, fifo):
+        import torch.distributed as dist
+        self.group, self.rank, self.n, self.fifo = group, v, n, fifo
+        self.me = dist.get_rank(group)
+        self.sends, self.local = [], {}
+        self.first_sub, self.last_sub = True, True
+
+    def get(self, key, like):
+        if not self.first_sub:
+            return self.local.get(key)
+        if self.rank == 0:
+            return None
+        pend, t = self.fifo.popleft()
+        pend.wait()
+        return t
+
+    def put(self, key, val):
+        from . import sp
+        if not self.last_sub:
+            self.local[key] = val
+            return
+        if self.rank + 1 >= self.n:
+            return
+        t = torch.empty_like(val)
+        self.fifo.append((sp._p2p([(val, self.me)], [(t, self.me)], self.group), t))
+
+    def finish(self):
+        pass
+
+
 def _all_gather(buf, N, group):
     """[N, *buf.shape]: every rank's buf (gathered as the concatenation along dim 0)"""
     import torch.distributed as dist
@@ -581,7 +616,7 @@ class AutoencoderKLWan(nn.Module):
         dev = pk.mean.device
         Cz, T, H, W = z.shape
         chunk = chunk or self.decode_chunk
-        if self.decode_group is not None and _world(self.decode_group) > 1:
+        if self.decode_group is not None and (_world(self.decode_group) > 1 or self.decode_loopback > 1):
             return self._decode_parallel(pk, z, post, chunk)
         if T <= chunk:
             return self._decode_chunk(pk, z, True, None, post)
@@ -594,43 +629,57 @@ class AutoencoderKLWan(nn.Module):
             out[:, o0:o0 + y.shape[1]].copy_(y)
         return out
 
-    def enable_multi_gpus_inference(self, group=None):
+    def enable_multi_gpus_inference(self, group=None, loopback_ranks=0):
         """Decode over the ranks of `group` (default: the torch.distributed world): rank r decodes the r-th
         contiguous run of latent frames, taking each causal conv's 2-frame cache from rank r-1 and handing
         its own to rank r+1 (P2P, one send per cache point: a wavefront over the ranks), then one gather.
-        Bit-identical to the single-GPU decode (the chunked decode == whole-clip decode)."""
+        Bit-identical to the single-GPU decode (the chunked decode == whole-clip decode).
+        loopback_ranks = n > 1 on a group of ONE rank: that rank decodes the n runs in turn and every hand-off
+        between them is a transfer to itself through the group's transport (the degree-1 RCCL test)."""
         import torch.distributed as dist
         self.decode_group = group if group is not None else dist.group.WORLD
+        self.decode_loopback = int(loopback_ranks) if _world(self.decode_group) == 1 else 0
         return self
+
+    decode_loopback = 0
 
     def disable_multi_gpus_inference(self):
         self.decode_group = None
+        self.decode_loopback = 0
         return self
 
     def _decode_parallel(self, pk, z, post, chunk):
         import torch.distributed as dist
+        import collections
         grp = self.decode_group
         N, r = _world(grp), dist.get_rank(grp)
+        virt = self.decode_loopback if N == 1 else 0  # virtual ranks decoded in turn on this one rank
         dev = pk.mean.device
         Cz, T, H, W = z.shape
-        n = min(N, T)
+        n = min(max(N, virt), T)
         bounds = [round(i * T / n) for i in range(n + 1)]  # contiguous runs of latent frames
         frames = lambda i: (1 + 4 * (bounds[1] - 1)) if i == 0 else 4 * (bounds[i + 1] - bounds[i])  # noqa: E731
         fmax = max(frames(i) for i in range(n))
-        buf = torch.zeros(fmax, 3, 8 * H, 8 * W, device=dev, dtype=torch.float32)
-        if r < n:
-            state = _ChainState(grp, r, n)
+        buf = torch.zeros(max(1, virt), fmax, 3, 8 * H, 8 * W, device=dev, dtype=torch.float32)
+        fifo = collections.deque()
+        for v in (range(n) if virt else [r]):
+            if v >= n:
+                continue
+            state = _LoopbackChain(grp, v, n, fifo) if virt else _ChainState(grp, v, n)
+            bv = buf[v if virt else 0]
             o = 0
-            subs = list(range(bounds[r], bounds[r + 1], chunk))
+            subs = list(range(bounds[v], bounds[v + 1], chunk))
             for j, c0 in enumerate(subs):  # sub-chunks of <= `chunk` latent frames bound the activations
-                c1 = min(c0 + chunk, bounds[r + 1])
+                c1 = min(c0 + chunk, bounds[v + 1])
                 state.begin(j == 0, j == len(subs) - 1)
                 y = self._decode_chunk(pk, z[:, c0:c1], c0 == 0, state, post)  # [3, F, 8H, 8W]
-                buf[o:o + y.shape[1]].copy_(y.transpose(0, 1))
+                bv[o:o + y.shape[1]].copy_(y.transpose(0, 1))
                 o += y.shape[1]
             state.finish()
-            assert o == frames(r)
-        allb = _all_gather(buf, N, grp)  # [N, fmax, 3, 8H, 8W]
+            assert o == frames(v)
+        assert not fifo
+        allb = _all_gather(buf.view(-1, *buf.shape[2:]) if virt else buf[0], N, grp)
+        allb = allb.view(max(N, virt), fmax, *buf.shape[2:])  # [ranks, fmax, 3, 8H, 8W]
         out = torch.cat([allb[i, :frames(i)] for i in range(n)]).transpose(0, 1).contiguous()
         assert out.shape[1] == 1 + 4 * (T - 1)
         return out

@@ -183,3 +183,21 @@ def clip_image(cfg):
     """the reference frame as the pipeline hands it to CLIP: [C, 1, H, W] in [-1, 1]"""
     H, W = cfg["img_hw"]
     return synthetic.seeded_normal((3, 1, H, W), 700 + cfg["seed"], 0.5).clamp(-1, 1)
+
+
+# The examples/case-1 windowed shape at full size (BASELINE config 2's long-clip form, SURVEY.md §8 a1): 512x512,
+# T_lat 42 (165 video frames), 81-frame windows (21 latent frames) at overlap 15 -> 5 windows per step, with a
+# 1-layer full-width DiT, 2 sampling steps of the 50-step schedule (the blend and the scatter run at full size in
+# step 2).  The expected latents come from oracle/pipeline.py's loop on the CPU (gen_case1_fullsize.py).
+CASE1_FULL = dict(dit=dict(DIT_FULL, num_layers=1, seed=61), T=42, clip_length=81, overlap=15, size=512,
+                  steps=50, run_steps=2, text_guide=3.0, audio_guide=5.0)
+
+
+def case1_fullsize_inputs(C=CASE1_FULL):
+    T, h = C["T"], C["size"] // 8
+    fpb = (C["clip_length"] - 1) // 4 + 1
+    return dict(latents=synthetic.seeded_normal((1, 16, T, h, h), 601),
+                y=synthetic.seeded_normal((3, 20, fpb, h, h), 602),
+                context=[synthetic.seeded_normal((24, 4096), 603)] * 2 + [synthetic.seeded_normal((31, 4096), 604)],
+                clip=synthetic.seeded_normal((1, 257, 1280), 605).expand(3, -1, -1).contiguous(),
+                audio=synthetic.seeded_normal(((1 + 4 * (T - 1)) * 640 + 320,), 606, 0.1))

@@ -139,8 +139,9 @@ def test_dit_gemm_fullsize(name, N, K, epi):
     print(f"gemm {name} M={M} N={N} K={K}: rel-L2 {e:.2e}")
     assert e < tol, e
     # the 192-row persistent tiles (picked by auto for the sequence-parallel per-rank shapes) accumulate every
-    # output in the same K order: bit-identical, here at M = 64 512 and at the N = 8 per-rank M = 8 064
-    for Mx in (M, 3 * 2688):
+    # output in the same K order: bit-identical, here at M = 64 512, at the N = 8 per-rank M = 8 064, and at M
+    # with a partial last tile of either height (12 285 = the per-rank M at 480x832, N = 8; 1 000)
+    for Mx in (M, 3 * 2688, 3 * 4095, 1000):
         y2 = torch.empty(Mx, N, device=dev, dtype=y.dtype)
         y3 = torch.empty_like(y2)
         for yy, kern in ((y2, ops.GEMM_PERSISTENT), (y3, ops.GEMM_PERSISTENT192)):

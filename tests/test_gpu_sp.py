@@ -5,7 +5,9 @@ dit14_small.npz, with the same tolerance as the single-GPU golden tests (rel-L2 
 run also matches the same process's single-GPU forward to 1e-3.  Cases: 'full' (80 tokens), 'short' (the padded
 last window), 'wide' (120 tokens); at world 8 the 80- and 84-token sequences are padded to a multiple of the
 degree (SP pads are queries only).  All three exchange schedules run (sync batched; per-row with per-row attention;
-per-row Q/K/V exchanges with one batched attention)."""
+per-row Q/K/V exchanges with one batched attention).  On RCCL the box's one GPU allows a single rank
+(two RCCL ranks cannot share a device), so the RCCL tests run at degree 1 with loopback transfers (each rank's own
+chunk sent to itself): every send / receive, stream wait and all-gather of the exchange executes on RCCL."""
 import os
 import socket
 import sys
@@ -111,10 +113,12 @@ def test_sp_matches_reference_golden(world, model):
 
 
 def _rccl_worker(port, overlap, qret):
-    """RCCL (backend "nccl") process group of ONE rank with the SP path forced on: every Ulysses
-    exchange is a real async all_to_all_single on ProcessGroupNCCL's stream (a self-copy at degree 1)
-    with the deferred unpack (sp.Pending), and the head output goes through all_gather_into_tensor -
-    the code that runs over xGMI at N = 2/4/8, here on the one GPU of the box."""
+    """RCCL (backend "nccl") process group of ONE rank with the SP path forced on, in loopback mode
+    (UlyssesExchange(loopback=True)): this rank's own token chunk goes through the point-to-point transport to
+    itself, so every Q/K/V and head-output transfer of the layer is a real dist.P2POp in a batch_isend_irecv group
+    on ProcessGroupNCCL's stream, with the caller's stream waiting on it (sp.Pending) -- the sends / receives that
+    run over xGMI at N = 2/4/8 -- and the head output goes through all_gather_into_tensor.  Without loopback the
+    degree-1 exchange has no remote rank and sends nothing; that run is checked too."""
     os.environ["SA_SP_OVERLAP"] = overlap
     import torch.distributed as dist
     sys.path.insert(0, HERE)
@@ -125,12 +129,19 @@ def _rccl_worker(port, overlap, qret):
                             device_id=torch.device("cuda:0"))
     try:
         m = make_model(DIT_SMALL)
-        inp = dit_inputs(DIT_SMALL, "full")
-        single = run(m, inp)
-        m.enable_multi_gpus_inference()
-        assert dist.get_backend() == "nccl" and m._sp_enabled
-        par = run(m, inp)
-        qret.put((torch.equal(par, single), ((par - single).norm() / single.norm()).item()))
+        res = []
+        for case in ("full", "short"):
+            inp = dit_inputs(DIT_SMALL, case)
+            m.disable_multi_gpus_inference()
+            single = run(m, inp)
+            for loop in (False, True):
+                m.enable_multi_gpus_inference(loopback=loop)
+                assert dist.get_backend() == "nccl" and m._sp_enabled
+                par = run(m, inp)
+                ex = m._sp_ex[1]
+                res.append((case, loop, torch.equal(par, single), ((par - single).norm() / single.norm()).item(),
+                            ex.loopback, len(ex.remote)))
+        qret.put(res)
     finally:
         dist.destroy_process_group()
 
@@ -141,7 +152,60 @@ def test_sp_rccl_path_degree1(overlap):
     qret = ctx.Queue()
     p = ctx.Process(target=_rccl_worker, args=(_free_port(), overlap, qret))
     p.start()
-    same, err = collect([p], qret, 1)[0]
+    res = collect([p], qret, 1)[0]
     p.join(timeout=120)
     assert p.exitcode == 0
-    assert same, err
+    for case, loop, same, err, ex_loop, n_remote in res:
+        print(f"RCCL degree 1 overlap {overlap} {case} loopback {loop}: bit-identical {same} (rel {err:.1e})")
+        assert ex_loop == loop and n_remote == (1 if loop else 0)
+        assert same, (case, loop, err)
+
+
+def _rccl_dp_vae_worker(port, qret):
+    """window parallelism's async all_gather_into_tensor (sp.all_gather_slots) on a one-rank RCCL group, and the VAE
+    decode's causal-cache wavefront over 3 virtual ranks whose hand-offs are RCCL transfers to this rank itself"""
+    import torch.distributed as dist
+    sys.path.insert(0, HERE)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda:0"))
+    try:
+        from golden_cases import PIPE
+        from stableavatar_amd import synthetic
+        from stableavatar_amd.pipeline import WanI2VTalkingInferenceLongPipeline
+        from stableavatar_amd.transformer import WanTransformer3DFantasyModel, param_shapes
+        from stableavatar_amd.vae import AutoencoderKLWan, encoder_param_shapes, param_shapes as vae_shapes
+        from test_gpu_window_dp import _run
+        dcfg = PIPE["dit"]
+        dit = WanTransformer3DFantasyModel(**{k: v for k, v in dcfg.items() if k != "seed"})
+        dit.load_state_dict(synthetic.fill_state_dict(param_shapes(dcfg), dcfg["seed"]))
+        pipe = WanI2VTalkingInferenceLongPipeline(transformer=dit.cuda())
+        single = _run(pipe, 9, False)
+        par = _run(pipe, 9, True)
+        res = {"window_dp": (bool(torch.equal(single, par)), float((single.float() - par.float()).abs().max()))}
+        v = AutoencoderKLWan(dim=32)
+        v.load_state_dict(synthetic.fill_state_dict(dict(vae_shapes(dim=32), **encoder_param_shapes(dim=32)), 24))
+        v = v.cuda()
+        z = synthetic.seeded_normal((16, 7, 8, 8), 424).cuda()
+        with torch.no_grad():
+            vs = v.decode_clip(z, post=True).cpu()
+            v.enable_multi_gpus_inference(loopback_ranks=3)
+            vp = v.decode_clip(z, post=True, chunk=2).cpu()
+        torch.cuda.synchronize()
+        res["vae_loopback"] = (bool(torch.equal(vs, vp)), float((vs - vp).abs().max()), v.decode_loopback)
+        qret.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_window_dp_and_vae_loopback_degree1():
+    ctx = mp.get_context("spawn")
+    qret = ctx.Queue()
+    p = ctx.Process(target=_rccl_dp_vae_worker, args=(_free_port(), qret))
+    p.start()
+    res = collect([p], qret, 1, timeout=300)[0]
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    print(res)
+    assert res["window_dp"][0], res
+    assert res["vae_loopback"][0] and res["vae_loopback"][2] == 3, res

@@ -46,7 +46,7 @@ def _pack(ex, mine, plan):
         kd.copy_(torch.cat([grp[:, :, 1], grp[:, :, 2]], -1))
 
 
-def _worker(rank, world, port, B, Lp, H, D, q_ret):
+def _worker(rank, world, port, B, Lp, H, D, q_ret, loopback=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -60,7 +60,8 @@ def _worker(rank, world, port, B, Lp, H, D, q_ret):
         hg, G = plan.hg, plan.G
         res = []
         for rows in ([list(range(B))], [[b] for b in range(B)]):          # batched / per CFG row
-            ex = sp.UlyssesExchange(plan, B, Lc, D, "cpu", dtype=torch.float32)
+            ex = sp.UlyssesExchange(plan, B, Lc, D, "cpu", dtype=torch.float32, loopback=loopback)
+            assert (rank in ex.remote) == loopback
             # the pack table is the slab views' addresses and strides (elements)
             for d, (qd, kd) in ex.slabs.items():
                 t = ex.table[d].tolist()
@@ -93,15 +94,17 @@ def _worker(rank, world, port, B, Lp, H, D, q_ret):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,H", [(2, 12), (3, 12), (4, 12), (8, 12), (8, 40)])
-def test_ulysses_exchange_matches_full_attention(world, H):
-    """12 heads: the 1.3B model (N = 8 is U4 x 2 query parts); 40 heads: the 14B model (N = 8 is U8)"""
+@pytest.mark.parametrize("world,H,loopback", [(2, 12, False), (3, 12, False), (4, 12, False), (8, 12, False),
+                                               (8, 40, False), (1, 12, True), (2, 12, True), (8, 12, True)])
+def test_ulysses_exchange_matches_full_attention(world, H, loopback):
+    """12 heads: the 1.3B model (N = 8 is U4 x 2 query parts); 40 heads: the 14B model (N = 8 is U8).  loopback:
+    each rank's own chunk also goes through the transport (to itself), the layout the degree-1 RCCL test runs"""
     B, D = 3, 16
     Lp = sp.padded_len(48, world)
     ctx = mp.get_context("spawn")
     qret = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, B, Lp, H, D, qret)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, B, Lp, H, D, qret, loopback)) for r in range(world)]
     for p in procs:
         p.start()
     res = [qret.get(timeout=120) for _ in range(world)]

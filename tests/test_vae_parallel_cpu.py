@@ -73,3 +73,48 @@ def test_chain_protocol(world):
             assert all(v == float(rank + 1) for v in first), (rank, first)
         assert seen[11:] == [float(rank + 1)] * 11  # sub-chunk 1 reads sub-chunk 0's local caches
         assert g == [[[float(i)] * 3] * 2 for i in range(world)]
+
+
+def _loop_worker(port, n, qret):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        import collections
+        from stableavatar_amd.vae import _LoopbackChain
+        like = torch.zeros(3, 2, 2, 4, dtype=torch.bfloat16)
+        fifo = collections.deque()
+        out = []
+        for v in range(n):  # the virtual ranks, decoded in turn on the one rank
+            x = torch.full_like(like, float(v + 1))
+            st = _LoopbackChain(dist.group.WORLD, v, n, fifo)
+            seen = []
+            for sub in range(2):
+                st.begin(sub == 0, sub == 1)
+                for k in range(12):
+                    if k == 5:
+                        st.skip(k, like)
+                        continue
+                    p = st.get(k, like)
+                    seen.append(None if p is None else float(p.float().mean()))
+                    st.put(k, (x + sub)[-2:].clone())
+            st.finish()
+            out.append((v, seen))
+        qret.put((out, len(fifo)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_chain_protocol_loopback():
+    """3 virtual ranks on ONE rank (AutoencoderKLWan.enable_multi_gpus_inference(loopback_ranks=3)): the same
+    hand-off sequence as 3 real ranks, every cache passed through a transfer to the rank itself"""
+    ctx = mp.get_context("spawn")
+    qret = ctx.Queue()
+    p = ctx.Process(target=_loop_worker, args=(_free_port(), 3, qret))
+    p.start()
+    (res, left), = collect([p], qret, 1)
+    p.join(timeout=60)
+    assert p.exitcode == 0 and left == 0
+    for v, seen in res:
+        first = seen[:11]
+        assert all(x is None for x in first) if v == 0 else all(x == float(v + 1) for x in first), (v, first)
+        assert seen[11:] == [float(v + 1)] * 11
