@@ -672,6 +672,10 @@ def main(argv=None, work_factory=ClipWorkload, device=None):
         return launch_workers(args, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        # the N > 1 sequence-parallel schedule runs each CFG row on its own stream beside RCCL's: enough hardware
+        # queues (HIP default 4) that the row streams and the transport do not share one; set before any HIP call
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")

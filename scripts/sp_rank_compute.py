@@ -46,8 +46,10 @@ def fwd():
 
 
 res = []
+modes = os.environ.get("SA_SPRC_MODES", "1").split(",")  # SA_SP_OVERLAP values to time at each degree > 1
 with torch.no_grad():
-    for N in degrees:
+    for N, ov in [(n, o) for n in degrees for o in (modes if n > 1 else ["1"])]:
+        os.environ["SA_SP_OVERLAP"] = ov
         if N == 1:
             m.disable_multi_gpus_inference()
         else:
@@ -66,7 +68,7 @@ with torch.no_grad():
             fwd()
             torch.cuda.synchronize()
             ts.append((time.perf_counter() - t0) * 1e3)
-        r = {"kernel": "sp_rank_forward", "degree": N, "ms": round(sorted(ts)[1], 2)}
+        r = {"kernel": "sp_rank_forward", "degree": N, "sp_overlap": ov, "ms": round(sorted(ts)[1], 2)}
         res.append(r)
         print(json.dumps(r), flush=True)
 base = res[0]["ms"] if res[0]["degree"] == 1 else None

@@ -14,6 +14,8 @@
 // Both use an XCD-aware tile order (T1) and fuse bias / GELU / SiLU / fp32 gated-residual epilogues.
 #include <stdlib.h>
 
+#include <utility>
+
 #include "common.h"
 
 namespace {
@@ -50,6 +52,12 @@ __device__ __forceinline__ void tile_coords(int wg, int nm, int nn, int gm, int&
 
 constexpr int BM = 256, BN = 256, BK = 64;
 // per-FLOP cost of the 192-row persistent tile relative to the 256-row one (auto tile choice; measured r3t2)
+// the persistent kernel's K schedule under auto: 9 = three barriers per K step (in the bench clip, 4 sampling
+// steps: QKV / cross-Q 520 -> 507 us, O-proj / cross-O / FFN-down 740 -> 702 us average, FFN-up 1594 -> 1549 us,
+// bit-identical; profiles/r04/README.md), 8 = the round-3 one-barrier step
+#ifndef SA_GEMM_SCHED_DEFAULT
+#define SA_GEMM_SCHED_DEFAULT 9
+#endif
 #ifndef SA_T192_COST
 #define SA_T192_COST 1.06  // QKV 1.025, O-proj 1.087, cross-Q 1.05, FFN-up 1.023, FFN-down 1.095 at M = 64 512
 #endif
@@ -694,10 +702,102 @@ __device__ __forceinline__ void s8_step(const GemmArgs& g, const S5Ctx& c, f32x4
   s5_half<S ^ 1, 0, true, S, true, MI>(c, acc, a1, b1, a0, b0, ks, s8_ksa<PANEL>(g, ks));
 }
 
+// ------------------------------------------------------------------------------------------------
+// s9 K step: the same stage / tile / fragment geometry as s8 on a three-barrier schedule, so the DMA of a K-tile
+// gets ~1.5 steps to land (s8: 0.5-1) and the one wait per step is a counted vmcnt, never 0.  Step t (stage S,
+// a0/b0 = (t, k 0-31) fragments, read at the end of step t-1), MFMA slots 0 .. 2*NS-1 (NS = 8*MI per k half,
+// row-major over (A fragment, W fragment)):
+//   slots  0-15  kh0 rows 0-1, reads of A (t, k 32-63) into a1              -> lgkmcnt(0), barrier #1
+//   slots 16-39  kh0 rows 2-4, reads of W (t, k 32-63) into b1 and the MI A
+//                DMA pieces of tile t+2 (into stage S's A region: its A reads are done)   -> lgkmcnt(0), barrier #2
+//   slots 40-T3  the 8 W DMA pieces of tile t+2 (stage S's W region)       -> vmcnt(MI+8): tile t+1 landed, barrier #3
+//   slots T3-..  the last 3 kh1 rows, reads of (t+1, k 0-31) into b0 / a0 from stage S^1
+// (T3 = 2*NS - 24).  Every fragment register is rewritten >= 12 MFMAs after its last use.
+template <int MI>
+struct S9 {
+  static constexpr int NS = 8 * MI, TOT = 2 * NS, T3 = TOT - 24, NR = 8 + MI;
+  // action after MFMA slot s: 0 none, 1+i read a1[i], 9+i read b1[i], 17+i A DMA i, 25+i W DMA i, 33+i read b0[i],
+  // 41+i read a0[i]
+  static constexpr int act(int s) {
+    if (s < 16) return (s & 1) && (s >> 1) < MI ? 1 + (s >> 1) : 0;
+    if (s < 40) {
+      const int k = (s - 16) / 3, r = (s - 16) % 3;
+      if (r == 0) return 9 + k;
+      if (r == 1 && k < MI) return 17 + k;
+      return 0;
+    }
+    if (s < T3) {
+      const int span = T3 - 40, step = span / 8;
+      const int o = s - 40 - step / 2;
+      return (o >= 0 && o % step == 0 && o / step < 8) ? 25 + o / step : 0;
+    }
+    // NR reads over the last 24 slots: b0[0..7] first, then a0[0..MI-1]
+    for (int k = 0; k < NR; ++k)
+      if (s == T3 + (k * 24) / NR) return k < 8 ? 33 + k : 41 + (k - 8);
+    return 0;
+  }
+};
+
+template <int STAGE_R, int STAGE_D, int MI, int S>
+__device__ __forceinline__ void s9_slot(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8], u32x4 (&b0)[8],
+                                        u32x4 (&a1)[8], u32x4 (&b1)[8], int ks, int ksa) {
+  using P = S9<MI>;
+  constexpr int kh = S / P::NS, r = S % P::NS, Q = r / 8, j = r % 8;
+  if constexpr (kh == 0)
+    s4_mma(acc[Q][j], b0[j], a0[Q]);
+  else
+    s4_mma(acc[Q][j], b1[j], a1[Q]);
+  constexpr int a = P::act(S);
+  // reads of the current tile's second k half come from stage STAGE_R; the next tile's first half from STAGE_R ^ 1
+  if constexpr (a >= 1 && a < 9)
+    s4_ds<(a - 1) * 2048>(a1[a - 1], c.ard[STAGE_R][1]);
+  else if constexpr (a >= 9 && a < 17)
+    s4_ds<(a - 9) * 2048>(b1[a - 9], c.wrd[STAGE_R][1]);
+  else if constexpr (a >= 17 && a < 25)
+    s5_dma<STAGE_D, a - 17, MI>(c, ks, ksa);
+  else if constexpr (a >= 25 && a < 33)
+    s5_dma<STAGE_D, MI + a - 25, MI>(c, ks, ksa);
+  else if constexpr (a >= 33 && a < 41)
+    s4_ds<(a - 33) * 2048>(b0[a - 33], c.wrd[STAGE_R ^ 1][0]);
+  else if constexpr (a >= 41)
+    s4_ds<(a - 41) * 2048>(a0[a - 41], c.ard[STAGE_R ^ 1][0]);
+  if constexpr (S == 15 || S == 39) {
+    if constexpr (S == 15)
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a1[0]), "+v"(a1[1]), "+v"(a1[2]), "+v"(a1[3]), "+v"(a1[4]),
+                   "+v"(a1[5]), "+v"(a1[6]), "+v"(a1[7])::"memory");
+    else
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b1[0]), "+v"(b1[1]), "+v"(b1[2]), "+v"(b1[3]), "+v"(b1[4]),
+                   "+v"(b1[5]), "+v"(b1[6]), "+v"(b1[7])::"memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  if constexpr (S == P::T3 - 1) {
+    if constexpr (MI == 8)
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+}
+
+template <int STAGE, int MI, int... Ss>
+__device__ __forceinline__ void s9_slots(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8], u32x4 (&b0)[8],
+                                         u32x4 (&a1)[8], u32x4 (&b1)[8], int ks, int ksa,
+                                         std::integer_sequence<int, Ss...>) {
+  (s9_slot<STAGE, STAGE, MI, Ss>(c, acc, a0, b0, a1, b1, ks, ksa), ...);
+}
+
+// step on the K-tile in stage S; ks = the K-tile (x 128 B) the step's DMA fetches into stage S
+template <int S, bool PANEL, int MI = 8>
+__device__ __forceinline__ void s9_step(const GemmArgs& g, const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8],
+                                        u32x4 (&b0)[8], u32x4 (&a1)[8], u32x4 (&b1)[8], int ks) {
+  s4_wait_frags<MI>(a0, b0);
+  s9_slots<S, MI>(c, acc, a0, b0, a1, b1, ks, s8_ksa<PANEL>(g, ks), std::make_integer_sequence<int, S9<MI>::TOT>{});
+}
+
 // MI = 6: 192 x 256 tiles (4 waves x 96 x 128), for launches whose 256-row tile count leaves the last round over
 // the CUs mostly empty (the per-rank GEMMs of sequence parallelism: 8 064 rows at N = 8 fill 0.74 of a round of
 // 256 x 256 tiles, 0.98 of a round of 192 x 256)
-template <int EPI, bool PANEL = false, int MI = 8>
+template <int EPI, bool PANEL = false, int MI = 8, int SCHED = 8>
 __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) {
   constexpr int BMT = 32 * MI;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -778,13 +878,21 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
         const bool nx = t + 2 >= nk;  // DMA of the next tile's K-tile t+2-nk (or a re-read of the last)
         c.ra = nx ? nra : cra;
         c.rw = nx ? nrw : crw;
-        s8_step<0, PANEL, MI>(g, c, acc, a0, b0, a1, b1, (nx ? (has_next ? t + 2 - nk : nk - 1) : t + 2) * 128);
+        const int ksd = (nx ? (has_next ? t + 2 - nk : nk - 1) : t + 2) * 128;
+        if constexpr (SCHED == 9)
+          s9_step<0, PANEL, MI>(g, c, acc, a0, b0, a1, b1, ksd);
+        else
+          s8_step<0, PANEL, MI>(g, c, acc, a0, b0, a1, b1, ksd);
       }
       {
         const bool nx = t + 3 >= nk;
         c.ra = nx ? nra : cra;
         c.rw = nx ? nrw : crw;
-        s8_step<1, PANEL, MI>(g, c, acc, a0, b0, a1, b1, (nx ? (has_next ? t + 3 - nk : nk - 1) : t + 3) * 128);
+        const int ksd = (nx ? (has_next ? t + 3 - nk : nk - 1) : t + 3) * 128;
+        if constexpr (SCHED == 9)
+          s9_step<1, PANEL, MI>(g, c, acc, a0, b0, a1, b1, ksd);
+        else
+          s8_step<1, PANEL, MI>(g, c, acc, a0, b0, a1, b1, ksd);
       }
     }
     asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // MFMA -> v_accvgpr_read
@@ -806,6 +914,34 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
 
 constexpr int KERNEL_AUTO = 0, KERNEL_PINGPONG = 1, KERNEL_PERSISTENT = 2, KERNEL_PERSISTENT192 = 3;
 constexpr int KERNEL_PERSISTENT_AUTO = 4;  // internal: the persistent kernel with the tile rows chosen as by auto
+// the s9 (three-barrier) schedule of the persistent kernel: tile rows by auto / 256 / 192
+constexpr int KERNEL_S9_AUTO = 5, KERNEL_S9 = 6, KERNEL_S9_192 = 7, KERNEL_MAX = 7;
+
+// dynamic-LDS opt-in of one persistent instantiation, once per process
+template <int EPI, bool PANEL, int MI, int SCHED>
+void s8_attr() {
+  static const bool once = [] {
+    (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI, PANEL, MI, SCHED>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, S7_LDS);
+    return true;
+  }();
+  (void)once;
+}
+
+template <int EPI, bool PANEL, int MI, int SCHED>
+void s8_launch(const GemmArgs& g, int batch, dim3 grid, hipStream_t st) {
+  s8_attr<EPI, PANEL, MI, SCHED>();
+  hipLaunchKernelGGL((gemm_s8_kernel<EPI, PANEL, MI, SCHED>), grid, dim3(256), S7_LDS, st, g, batch);
+}
+
+// the persistent schedule auto picks (SA_GEMM_SCHED=8|9 overrides, read once per process)
+int env_sched() {
+  static const int sc = [] {
+    const char* e = getenv("SA_GEMM_SCHED");
+    return (e && atoi(e) == 8) ? 8 : (e && atoi(e) == 9) ? 9 : SA_GEMM_SCHED_DEFAULT;
+  }();
+  return sc;
+}
 
 int num_cus() {
   // per device: the persistent grid is one workgroup per CU
@@ -832,17 +968,8 @@ int env_group_m() {
 
 template <int EPI>
 int launch(const GemmArgs& g_in, int batch, int kernel, hipStream_t st) {
-  // one-time per epilogue instantiation: allow the dynamic LDS sizes (idempotent, thread-safe init)
+  // one-time per epilogue instantiation: allow the ping-pong kernel's dynamic LDS size
   static const bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, S7_LDS);
-    (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI, false, 6>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              S7_LDS);
-    if constexpr (EPI == EPI_RES_F32) {
-      (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                S7_LDS);
-      (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI, true, 6>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                S7_LDS);
-    }
     (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
     return true;
@@ -854,35 +981,38 @@ int launch(const GemmArgs& g_in, int batch, int kernel, hipStream_t st) {
   // cross-Q +7-10 %, FFN-up +3-4 %, FFN-down +4 %, O-proj +-1 %), else the ping-pong kernel (e.g. the
   // K = 192 patch embedding)
   const bool persistent_ok = g.K % 128 == 0 && (long)BM * g.lda * 2 < 0x7fffffffL && (long)BN * g.ldw * 2 < 0x7fffffffL;
-  const bool forced = kernel == KERNEL_PERSISTENT || kernel == KERNEL_PERSISTENT192 || kernel == KERNEL_PERSISTENT_AUTO;
+  const bool s9 = kernel >= KERNEL_S9_AUTO;
+  const bool forced = kernel == KERNEL_PERSISTENT || kernel == KERNEL_PERSISTENT192 || kernel == KERNEL_PERSISTENT_AUTO || s9;
   if (forced && !persistent_ok) return SA_ERR_ARG;
   const bool persistent = forced || (kernel == KERNEL_AUTO && persistent_ok);
+  const int sched = s9 ? 9 : (kernel == KERNEL_PERSISTENT || kernel == KERNEL_PERSISTENT192) ? 8 : env_sched();
   constexpr bool BF16_OUT = EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16;
   if (g.group_m == 0) g.group_m = persistent ? (BF16_OUT ? 8 : 4) : (g.N >= 4096 ? 8 : 1);
   const int nn = (g.N + BN - 1) / BN, ncu = num_cus();
   const long n256 = (long)((g.M + 255) / 256) * nn * batch, n192 = (long)((g.M + 191) / 192) * nn * batch;
   // persistent tile rows: 192 where its rounds over the CUs, at 0.75 of a 256-row tile's work and a measured
   // per-FLOP cost of SA_T192_COST, finish first (the per-rank shapes of sequence parallelism)
-  bool t192 = kernel == KERNEL_PERSISTENT192;
-  if ((kernel == KERNEL_AUTO || kernel == KERNEL_PERSISTENT_AUTO) && persistent)
+  bool t192 = kernel == KERNEL_PERSISTENT192 || kernel == KERNEL_S9_192;
+  if ((kernel == KERNEL_AUTO || kernel == KERNEL_PERSISTENT_AUTO || kernel == KERNEL_S9_AUTO) && persistent)
     t192 = (double)((n192 + ncu - 1) / ncu) * 0.75 * SA_T192_COST < (double)((n256 + ncu - 1) / ncu);
   const int nm = t192 ? (g.M + 191) / 192 : (g.M + BM - 1) / BM;
   const dim3 pgrid(min(nm * nn * batch, ncu));
   if (g.a_pmul) {  // column-panel A: the O-projection of the sequence-parallel path only
     if constexpr (EPI == EPI_RES_F32) {
       if (t192)
-        hipLaunchKernelGGL((gemm_s8_kernel<EPI, true, 6>), pgrid, dim3(256), S7_LDS, st, g, batch);
+        sched == 9 ? s8_launch<EPI, true, 6, 9>(g, batch, pgrid, st) : s8_launch<EPI, true, 6, 8>(g, batch, pgrid, st);
       else
-        hipLaunchKernelGGL((gemm_s8_kernel<EPI, true>), pgrid, dim3(256), S7_LDS, st, g, batch);
+        sched == 9 ? s8_launch<EPI, true, 8, 9>(g, batch, pgrid, st) : s8_launch<EPI, true, 8, 8>(g, batch, pgrid, st);
     } else {
       return SA_ERR_ARG;
     }
-  } else if (persistent && t192)
-    hipLaunchKernelGGL((gemm_s8_kernel<EPI, false, 6>), pgrid, dim3(256), S7_LDS, st, g, batch);
-  else if (persistent)
-    hipLaunchKernelGGL(gemm_s8_kernel<EPI>, pgrid, dim3(256), S7_LDS, st, g, batch);
-  else
+  } else if (persistent && t192) {
+    sched == 9 ? s8_launch<EPI, false, 6, 9>(g, batch, pgrid, st) : s8_launch<EPI, false, 6, 8>(g, batch, pgrid, st);
+  } else if (persistent) {
+    sched == 9 ? s8_launch<EPI, false, 8, 9>(g, batch, pgrid, st) : s8_launch<EPI, false, 8, 8>(g, batch, pgrid, st);
+  } else {
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, true>), dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
+  }
   SA_LAUNCH_CHECK();
   return SA_OK;
 }
@@ -903,7 +1033,7 @@ extern "C" int sa_gemm_bf16_panels(const void* A, int64_t lda, int64_t strideA, 
   if (K % BK != 0 || lda % 8 != 0 || ldw % 8 != 0) return SA_ERR_ARG;
   if ((((uintptr_t)A) & 15) || (((uintptr_t)W) & 15)) return SA_ERR_ARG;
   if (epilogue == EPI_RES_F32 && (!residual || (gate && rows_per_batch <= 0))) return SA_ERR_ARG;
-  if (kernel < KERNEL_AUTO || kernel > KERNEL_PERSISTENT192 || group_m < 0) return SA_ERR_ARG;
+  if (kernel < KERNEL_AUTO || kernel > KERNEL_MAX || kernel == KERNEL_PERSISTENT_AUTO || group_m < 0) return SA_ERR_ARG;
   GemmArgs g{(const bf16*)A, lda, strideA, (const bf16*)W, ldw, strideW, bias, C, ldc, strideC,
              residual, ldr, strideR, gate, gate_bstride, rows_per_batch > 0 ? rows_per_batch : 1, M, N, K,
              group_m > 0 ? group_m : env_group_m(), 0u, 0, 0};

@@ -243,7 +243,7 @@ def all_gather_slots(buf: torch.Tensor, rank: int, group=None) -> Pending:
         else:
             dist.all_gather_into_tensor(buf, mine.clone(), group=group)
         return Pending(None, None)
-    return Pending(dist.all_gather_into_tensor(buf, mine, group=group, async_op=True), None)
+    return Pending([dist.all_gather_into_tensor(buf, mine, group=group, async_op=True)], None)
 
 
 def gather_tokens(local: torch.Tensor, B: int, Lc: int, world: int, group=None) -> torch.Tensor:

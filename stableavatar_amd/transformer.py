@@ -555,6 +555,90 @@ class WanTransformer3DFantasyModel(nn.Module):
         ops.layernorm_mod(x, hb, 1e-6, shift=ef[0, 0, 0:1], scale=ef[0, 0, 1:2], rows_per_batch=Mv)
         return ops.linear(hb, V.w_fp, V.b_fp, ops.EPI_BF16), Fn, nper
 
+    # ------------------------------------------------------------------ sequence parallel, one stream per CFG row
+
+    def _row_streams(self, B, dev):
+        """B HIP streams (one per CFG row) for the SP_OVERLAP=4 layer schedule, kept per device"""
+        st = getattr(self, "_rstreams", None)
+        if st is None or len(st) < B or st[0].device != dev:
+            st = self._rstreams = [torch.cuda.Stream(dev) for _ in range(B)]
+        return st[:B]
+
+    def _row_cross_segs(self, B, Lc, ctx, voc_list, dev):
+        """per-row cross-attention segment tables (query rows relative to the row's chunk, key rows absolute in the
+        shared text / image / vocal K|V buffers) for the three-launch path"""
+        out = []
+        for b in range(B):
+            txt = self._segs.get(("rtxt", b, Lc, ctx.text_len), [[0, Lc, b * ctx.text_len, ctx.text_len]], dev)
+            img = self._segs.get(("rimg", b, Lc, ctx.img_len), [[0, Lc, b * ctx.img_len, ctx.img_len]], dev)
+            vl = [[q0 - b * Lc, ql, k0, kl] for q0, ql, k0, kl in voc_list if b * Lc <= q0 < (b + 1) * Lc]
+            voc = self._segs.get(("rvoc", b, Lc, tuple(map(tuple, vl))), vl, dev)
+            out.append((txt, img, voc, len(vl), max(s_[1] for s_ in vl)))
+        return out
+
+    def _sp_layer_rows(self, pk, L, li, x, ws, em, ex, pack_kw, rank, Lc, Lq, hg, hgd, grid, segs_rows, row_segs,
+                       ctx, vctx, kvv, nper, Gf, n_fr, use_cross3, rstreams):
+        """One DiT block (1B:650-695) with Ulysses sequence parallelism, each CFG row on its own stream
+        (SA_SP_OVERLAP=4): row b's Q/K/V exchange (wan_xfuser.py:102-107) travels while the other rows compute
+        (their QKV GEMMs, attention, O-projection, cross-attention and FFN), and its head-output exchange travels
+        under the other rows' attention and FFN.  The host issues the phases of the three rows interleaved
+        (QKV+pack+send for every row, then attention+send back for every row, then the rest of the block), so the
+        transport sees the same order of transfers on every rank.  Per-row kernels are the batched ones applied to
+        row slices: the output is bit-identical to the batched schedule."""
+        dim, H_, eps = self.dim, self.num_heads, self.eps
+        B = len(rstreams)
+        rope_kw = dict(rope=pk.rope, rows_per_batch=Lc, tok_offset=rank * Lc, grid=grid, head_dim=self.d,
+                       n_frame_pairs=self.d // 2 - 2 * (self.d // 6), n_height_pairs=self.d // 6)
+        tl, ni = ctx.text_len, ctx.img_len
+        kvt, kvi = ctx.kv[li]
+        nv = n_fr * nper
+        pend, back = [], []
+        for b, st in enumerate(rstreams):  # self-attention inputs (1B:675-676) and the Q/K/V exchange
+            rs = slice(b * Lc, (b + 1) * Lc)
+            with torch.cuda.stream(st):
+                ops.layernorm_mod(x[rs], ws.mod[rs], eps, shift=em[b:b + 1, 0], scale=em[b:b + 1, 1],
+                                  rows_per_batch=Lc)
+                ops.linear(ws.mod[rs], L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv[rs])
+                ops.qkv_pack(ws.qkv[rs], L.nq, L.nk, dim, eps, b_offset=b, **pack_kw, **rope_kw)
+                pend.append(ex.heads([b]))
+        for b, st in enumerate(rstreams):  # attention over the full key sequence, head outputs back to the owners
+            with torch.cuda.stream(st):
+                pend[b].wait()
+                ev0 = self._record_event()
+                ops.attention(ex.q, ex.kv[:, :hgd], ex.kv[:, hgd:], ex.obuf, segs_rows[b], 1, Lq, hg,
+                              kernel=self.attn_kernel, o_rows=ex.omap)
+                self._record_span(ev0, rows=1, batch=B)
+                back.append(ex.tokens([b]))
+        for b, st in enumerate(rstreams):  # O-projection + gated residual, cross-attention, FFN (1B:677-691)
+            rs = slice(b * Lc, (b + 1) * Lc)
+            xr, mod, att = x[rs], ws.mod[rs], ws.att[rs]
+            with torch.cuda.stream(st):
+                back[b].wait()
+                a0, pnl = ex.panels(range(b, b + 1))
+                ops.linear(a0, L.w_o, L.b_o, ops.EPI_RES_F32, out=xr, residual=xr, gate=em[b:b + 1, 2],
+                           rows_per_batch=Lc, a_panels=pnl)
+                ops.layernorm_mod(xr, mod, eps, weight=L.n3w, bias=L.n3b)
+                qc = ws.qkv[rs, :dim]
+                ops.linear(mod, L.w_cq, L.b_cq, ops.EPI_BF16, out=qc)
+                ops.qk_rmsnorm_rope(qc, 0, -1, L.cnq, None, dim, eps)
+                kv_b = kvv[b * nv:(b + 1) * nv]
+                ops.linear(vctx[b * nv:(b + 1) * nv], L.w_kv_v, L.b_kv_v, ops.EPI_BF16, out=kv_b)
+                if use_cross3:
+                    kt, ki = kvt[b * tl:(b + 1) * tl], kvi[b * ni:(b + 1) * ni]
+                    ops.attention_cross3(qc, kt[:, :dim], kt[:, dim:], tl, ki[:, :dim], ki[:, dim:], ni, kv_b[:, :dim],
+                                         kv_b[:, dim:], nper, Gf, n_fr, att, 1, Lc, H_, tok_offset=rank * Lc)
+                else:
+                    s_txt, s_img, s_voc, n_voc, q_voc = row_segs[b]
+                    ops.attention(qc, kvt[:, :dim], kvt[:, dim:], att, s_txt, 1, Lc, H_)
+                    if kvi is not None:
+                        ops.attention(qc, kvi[:, :dim], kvi[:, dim:], att, s_img, 1, Lc, H_, accumulate=True)
+                    ops.attention(qc, kvv[:, :dim], kvv[:, dim:], att, s_voc, n_voc, q_voc, H_, accumulate=True)
+                ops.linear(att, L.w_co, L.b_co, ops.EPI_RES_F32, out=xr, residual=xr)
+                ops.layernorm_mod(xr, mod, eps, shift=em[b:b + 1, 3], scale=em[b:b + 1, 4], rows_per_batch=Lc)
+                ops.linear(mod, L.w_f0, L.b_f0, ops.EPI_GELU_TANH_BF16, out=ws.ffn[rs])
+                ops.linear(ws.ffn[rs], L.w_f2, L.b_f2, ops.EPI_RES_F32, out=xr, residual=xr, gate=em[b:b + 1, 5],
+                           rows_per_batch=Lc)
+
     # ------------------------------------------------------------------ timing hooks (bench.py)
 
     def _record_event(self):
@@ -704,14 +788,21 @@ class WanTransformer3DFantasyModel(nn.Module):
                 n_cu = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 256
                 wg_row = -(-Lq // 256) * hg
                 ov = os.environ.get("SA_SP_OVERLAP", "1")
-                if ov == "1":
+                if ov == "1" and B > 1 and dev.type == "cuda":
+                    # one stream per CFG row through the whole block: its compute alone matches the best of the
+                    # other schedules at every degree (per-rank forward with the transfers stubbed out, N = 2 / 4 / 8:
+                    # 197.2 / 103.3 / 59.3 ms vs 198.5 / 103.8 / 59.0 ms, profiles/r04/sp_rank_compute_r4s.jsonl)
+                    # and every transfer travels under the other rows' work
+                    ov = "4"
+                elif ov == "1":
                     ov = "2" if B * -(-wg_row // n_cu) <= -(-(B * wg_row) // n_cu) else "3"
                 sp_rows, sp_rows_x = ov == "2", ov == "3" and B > 1
-                if sp_rows:
+                sp_streams = ov == "4" and B > 1 and dev.type == "cuda"
+                if sp_rows or sp_streams:
                     segs_rows = [self._segs.get(("self_sp_row", b, Lp, Lq, S), [[b * Lq, Lq, b * Lp, S]], dev)
                                  for b in range(B)]
             else:
-                sp_rows = sp_rows_x = False
+                sp_rows = sp_rows_x = sp_streams = False
                 segs_self = self._segs.get(("self", B, Lp), [[b * Lp, Lp, b * Lp, Lp] for b in range(B)], dev)
             segs_txt = self._segs.get(("txt", B, Lc, ctx.text_len), sp.local_segments(B, Lc, ctx.text_len), dev)
             segs_img = self._segs.get(("img", B, Lc, ctx.img_len), sp.local_segments(B, Lc, ctx.img_len), dev)
@@ -723,7 +814,18 @@ class WanTransformer3DFantasyModel(nn.Module):
             x = ws.x
             kvv = torch.empty(B * n_fr * nper, 2 * dim, device=dev, dtype=torch.bfloat16)  # per-frame vocal K|V
             grid = (Fw, hp, wp)
+            if sp_streams:
+                # every CFG row through the whole layer on its own HIP stream (_sp_layer_rows); rows are independent
+                rstreams = self._row_streams(B, dev)
+                main = torch.cuda.current_stream(dev)
+                for rs_ in rstreams:
+                    rs_.wait_stream(main)
+                row_segs = self._row_cross_segs(B, Lc, ctx, voc_list, dev)
             for li, L in enumerate(pk.layers):
+                if sp_streams:
+                    self._sp_layer_rows(pk, L, li, x, ws, emod[li], ex, pack_kw, rank, Lc, Lq, hg, hgd, grid,
+                                        segs_rows, row_segs, ctx, vctx, kvv, nper, G, n_fr, use_cross3, rstreams)
+                    continue
                 em = emod[li]  # [B, 6, dim]
                 # self-attention (1B:675-679)
                 ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 0], scale=em[:, 1], rows_per_batch=Lc)
@@ -810,6 +912,9 @@ class WanTransformer3DFantasyModel(nn.Module):
                 ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 3], scale=em[:, 4], rows_per_batch=Lc)
                 ops.linear(ws.mod, L.w_f0, L.b_f0, ops.EPI_GELU_TANH_BF16, out=ws.ffn)
                 ops.linear(ws.ffn, L.w_f2, L.b_f2, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 5], rows_per_batch=Lc)
+            if sp_streams:
+                for rs_ in rstreams:
+                    main.wait_stream(rs_)
             if tc is not None:  # 1B:1096-1099
                 tc.store(ws.x - x_in, cond_flag)
                 del x_in

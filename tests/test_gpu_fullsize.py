@@ -141,10 +141,12 @@ def test_dit_gemm_fullsize(name, N, K, epi):
     # the 192-row persistent tiles (picked by auto for the sequence-parallel per-rank shapes) accumulate every
     # output in the same K order: bit-identical, here at M = 64 512, at the N = 8 per-rank M = 8 064, and at M
     # with a partial last tile of either height (12 285 = the per-rank M at 480x832, N = 8; 1 000)
+    # and the three-barrier K schedule (GEMM_S9*, auto's default) computes the same products in the same order
     for Mx in (M, 3 * 2688, 3 * 4095, 1000):
         y2 = torch.empty(Mx, N, device=dev, dtype=y.dtype)
-        y3 = torch.empty_like(y2)
-        for yy, kern in ((y2, ops.GEMM_PERSISTENT), (y3, ops.GEMM_PERSISTENT192)):
+        outs = [torch.empty_like(y2) for _ in range(3)]
+        for yy, kern in ((y2, ops.GEMM_PERSISTENT), (outs[0], ops.GEMM_PERSISTENT192), (outs[1], ops.GEMM_S9),
+                         (outs[2], ops.GEMM_S9_192)):
             if epi == "bf16":
                 ops.linear(x[:Mx], w, b, ops.EPI_BF16, out=yy, kernel=kern)
             elif epi == "gelu":
@@ -153,7 +155,8 @@ def test_dit_gemm_fullsize(name, N, K, epi):
                 yy.copy_(res[:Mx])
                 ops.linear(x[:Mx], w, b, ops.EPI_RES_F32, out=yy, residual=yy, gate=gate, rows_per_batch=L, kernel=kern)
         torch.cuda.synchronize()
-        assert torch.equal(y2, y3), (name, Mx)
+        for i, y3 in enumerate(outs):
+            assert torch.equal(y2, y3), (name, Mx, i)
 
 
 @pytest.mark.timeout(600)

@@ -4,8 +4,8 @@ and at 8 the U4 x 2 query-split layout) and, at world 8, the 14B-width model (40
 dit14_small.npz, with the same tolerance as the single-GPU golden tests (rel-L2 <= 2e-2, cosine >= 0.9995).  Each
 run also matches the same process's single-GPU forward to 1e-3.  Cases: 'full' (80 tokens), 'short' (the padded
 last window), 'wide' (120 tokens); at world 8 the 80- and 84-token sequences are padded to a multiple of the
-degree (SP pads are queries only).  All three exchange schedules run (sync batched; per-row with per-row attention;
-per-row Q/K/V exchanges with one batched attention).  On RCCL the box's one GPU allows a single rank
+degree (SP pads are queries only).  All four exchange schedules run (sync batched; per-row with per-row attention;
+per-row Q/K/V exchanges with one batched attention; every CFG row through the whole block on its own stream).  On RCCL the box's one GPU allows a single rank
 (two RCCL ranks cannot share a device), so the RCCL tests run at degree 1 with loopback transfers (each rank's own
 chunk sent to itself): every send / receive, stream wait and all-gather of the exchange executes on RCCL."""
 import os
@@ -77,7 +77,7 @@ def _worker(rank, world, port, model, qret):
             es_gold, _ = _stats(single, gold)
             m.enable_multi_gpus_inference()
             # one batched exchange / per-row exchanges + per-row attention / per-row Q/K/V exchanges + batched attention
-            for ov in ("0", "2", "3"):
+            for ov in ("0", "2", "3", "4"):
                 os.environ["SA_SP_OVERLAP"] = ov
                 par = run(m, inp)
                 e_single = ((par - single).norm() / single.norm()).item()
@@ -146,7 +146,8 @@ def _rccl_worker(port, overlap, qret):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("overlap", ["0", "2", "3"], ids=["batched", "per_row_async", "row_exchange_batched_attn"])
+@pytest.mark.parametrize("overlap", ["0", "2", "3", "4"],
+                         ids=["batched", "per_row_async", "row_exchange_batched_attn", "row_streams"])
 def test_sp_rccl_path_degree1(overlap):
     ctx = mp.get_context("spawn")
     qret = ctx.Queue()
