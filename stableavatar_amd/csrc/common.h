@@ -48,6 +48,16 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   const float e = __builtin_amdgcn_exp2f(x * fmaf(c1, x * x, c0));
   return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+// gelu_tanh on a pair: the polynomial and the final product as packed f32 VALU (v_pk_mul / v_pk_fma: two
+// elements per instruction), the exp2 / rcp per element -- the same operations, so the same results
+__device__ __forceinline__ f32x2 gelu_tanh2(f32x2 x) {
+  const float c0 = -2.0f * 0.7978845608028654f * 1.4426950408889634f;
+  const float c1 = c0 * 0.044715f;
+  const f32x2 z = x * __builtin_elementwise_fma((f32x2){c1, c1}, x * x, (f32x2){c0, c0});
+  const f32x2 d = (f32x2){__builtin_amdgcn_exp2f(z[0]), __builtin_amdgcn_exp2f(z[1])} + (f32x2){1.0f, 1.0f};
+  return x * (f32x2){__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+}
 __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
 }

@@ -83,14 +83,25 @@ __device__ __forceinline__ void epi_row(const GemmArgs& g, float* v, long bz, in
       for (int j = 0; j < NC; ++j) v[j] += (gcol + j < g.N) ? g.bias[gcol + j] : 0.f;
     }
   }
+  if constexpr (EPI == EPI_GELU_BF16 && NC % 2 == 0) {
+    // pairs: the bf16 rounding of the Linear output (one v_cvt_pk per pair), then the packed GELU
 #pragma unroll
-  for (int j = 0; j < NC; ++j) {
-    // the reference's nn.Linear returns bf16 under autocast; GELU and the gated residual
-    // (1B:677-678,688-690) consume that rounded value
-    if (EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16 || EPI == EPI_RES_F32) v[j] = bf2f(f2bf(v[j]));
-    if (EPI == EPI_GELU_BF16) v[j] = gelu_tanh(v[j]);
-    if (EPI == EPI_GELU_ERF_BF16) v[j] = gelu_erf(v[j]);
-    if (EPI == EPI_SILU_F32) v[j] = silu(v[j]);
+    for (int j = 0; j < NC; j += 2) {
+      const bf16x2 h = __builtin_convertvector((f32x2){v[j], v[j + 1]}, bf16x2);
+      const f32x2 y = gelu_tanh2(__builtin_convertvector(h, f32x2));
+      v[j] = y[0];
+      v[j + 1] = y[1];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      // the reference's nn.Linear returns bf16 under autocast; GELU and the gated residual
+      // (1B:677-678,688-690) consume that rounded value
+      if (EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16 || EPI == EPI_RES_F32) v[j] = bf2f(f2bf(v[j]));
+      if (EPI == EPI_GELU_BF16) v[j] = gelu_tanh(v[j]);
+      if (EPI == EPI_GELU_ERF_BF16) v[j] = gelu_erf(v[j]);
+      if (EPI == EPI_SILU_F32) v[j] = silu(v[j]);
+    }
   }
   if (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16) {
     bf16* C = (bf16*)g.C + bz * g.sC + (long)grow * g.ldc + gcol;
