@@ -63,9 +63,12 @@ def parse(argv=None):
                         "the run at 600 s): the CPU baseline's config-1 leg, the VAE encode and --dit14 are "
                         "skipped, and say so in the JSON, when they would not fit")
     p.add_argument("--cpu-child", type=str, default=None, help=argparse.SUPPRESS)  # internal: CPU baseline process
-    p.add_argument("--vae-parallel", action="store_true",
-                   help="N>1 sp / window-dp: split the VAE decode over the ranks (default: every rank decodes "
-                        "the whole clip, as the reference does)")
+    p.add_argument("--vae-parallel", dest="vae_parallel", action="store_true", default=True,
+                   help="N>1 sp / window-dp: split the VAE decode over the ranks (the default since round 4: a "
+                        "wavefront of causal-cache hand-offs, bit-identical to one GPU)")
+    p.add_argument("--no-vae-parallel", dest="vae_parallel", action="store_false",
+                   help="every rank decodes the whole clip, as the reference does (wan_inference_long_pipeline.py"
+                        ":793-796)")
     p.add_argument("--replica-warmup", type=int, default=1,
                    help="sp mode: untimed replicas clips per rank after the layout switch, before the timed ones")
     p.add_argument("--mode", choices=("sp", "replicas", "window-dp"), default=None,

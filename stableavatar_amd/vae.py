@@ -220,8 +220,12 @@ class _ChainState:
             h = torch.empty(shape, dtype=like.dtype)
             dist.recv(h, self.prev_g, group=self.group)
             return h.to(like.device)
+        # RCCL: a one-op batch_isend_irecv group on the process group's communicator -- the primitive the sequence-
+        # parallel exchange and the degree-1 loopback test run (a bare irecv would set up a separate per-pair
+        # communicator lazily); the caller's stream waits for it, the host does not
         t = torch.empty(shape, dtype=like.dtype, device=like.device)
-        dist.irecv(t, self.prev_g, group=self.group).wait()
+        for w in dist.batch_isend_irecv([dist.P2POp(dist.irecv, t, group=self.group, group_peer=self.rank - 1)]):
+            w.wait()
         return t
 
     def put(self, key, val):
@@ -234,8 +238,11 @@ class _ChainState:
         if _gloo(self.group) and val.is_cuda:
             h = val.cpu()
             self.sends.append((dist.isend(h, self.next_g, group=self.group), h))
-        else:
+        elif _gloo(self.group):
             self.sends.append((dist.isend(val, self.next_g, group=self.group), val))
+        else:
+            ws = dist.batch_isend_irecv([dist.P2POp(dist.isend, val, group=self.group, group_peer=self.rank + 1)])
+            self.sends.append((ws[0] if len(ws) == 1 else None, val))
 
     def skip(self, key, like):
         prev = self.get(key, like)
@@ -245,7 +252,8 @@ class _ChainState:
 
     def finish(self):
         for w, _ in self.sends:
-            w.wait()
+            if w is not None:
+                w.wait()
         self.sends = []
 
 
