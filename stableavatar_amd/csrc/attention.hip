@@ -504,6 +504,100 @@ __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2]
   }
 }
 
+// the fused cross-attention's last block of a source with at most 32 keys left (the image's 257th key, the 32
+// vocal keys of a frame): attn_v6_block on key tiles 0-1 only -- half the QK^T / PV MFMAs and exponentials
+__device__ __forceinline__ float rowmax32_c0(const f32x4 (&S)[2][2], int qt) {
+  float m = vmax3(S[0][qt][0], S[0][qt][1], S[0][qt][2]);
+  m = vmax3(m, S[0][qt][3], S[1][qt][0]);
+  m = vmax3(m, S[1][qt][1], S[1][qt][2]);
+  m = vmax2(m, S[1][qt][3]);
+  const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+  m = vmax2(__uint_as_float(x[0]), __uint_as_float(x[1]));
+  const auto y = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+  return vmax2(__uint_as_float(y[0]), __uint_as_float(y[1]));
+}
+
+template <int KOFF, int VOFF>
+__device__ __forceinline__ void attn_half_block(V6State& st, const bf16x8 (&qf)[2][4], const uint32_t* ka,
+                                                const uint32_t* va, int kb, int kv_len, int g, bool first) {
+  f32x4 S[2][2];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) S[kt][qt] = st.negm4[qt];
+  u32x4 k0[4], k1[4];
+  v6_read_k<KOFF, 0>(k0, ka);
+  v6_read_k<KOFF, 1>(k1, ka);
+  wait_k4<4>(k0);
+#pragma unroll
+  for (int dc = 0; dc < 4; ++dc) {
+    S[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v6_as_bf8(k0[dc]), qf[0][dc], S[0][0], 0, 0, 0);
+    S[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v6_as_bf8(k0[dc]), qf[1][dc], S[0][1], 0, 0, 0);
+  }
+  wait_k4<0>(k1);
+#pragma unroll
+  for (int dc = 0; dc < 4; ++dc) {
+    S[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v6_as_bf8(k1[dc]), qf[0][dc], S[1][0], 0, 0, 0);
+    S[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v6_as_bf8(k1[dc]), qf[1][dc], S[1][1], 0, 0, 0);
+  }
+  u32x2 v0[8], v1[8];
+  v6_read_v<VOFF, 0, 0>(v0, va);
+  v6_read_v<VOFF, 0, 4>(v1, va);
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (kb * KVB + kt * 16 + 4 * g + i >= kv_len) { S[kt][0][i] = -INFINITY; S[kt][1][i] = -INFINITY; }
+  float lm = vmax3(S[0][0][0], S[0][0][1], S[0][0][2]);
+  lm = vmax3(lm, S[0][0][3], S[0][1][0]);
+  lm = vmax3(lm, S[0][1][1], S[0][1][2]);
+  lm = vmax3(lm, S[0][1][3], S[1][0][0]);
+  lm = vmax3(lm, S[1][0][1], S[1][0][2]);
+  lm = vmax3(lm, S[1][0][3], S[1][1][0]);
+  lm = vmax3(lm, S[1][1][1], S[1][1][2]);
+  lm = vmax2(lm, S[1][1][3]);
+  if (first || !__all(lm <= RESCALE_THR)) {  // wave-uniform
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const float mx = rowmax32_c0(S, qt);
+      const float delta = first ? mx : fmaxf(mx, 0.f);
+      if (!first) {
+        const float alpha = __builtin_amdgcn_exp2f(-delta);
+        st.L[qt] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) st.O[dt][qt][i] *= alpha;
+      }
+      st.negm[qt] -= delta;
+      st.negm4[qt] = (f32x4){st.negm[qt], st.negm[qt], st.negm[qt], st.negm[qt]};
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) S[kt][qt][i] -= delta;
+    }
+  }
+  bf16x8 pb[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pb[qt][j] = f2bf(__builtin_amdgcn_exp2f(S[0][qt][j]));
+      pb[qt][4 + j] = f2bf(__builtin_amdgcn_exp2f(S[1][qt][j]));
+    }
+  {
+    bf16x8 ones;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+    st.L[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[0], st.L[0], 0, 0, 0);
+    st.L[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[1], st.L[1], 0, 0, 0);
+  }
+  wait_v<8>(v0);
+  v6_mma_v(st.O, 0, v0, pb);
+  wait_v<0>(v1);
+  v6_mma_v(st.O, 4, v1, pb);
+}
+
 namespace {
 
 // NW = 8: 256 query rows per workgroup, waves w and w+4 share a SIMD (one workgroup per CU); NW = 4: 128
@@ -687,6 +781,9 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
   // (K rows chunk ^ (row & 15), V rows chunk ^ 2 (row & 7)); each wave moves 2 x 1-KB pieces of K and V
   const int nT = (a.t_len + KVB - 1) / KVB, nI = (a.i_len + KVB - 1) / KVB, nV = (a.nper + KVB - 1) / KVB;
   const int ntot = nT + nI + nV;
+  // staging by buffer descriptors over each source's rows of this batch row (rows past the source read as
+  // zeros and are masked): SGPR bases, per-lane 32-bit offsets, the block in soffset -- no 64-bit address math
+  // per block (the round-3 kernel formed clamped 64-bit row addresses for every piece of every block)
   int srow[2], kch[2], vch[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -694,26 +791,36 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
     kch[i] = r16 ^ (srow[i] & 15);
     vch[i] = r16 ^ ((srow[i] & 7) << 1);
   }
+  const long vrow0 = (long)(b * a.n_frames + frame) * a.nper;
+  const __amdgpu_buffer_rsrc_t rkt = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.kt + (long)b * a.t_len * a.ts + h * D), (short)0, (int)(((long)a.t_len - 1) * a.ts * 2 + 256), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rvt = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.vt + (long)b * a.t_len * a.ts + h * D), (short)0, (int)(((long)a.t_len - 1) * a.ts * 2 + 256), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rki = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.ki + (long)b * a.i_len * a.is + h * D), (short)0, (int)(((long)a.i_len - 1) * a.is * 2 + 256), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rvi = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.vi + (long)b * a.i_len * a.is + h * D), (short)0, (int)(((long)a.i_len - 1) * a.is * 2 + 256), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rkv = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.kv + vrow0 * a.vs + h * D), (short)0, (int)(((long)a.nper - 1) * a.vs * 2 + 256), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rvv = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.vv + vrow0 * a.vs + h * D), (short)0, (int)(((long)a.nper - 1) * a.vs * 2 + 256), 0x00020000);
+  const uint32_t lds_k = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + wave * 2 * 1024);
   auto stage = [&](int j, int buf) {
-    const bf16 *kb, *vb;
-    long st;
-    int row0, len, blk;
-    if (j < nT) {
-      kb = a.kt; vb = a.vt; st = a.ts; row0 = b * a.t_len; len = a.t_len; blk = j;
-    } else if (j < nT + nI) {
-      kb = a.ki; vb = a.vi; st = a.is; row0 = b * a.i_len; len = a.i_len; blk = j - nT;
-    } else {
-      kb = a.kv; vb = a.vv; st = a.vs; row0 = (b * a.n_frames + frame) * a.nper; len = a.nper; blk = j - nT - nI;
+    __amdgpu_buffer_rsrc_t rk = rkt, rv = rvt;
+    int st = (int)a.ts, blk = j;
+    if (j >= nT + nI) {
+      rk = rkv; rv = rvv; st = (int)a.vs; blk = j - nT - nI;
+    } else if (j >= nT) {
+      rk = rki; rv = rvi; st = (int)a.is; blk = j - nT;
     }
-    char* kbase = smem + buf * TILE_BYTES;
-    char* vbase = smem + X3_VBASE + buf * TILE_BYTES;
+    const int boff = blk * KVB * st * 2;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const long key = row0 + min(blk * KVB + srow[i], len - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(kb + key * st + h * D + kch[i] * 8),
-                                       LDS_PTR(kbase + (wave * 2 + i) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(vb + key * st + h * D + vch[i] * 8),
-                                       LDS_PTR(vbase + (wave * 2 + i) * 1024), 16, 0, 0);
+      const int rowoff = srow[i] * st * 2;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, LDS_PTR((uintptr_t)(lds_k + buf * TILE_BYTES + i * 1024)), 16,
+                                               rowoff + kch[i] * 16, boff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rv, LDS_PTR((uintptr_t)(lds_k + X3_VBASE + buf * TILE_BYTES + i * 1024)), 16, rowoff + vch[i] * 16, boff, 0, 0);
     }
   };
 
@@ -780,15 +887,35 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
     attn_v6_block<BUF * TILE_BYTES, BUF * TILE_BYTES, false>(st, qf, ka, va, kb, len, g, kb == 0);
     if (jj == nT - 1 || jj == nT + nI - 1 || jj == ntot - 1) finish(src);
   };
+  // the vocal stream's single block when a frame has at most 32 audio tokens (StableAvatar: 32): peeled out of
+  // the loop as a half block (key tiles 0-1: half the MFMAs and exponentials of a 64-key block)
+  const bool vhalf = nV == 1 && a.nper <= KVB / 2;
+  auto last_half = [&](int jj, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    attn_half_block<BUF * TILE_BYTES, BUF * TILE_BYTES>(st, qf, ka, va, 0, a.nper, g, true);
+    finish(2);
+  };
+  const int nloop = vhalf ? ntot - 1 : ntot;
   stage(0, 0);
   if (1 < ntot) stage(1, 1);
   if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-  for (int j = 0; j < ntot; j += 3) {
+  for (int j = 0; j < nloop; j += 3) {
     step(j, std::integral_constant<int, 0>{});
-    if (j + 1 >= ntot) break;
+    if (j + 1 >= nloop) break;
     step(j + 1, std::integral_constant<int, 1>{});
-    if (j + 2 >= ntot) break;
+    if (j + 2 >= nloop) break;
     step(j + 2, std::integral_constant<int, 2>{});
+  }
+  if (vhalf) {
+    const int jl = ntot - 1;
+    if (jl % 3 == 0)
+      last_half(jl, std::integral_constant<int, 0>{});
+    else if (jl % 3 == 1)
+      last_half(jl, std::integral_constant<int, 1>{});
+    else
+      last_half(jl, std::integral_constant<int, 2>{});
   }
 
   // 16-byte stores from permlane16-swapped column-group pairs, as the self-attention epilogue (T21)

@@ -114,8 +114,10 @@ def main(which=("gemm", "attn")):
                                           kvv[:, :H * D], kvv[:, H * D:], nper, L // nfr, nfr, o, B, L, H)
         ms = sorted(_time(fn, iters=20, warmup=3) for _ in range(5))[2]
         fl = 4.0 * B * H * L * D * (512 + 257 + nper)
+        import hashlib
         r = {"kernel": "attn_cross3", "ms": round(ms, 4), "tflops": round(fl / ms / 1e9, 1),
-             "out_sum": float(o.float().abs().sum())}
+             "out_sum": float(o.float().abs().sum()),
+             "out_sha": hashlib.sha256(o.view(torch.uint8).cpu().numpy().tobytes()).hexdigest()[:16]}
         res.append(r)
         print(json.dumps(r), flush=True)
     if "gemm" in which:
