@@ -36,6 +36,7 @@ def main(which=("gemm", "attn")):
                                       (M, 1536, 1536, ops.EPI_BF16, "cross_q"),
                                       (M, 8960, 1536, ops.EPI_GELU_TANH_BF16, "ffn_up"),
                                       (M, 1536, 8960, ops.EPI_RES_F32, "ffn_down"),
+                                      (M, 1536, 8960, ops.EPI_BF16, "ffn_down_bf16"),
                                       (8192, 8192, 8192, ops.EPI_BF16, "sq8192")]:
             if os.environ.get("SA_KB_SHAPES") and name not in os.environ["SA_KB_SHAPES"].split(","):
                 continue

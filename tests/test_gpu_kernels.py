@@ -109,7 +109,7 @@ def _ref_attn(q, k, v, scale):
 
 
 @pytest.mark.parametrize("kernel", [1, 2], ids=["wg256", "wg128"])
-@pytest.mark.parametrize("Lq,Lk", [(300, 300), (512, 257), (1024, 17), (64, 512)])
+@pytest.mark.parametrize("Lq,Lk", [(300, 300), (512, 257), (1024, 17), (64, 512), (256, 1000)])
 def test_attention_segments(Lq, Lk, kernel):
     from stableavatar_amd import ops
     B, H, D = 2, 3, 128
@@ -147,18 +147,27 @@ def test_attention_vocal_grouping():
             assert rel(o[i * G:(i + 1) * G, sl], ref) < 1e-2
 
 
-def test_attention_spike_rescale():
-    """force the online-softmax rescale branch: a late key with a huge score"""
+@pytest.mark.parametrize("kernel", [1, 2], ids=["wg256", "wg128"])
+def test_attention_spike_rescale(kernel):
+    """force the online-softmax rescale branch: late keys with huge scores, in the first and the second
+    32-key half of a block, and a ramp that rescales block after block"""
     from stableavatar_amd import ops
     L, D = 512, 128
     q = torch.randn(L, D, device=dev).bfloat16()
     k = torch.randn(L, D, device=dev).bfloat16()
-    k[400] = q[5] * 4
+    k[400] = q[5] * 4   # key 16 of block 6: first half
+    k[440] = q[9] * 4   # key 56 of block 6: second half
+    k[33] = q[9] * 2    # second half of the first block
+    ramp = torch.linspace(0.2, 3.0, L, device=dev)[:, None]
+    k[:, :] = (k.float() + ramp * q[17].float()).bfloat16()  # query 17's scores rise across the keys
     v = torch.randn(L, D, device=dev).bfloat16()
     o = torch.empty_like(q)
     segs = torch.tensor([[0, L, 0, L]], dtype=torch.int32, device=dev)
-    ops.attention(q, k, v, o, segs, 1, L, 1)
-    assert rel(o, _ref_attn(q, k, v, D ** -0.5)) < 1e-2
+    ops.attention(q, k, v, o, segs, 1, L, 1, kernel=kernel)
+    ref = _ref_attn(q, k, v, D ** -0.5)
+    assert rel(o, ref) < 1e-2
+    for r in (5, 9, 17):
+        assert rel(o[r], ref[r]) < 1e-2, r
 
 
 @pytest.mark.parametrize("tok_offset", [0, 256])
