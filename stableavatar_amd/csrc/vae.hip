@@ -14,7 +14,13 @@
 //  sa_transpose_bf16   : batched 2-D transpose (V -> V^T for the P·V GEMM)
 #include "common.h"
 
+#include <stdlib.h>
+
 #include <type_traits>
+
+#ifndef SA_CONV_DMA_DEFAULT
+#define SA_CONV_DMA_DEFAULT 1
+#endif
 
 namespace {
 
@@ -263,6 +269,221 @@ int launch_conv(const ConvArgs& a, hipStream_t st) {
   return SA_OK;
 }
 
+// ---- the same implicit GEMM with both operands staged by LDS-DMA (buffer_load_dwordx4 ... lds) into a
+// 3-stage ring instead of through VGPRs and ds_write_b128.  The register-staged kernel above spends the
+// LDS store path on 14 KB per K step per workgroup (ds_write_b128: ~13 cycles of the CU's store path per
+// wave-instruction, MI355X_MICROARCH.md LDS table) for 48 MFMAs per step at NT = 6.  Here each wave
+// issues 1-KB pieces (16 rows x 64 B): lane l loads row 16p + l/4, swizzled chunk (l%4) ^ ((row>>1)&3), so
+// the LDS image is the one swz64 reads.  Every (tile, tap) reads ONE input frame (a tile is 128 pixels of
+// one frame: the launcher requires H*W % 128 == 0), so a tap's descriptor spans exactly that frame (or the
+// causal cache frame, or nothing: num_records 0 reads zeros); padded taps point their lanes out of range.
+// Same (tap, channel chunk) K order and the same MFMA sequence per accumulator as conv3d_cl_kernel:
+// bit-identical output.  Stride-1 convs only (down == 0).
+template <int NT, int BMT, int NSTAGE>
+__device__ __forceinline__ void conv3d_dma_body(const ConvArgs& a) {
+  constexpr int BN = NT * 16;
+  constexpr int APW = BMT / 64;                  // A pieces (16 rows) per wave per step
+  constexpr int BPW = (NT + 3) / 4;              // B pieces per wave per step (pieces >= NT are dummies)
+  constexpr int PPS = APW + BPW;                 // DMA instructions per wave per step
+  constexpr int SBYTES = BMT * 64 + 4 * BPW * 1024;  // one stage: A tile then B pieces
+  constexpr uint32_t OOR = 0x80000000u;          // out-of-range offset: the load returns zeros
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const long m0 = (long)blockIdx.x * BMT;
+  const int n0 = blockIdx.y * BN;
+  const long HW = (long)a.H * a.W;
+  const int K = a.kt * a.kh * a.kw * a.Cin;
+  const int nk = K / BK, cpt = a.Cin / BK;
+  const int tile_t = (int)(m0 / HW);  // every row of the tile is in this frame
+  const long frame_bytes = (long)a.Hin * a.Win * a.Cin * 2;
+
+  // A lanes: pieces APW*w + j -> tile rows r = 16p + lane/4
+  int ah[APW], aw[APW];
+  uint32_t acol[APW];
+  bool aok[APW];
+#pragma unroll
+  for (int j = 0; j < APW; ++j) {
+    const int r = 16 * (APW * wave + j) + (lane >> 2);
+    const long m = m0 + r;
+    aok[j] = m < a.M;
+    const int p = (int)((aok[j] ? m : m0) % HW);
+    ah[j] = p / a.W;
+    aw[j] = p % a.W;
+    acol[j] = (uint32_t)(((lane & 3) ^ ((r >> 1) & 3)) << 4);
+  }
+  // B lanes: pieces w*BPW + j -> weight rows n0 + 16p + lane/4
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, (int)((long)gridDim.y * BN * K * 2), 0x00020000);
+  uint32_t boff[BPW];
+#pragma unroll
+  for (int j = 0; j < BPW; ++j) {
+    const int p = wave * BPW + j;
+    const int r = 16 * p + (lane >> 2);
+    boff[j] = p < NT ? (uint32_t)((long)(n0 + r) * K * 2 + ((((lane & 3) ^ ((r >> 1) & 3))) << 4)) : OOR;
+  }
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem));
+
+  // issue side: (tap, channel chunk) of the next step to load, its frame descriptor and A lane offsets
+  int ld_tap = -1, ld_ci = 0, ld_ks = 0;
+  __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, 0, 0x00020000);
+  uint32_t aoff[APW];
+#pragma unroll
+  for (int j = 0; j < APW; ++j) aoff[j] = OOR;
+  auto set_tap = [&](int tap) {
+    const int dt = tap / (a.kh * a.kw), dh = (tap / a.kw) % a.kh, dw = tap % a.kw;
+    int ti = tile_t + dt - (a.kt - 1);
+    const bf16* fb = nullptr;
+    if (ti >= 0) {
+      fb = a.x + (long)ti * a.Hin * a.Win * a.Cin;
+    } else if (a.xprev) {
+      fb = a.xprev + (long)(ti + a.kt - 1) * a.Hin * a.Win * a.Cin;
+    }
+    rx = __builtin_amdgcn_make_buffer_rsrc((void*)(fb ? fb : a.x), (short)0, fb ? (int)frame_bytes : 0, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < APW; ++j) {
+      const int hi = ah[j] + dh - (a.kh - 1) / 2, wi = aw[j] + dw - (a.kw - 1) / 2;
+      const bool ok = aok[j] && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
+      const int hp = a.upsample ? (hi >> 1) : hi, wp = a.upsample ? (wi >> 1) : wi;
+      aoff[j] = ok ? (uint32_t)(((long)hp * a.Win + wp) * a.Cin * 2) + acol[j] : OOR;
+    }
+  };
+  auto issue = [&](int slot) {  // DMA of step ld_ks into ring slot `slot`
+    if (ld_ci == 0) set_tap(++ld_tap);
+    const uint32_t sb = lds0 + slot * SBYTES;
+#pragma unroll
+    for (int j = 0; j < APW; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, LDS_PTR((uintptr_t)(sb + (APW * wave + j) * 1024)), 16, aoff[j],
+                                               ld_ci * 2, 0, 0);
+#pragma unroll
+    for (int j = 0; j < BPW; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rw, LDS_PTR((uintptr_t)(sb + BMT * 64 + (wave * BPW + j) * 1024)), 16, boff[j], ld_ks * BK * 2, 0, 0);
+    ++ld_ks;
+    ld_ci += BK;
+    if (ld_ci == a.Cin) ld_ci = 0;
+  };
+
+  constexpr int WN = NT % 2 == 0 ? 2 : 1, WM = 4 / WN;
+  constexpr int AI = BMT / WM / 16, NB = NT / WN;
+  const int wm = wave / WN, wn = wave % WN;
+  f32x4 acc[AI][NB];
+#pragma unroll
+  for (int i = 0; i < AI; ++i)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) acc[i][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // steps ks+1 .. ks+NSTAGE-2 in flight while step ks is multiplied
+#pragma unroll
+  for (int s = 0; s < NSTAGE - 1; ++s)
+    if (s < nk) issue(s);
+  for (int ks = 0; ks < nk; ++ks) {
+    // step ks landed: at most the later issued steps' pieces still in flight
+    const int ahead = min(nk - 1 - ks, NSTAGE - 2);
+    if (ahead >= 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPS) : "memory");
+    else if (ahead == 1)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PPS) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // into the slot every wave finished reading at step ks - 1
+    if (ks + NSTAGE - 1 < nk) issue((ks + NSTAGE - 1) % NSTAGE);
+    const char* st = smem + (ks % NSTAGE) * SBYTES;
+    const int c = lane >> 4;
+    bf16x8 af[AI];
+#pragma unroll
+    for (int i = 0; i < AI; ++i) af[i] = *(const bf16x8*)(st + swz64(wm * AI * 16 + i * 16 + (lane & 15), c));
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const bf16x8 bfr = *(const bf16x8*)(st + BMT * 64 + swz64((wn * NB + n) * 16 + (lane & 15), c));
+#pragma unroll
+      for (int i = 0; i < AI; ++i) acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][n], 0, 0, 0);
+    }
+  }
+  (void)cpt;
+  __syncthreads();
+
+  // epilogue: as conv3d_cl_kernel
+  constexpr int LD = NB * 16 + 4;
+  float* strip = (float*)(smem + wave * 16 * LD * 4);
+  const int er = lane >> 2, q = lane & 3;
+  constexpr int CPL = NB * 4;
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) strip[((lane >> 4) * 4 + r) * LD + n * 16 + (lane & 15)] = acc[i][n][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const long m = m0 + wm * AI * 16 + i * 16 + er;
+    if (m < a.M) {
+      const long t = m / HW, p = m % HW;
+#pragma unroll
+      for (int g = 0; g < CPL; g += 4) {
+        const int n = n0 + wn * NB * 16 + q * CPL + g;
+        if (n < a.Cout) {
+          float v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = strip[er * LD + q * CPL + g + u] + a.bias[n + u];
+          long off;
+          if (a.ichalf > 0) {
+            const int half = n / a.ichalf, nc = n % a.ichalf;
+            off = ((2 * t + half) * HW + p) * a.ichalf + nc;
+          } else {
+            off = m * a.Cout + n;
+          }
+          if (a.res) {
+            const bf16x4 rr = *(const bf16x4*)(a.res + off);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] += bf2f(rr[u]);
+          }
+          if (a.out_f32) {
+            *(f32x4*)((float*)a.y + off) = (f32x4){v[0], v[1], v[2], v[3]};
+          } else {
+            *(bf16x4*)((bf16*)a.y + off) = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+          }
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// (the body is a device function: host compilation does not emit the stub of a kernel that declares buffer
+// resource variables itself)
+template <int NT, int BMT, int NSTAGE>
+__global__ __launch_bounds__(256, 2) void conv3d_dma_kernel(ConvArgs a) {
+  conv3d_dma_body<NT, BMT, NSTAGE>(a);
+}
+
+template <int NT, int BMT, int NSTAGE>
+int launch_conv_dma(const ConvArgs& a, hipStream_t st) {
+  constexpr int BN = NT * 16, BPW = (NT + 3) / 4;
+  const int lds_main = NSTAGE * (BMT * 64 + 4 * BPW * 1024);
+  const int lds_epi = 4 * 16 * (BN + 4) * 4;
+  const int lds = lds_main > lds_epi ? lds_main : lds_epi;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv3d_dma_kernel<NT, BMT, NSTAGE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              lds);
+    attr = true;
+  }
+  dim3 grid((unsigned)((a.M + BMT - 1) / BMT), (a.Cout + BN - 1) / BN);
+  hipLaunchKernelGGL((conv3d_dma_kernel<NT, BMT, NSTAGE>), grid, dim3(256), lds, st, a);
+  SA_LAUNCH_CHECK();
+  return SA_OK;
+}
+
+// SA_CONV_DMA=0 selects the register-staged kernel for every conv (A/B, read per call so a test can compare
+// both in one process); default: LDS-DMA where it applies
+int conv_dma_enabled() {
+  const char* e = getenv("SA_CONV_DMA");
+  return e ? atoi(e) : SA_CONV_DMA_DEFAULT;
+}
+
 // ---------------------------------------------------------------------------------------------
 
 // rows of C channels; G lanes per row (power of two >= C/8), 64/G rows per wave
@@ -383,6 +604,29 @@ extern "C" int sa_conv3d_cl(const void* x, int T, int H, int W, int Cin, int ups
              kt > 1 ? (const bf16*)x_prev : nullptr};
   hipStream_t st = (hipStream_t)stream;
   // N tile chosen so the packed weight rows (Cout_pad) cover whole tiles
+  const int dma = conv_dma_enabled();
+  if (dma && ((long)H * W) % BM == 0) {
+    // A/B variants (SA_CONV_DMA): 1 128-row tiles, 3-stage ring; 2 4 stages; 3 256-row tiles for the 96-wide
+    // and head convs; 4 = 3 with 4 stages; 5 = 3 with a 2-stage ring for the 192-wide; 6 = 3 with 2 stages
+    // for the 96-wide and head convs
+    const bool m256 = dma >= 3 && ((long)H * W) % 256 == 0;
+    if (Cout_pad % 192 == 0 && Cout > 96) {
+      if (dma == 2 || dma == 4) return launch_conv_dma<12, 128, 4>(a, st);
+      if (dma == 5) return launch_conv_dma<12, 128, 2>(a, st);
+      return launch_conv_dma<12, 128, 3>(a, st);
+    }
+    if (Cout_pad % 96 == 0 && Cout > 16) {
+      if (!m256) return dma == 2 ? launch_conv_dma<6, 128, 4>(a, st) : launch_conv_dma<6, 128, 3>(a, st);
+      if (dma == 4) return launch_conv_dma<6, 256, 4>(a, st);
+      if (dma == 6) return launch_conv_dma<6, 256, 2>(a, st);
+      return launch_conv_dma<6, 256, 3>(a, st);
+    }
+    if (Cout_pad % 16 == 0 && Cout <= 16) {
+      if (!m256) return launch_conv_dma<1, 128, 3>(a, st);
+      return dma == 6 ? launch_conv_dma<1, 256, 2>(a, st) : launch_conv_dma<1, 256, 3>(a, st);
+    }
+    return SA_ERR_ARG;
+  }
   if (Cout_pad % 192 == 0 && Cout > 96) return launch_conv<12>(a, st);
   if (Cout_pad % 96 == 0 && Cout > 16) return launch_conv<6>(a, st);
   if (Cout_pad % 16 == 0 && Cout <= 16) return launch_conv<1>(a, st);
