@@ -61,14 +61,21 @@ CASES = [
     (2, 16, 16, 96, 4, (3, 3, 3), {"out_f32": True}),
     (2, 16, 16, 32, 96, (1, 1, 1), {}),
     (2, 16, 16, 96, 192, (3, 1, 1), {"interleave": 96, "prev": True}),
+    # rows of >= 128 pixels: the A-strip kernel (variant 8) takes these
+    (2, 4, 128, 96, 96, (3, 3, 3), {"prev": True, "residual": True}),
+    (2, 4, 256, 96, 4, (3, 3, 3), {"out_f32": True}),
+    (2, 2, 128, 64, 96, (1, 3, 3), {"upsample": True}),
+    (3, 2, 128, 32, 192, (3, 3, 3), {}),
 ]
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6], ids=["m128s3", "m128s4", "m256s3", "m256s4", "v5", "v6"])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8],
+                         ids=["m128s3", "m128s4", "m256s3", "m256s4", "v5", "v6", "v7", "strip"])
 @pytest.mark.parametrize("case", range(len(CASES)))
 def test_conv_dma_vs_register_staged_and_torch(case, variant):
-    """SA_CONV_DMA variants: 1 = 128-row tiles, 3-stage ring (default); 2 = 4 stages; 3 / 4 = 256-row tiles
-    where H*W % 256 == 0 (96-wide and head convs)"""
+    """SA_CONV_DMA variants: 1 = 128-row tiles, 3-stage ring; 2 = 4 stages; 3 / 4 = 256-row tiles where
+    H*W % 256 == 0 (96-wide and head convs); 5-7 ring-depth / tile variants; 8 = the A-strip kernel where
+    kw = 3, Cin <= 96 and W % 128 == 0"""
     T, H, W, cin, cout, k, o = CASES[case]
     g = torch.Generator(device=dev).manual_seed(case)
     up = o.get("upsample", False)
@@ -88,3 +95,30 @@ def test_conv_dma_vs_register_staged_and_torch(case, variant):
     ref = _ref(x, T, H, W, cin, w, b, cout, k, residual=res, upsample=up, interleave=il, prev=prev)
     err = ((y_dma.float() - ref).norm() / ref.norm()).item()
     assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("C", [96, 192, 384])
+@pytest.mark.parametrize("silu", [0, 1])
+def test_rmsnorm3_bit_identical(C, silu):
+    """rmsnorm_silu3_kernel (every lane busy for C = 96 / 192 / 384) vs rmsnorm_silu_kernel: same sum order,
+    bit-identical; and vs torch RMS_norm (wan_vae.py:42-57: F.normalize * sqrt(C) * gamma) + SiLU"""
+    rows = 1000 + 37
+    g = torch.Generator(device=dev).manual_seed(C + silu)
+    x = (torch.randn(rows, C, device=dev, generator=g) * 3).bfloat16()
+    x[5] = 0  # an all-zero row: the 1e-12 clamp
+    gamma = torch.rand(C, device=dev, generator=g) + 0.5
+    outs = []
+    for v in ("1", "0"):
+        y = torch.empty_like(x)
+        os.environ["SA_RMS3"] = v
+        try:
+            call("sa_vae_rmsnorm_silu", x.data_ptr(), y.data_ptr(), gamma.data_ptr(), rows, C, silu, ops._stream())
+        finally:
+            os.environ.pop("SA_RMS3", None)
+        torch.cuda.synchronize()
+        outs.append(y)
+    assert torch.equal(outs[0], outs[1])
+    ref = F.normalize(x.float(), dim=1) * C ** 0.5 * gamma
+    if silu:
+        ref = F.silu(ref)
+    assert ((outs[0].float() - ref).norm() / ref.norm()).item() < 1e-2
