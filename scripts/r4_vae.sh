@@ -9,7 +9,7 @@ timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method threa
 rc=$?; grep -E "passed|failed|Error|assert" gpurun_out/t_$TAG.log | tail -8; [ $rc -ne 0 ] && exit $rc
 : > gpurun_out/kbvae_$TAG.jsonl
 # a variant "D" runs SA_CONV_DMA=D; "D:0" also sets SA_RMS3=0 (the lane-padded RMS-norm kernel)
-for r in 1 2; do for v in ${VARIANTS:-0 1}; do
+for r in 1 2; do for v in ${VARIANTS:-0 1 2}; do
   d=${v%%:*}; rms=1; [ "$v" != "$d" ] && rms=${v#*:}
   SA_CONV_DMA=$d SA_RMS3=$rms timeout -k 10 300 python scripts/kb_vae.py 3 2>/dev/null | sed "s/^{/{\"dma\": $d, \"rms3\": $rms, \"round\": $r, /" >> gpurun_out/kbvae_$TAG.jsonl
   rc=$?; [ $rc -ne 0 ] && { echo "kb_vae failed rc=$rc"; exit $rc; }

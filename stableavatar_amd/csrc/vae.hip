@@ -19,7 +19,7 @@
 #include <type_traits>
 
 #ifndef SA_CONV_DMA_DEFAULT
-#define SA_CONV_DMA_DEFAULT 1
+#define SA_CONV_DMA_DEFAULT 2
 #endif
 
 namespace {
@@ -494,164 +494,8 @@ int launch_conv_dma(const ConvArgs& a, hipStream_t st) {
   return SA_OK;
 }
 
-// ---- A-strip reuse across the kw taps (3-wide kernels whose 128-pixel tile lies in one image row).  For each
-// (dt, dh) the tile's A operand over the three kw taps is one 130-pixel strip of that input row, shifted by
-// 0 / 1 / 2 pixels: the strip of every channel chunk (Cin <= 96: at most 3 planes of 144 x 64 B) is DMA'd once
-// per (dt, dh) -- a group ahead, into the other of two strip buffers -- and the group's 3 x Cin/32 K steps read
-// their A fragments from it at row + dw.  B keeps the per-step 3-stage ring.  A DMA per group: 9 x Cin/32
-// pieces... 28 at Cin = 96 instead of 72.  The (tap, channel chunk) K order and the MFMA sequence are
-// conv3d_dma_kernel's (bit-identical).
-template <int NT, int CH>
-__device__ __forceinline__ void conv3d_strip_body(const ConvArgs& a) {
-  constexpr int BMT = 128, NSB = 3;
-  constexpr int BN = NT * 16;
-  constexpr int BPW = (NT + 3) / 4;
-  static_assert(NT % BPW == 0, "a wave holds all or none of its B pieces");
-  constexpr int PR = BMT + 16;                  // strip rows per plane (130 used), 9 pieces of 16
-  constexpr int SPIECES = ((CH * PR / 16) + 3) / 4 * 4, SPW = SPIECES / 4;  // strip pieces (padded), per wave
-  constexpr int STRIP_BYTES = SPIECES * 1024;
-  constexpr int BSTAGE = 4 * BPW * 1024;
-  constexpr uint32_t OOR = 0x80000000u;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const long m0 = (long)blockIdx.x * BMT;
-  const int n0 = blockIdx.y * BN;
-  const long HW = (long)a.H * a.W;
-  const int K = a.kt * a.kh * 3 * a.Cin;
-  const int nk = K / BK, spg = 3 * CH, ngroups = a.kt * a.kh;
-  const int tile_t = (int)(m0 / HW), p0 = (int)(m0 % HW);
-  const int tile_h = p0 / a.W, tile_w0 = p0 % a.W;
-  const long frame_bytes = (long)a.Hin * a.Win * a.Cin * 2;
-  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem));
-  const uint32_t bring = lds0 + 2 * STRIP_BYTES;
-
-  // B lanes (as conv3d_dma_body)
-  const __amdgpu_buffer_rsrc_t rw =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, (int)((long)gridDim.y * BN * K * 2), 0x00020000);
-  uint32_t boff[BPW];
-#pragma unroll
-  for (int j = 0; j < BPW; ++j) {
-    const int r = 16 * (wave * BPW + j) + (lane >> 2);
-    boff[j] = (uint32_t)((long)(n0 + r) * K * 2 + ((((lane & 3) ^ ((r >> 1) & 3))) << 4));
-  }
-  const bool bw = wave * BPW < NT;
-  int bks = 0;
-  auto issue_b = [&]() {  // B of step bks into ring slot bks % NSB
-    if (bw) {
-      const uint32_t sb = bring + (bks % NSB) * BSTAGE;
-#pragma unroll
-      for (int j = 0; j < BPW; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, LDS_PTR((uintptr_t)(sb + (wave * BPW + j) * 1024)), 16, boff[j],
-                                                 bks * BK * 2, 0, 0);
-    }
-    ++bks;
-  };
-  // strip of group g = (dt, dh) into buffer g & 1: piece P = wave * SPW + j -> plane P / 9, strip rows
-  // 16 (P % 9) + lane / 4 = input pixel (row tile_h + dh - 1, column tile_w0 + s - 1)
-  auto issue_strip = [&](int g) {
-    const int dt = g / a.kh, dh = g % a.kh;
-    const int ti = tile_t + dt - (a.kt - 1);
-    const bf16* fb = nullptr;
-    if (ti >= 0) {
-      fb = a.x + (long)ti * a.Hin * a.Win * a.Cin;
-    } else if (a.xprev) {
-      fb = a.xprev + (long)(ti + a.kt - 1) * a.Hin * a.Win * a.Cin;
-    }
-    const __amdgpu_buffer_rsrc_t rx =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(fb ? fb : a.x), (short)0, fb ? (int)frame_bytes : 0, 0x00020000);
-    const int hi = tile_h + dh - (a.kh - 1) / 2;
-    const bool row_ok = hi >= 0 && hi < a.H;
-    const int hp = a.upsample ? (hi >> 1) : hi;
-    const uint32_t sb = lds0 + (g & 1) * STRIP_BYTES;
-#pragma unroll
-    for (int j = 0; j < SPW; ++j) {
-      const int P = wave * SPW + j;
-      const int plane = P / (PR / 16), s = 16 * (P % (PR / 16)) + (lane >> 2);
-      const int wi = tile_w0 + s - 1;
-      const bool ok = row_ok && P < CH * (PR / 16) && s < BMT + 2 && wi >= 0 && wi < a.W;
-      const int wp = a.upsample ? (wi >> 1) : wi;
-      const uint32_t off = ok ? (uint32_t)(((long)hp * a.Win + wp) * a.Cin * 2) + plane * 64 +
-                                    (uint32_t)((((lane & 3) ^ ((s >> 1) & 3))) << 4)
-                              : OOR;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, LDS_PTR((uintptr_t)(sb + P * 1024)), 16, off, 0, 0, 0);
-    }
-  };
-
-  constexpr int WN = NT % 2 == 0 ? 2 : 1, WM = 4 / WN;
-  constexpr int AI = BMT / WM / 16, NB = NT / WN;
-  const int wm = wave / WN, wn = wave % WN;
-  f32x4 acc[AI][NB];
-#pragma unroll
-  for (int i = 0; i < AI; ++i)
-#pragma unroll
-    for (int n = 0; n < NB; ++n) acc[i][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  // issue order per wave: strip 0, B 0, B 1, then at step ks after its barrier: [strip g+1 at a group's first
-  // step], B ks+2.  At step ks's wait, B ks must have landed (and at a group's first step its strip, issued
-  // earlier); what may still be in flight: B ks+1 and a strip issued at step ks-1.
-  issue_strip(0);
-  issue_b();
-  if (nk > 1) issue_b();
-  const int c = lane >> 4;
-  for (int ks = 0; ks < nk; ++ks) {
-    const int g = ks / spg, q = ks % spg;
-    const bool strip_after = ks >= 1 && (ks - 1) % spg == 0 && (ks - 1) / spg + 1 < ngroups;
-    const bool b_after = ks + 1 < nk && bw;
-    if (b_after && strip_after)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(BPW + SPW) : "memory");
-    else if (b_after)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(BPW) : "memory");
-    else if (strip_after)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(SPW) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (q == 0 && g + 1 < ngroups) issue_strip(g + 1);  // the buffer group g - 1 read, free after this barrier
-    if (ks + 2 < nk) issue_b();
-    const int dw = q / CH, ci = q % CH;
-    const char* sa = smem + (g & 1) * STRIP_BYTES + ci * (PR * 64);
-    const char* sbp = smem + 2 * STRIP_BYTES + (ks % NSB) * BSTAGE;
-    bf16x8 af[AI];
-#pragma unroll
-    for (int i = 0; i < AI; ++i) af[i] = *(const bf16x8*)(sa + swz64(wm * AI * 16 + i * 16 + (lane & 15) + dw, c));
-#pragma unroll
-    for (int n = 0; n < NB; ++n) {
-      const bf16x8 bfr = *(const bf16x8*)(sbp + swz64((wn * NB + n) * 16 + (lane & 15), c));
-#pragma unroll
-      for (int i = 0; i < AI; ++i) acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][n], 0, 0, 0);
-    }
-  }
-  __syncthreads();
-  conv_epilogue<AI, NB>(a, acc, smem, m0, n0, HW, wm, wn, wave, lane);
-}
-
-template <int NT, int CH>
-__global__ __launch_bounds__(256, 2) void conv3d_strip_kernel(ConvArgs a) {
-  conv3d_strip_body<NT, CH>(a);
-}
-
-template <int NT, int CH>
-int launch_conv_strip(const ConvArgs& a, hipStream_t st) {
-  constexpr int BN = NT * 16, BPW = (NT + 3) / 4;
-  constexpr int SPIECES = ((CH * (BM + 16) / 16) + 3) / 4 * 4;
-  const int lds_main = 2 * SPIECES * 1024 + 3 * 4 * BPW * 1024;
-  const int lds_epi = 4 * 16 * (BN + 4) * 4;
-  const int lds = lds_main > lds_epi ? lds_main : lds_epi;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv3d_strip_kernel<NT, CH>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              lds);
-    attr = true;
-  }
-  dim3 grid((unsigned)((a.M + BM - 1) / BM), (a.Cout + BN - 1) / BN);
-  hipLaunchKernelGGL((conv3d_strip_kernel<NT, CH>), grid, dim3(256), lds, st, a);
-  SA_LAUNCH_CHECK();
-  return SA_OK;
-}
-
-// SA_CONV_DMA=0 selects the register-staged kernel for every conv (A/B, read per call so a test can compare
-// both in one process); default: LDS-DMA where it applies
+// SA_CONV_DMA (read per call so a test can compare the paths in one process): 0 the register-staged kernel for
+// every conv; 1 the LDS-DMA kernel on 128-row tiles; 2 (default) also 256-row tiles for the 96-wide / head convs
 int conv_dma_enabled() {
   const char* e = getenv("SA_CONV_DMA");
   return e ? atoi(e) : SA_CONV_DMA_DEFAULT;
@@ -821,39 +665,14 @@ extern "C" int sa_conv3d_cl(const void* x, int T, int H, int W, int Cin, int ups
   // N tile chosen so the packed weight rows (Cout_pad) cover whole tiles
   const int dma = conv_dma_enabled();
   if (dma && ((long)H * W) % BM == 0) {
-    // A/B variants (SA_CONV_DMA): 1 128-row tiles, 3-stage ring; 2 4 stages; 3 256-row tiles for the 96-wide
-    // and head convs; 4 = 3 with 4 stages; 5 = 3 with a 2-stage ring for the 192-wide; 6 = 3 with 2 stages
-    // for the 96-wide and head convs; 7 = 3 with 256-row, 2-stage tiles for the 192-wide
-    const bool m256 = dma >= 3 && ((long)H * W) % 256 == 0;
-    // 8: the A-strip kernel where it applies (kw = 3, Cin <= 96, 128-pixel tiles inside one image row), else 3
-    if (dma == 8 && kw == 3 && Cin <= 96 && W % BM == 0) {
-      const int ch = Cin / BK;
-      if (Cout_pad % 192 == 0 && Cout > 96)
-        return ch == 3 ? launch_conv_strip<12, 3>(a, st) : ch == 2 ? launch_conv_strip<12, 2>(a, st)
-                                                                     : launch_conv_strip<12, 1>(a, st);
-      if (Cout_pad % 96 == 0 && Cout > 16)
-        return ch == 3 ? launch_conv_strip<6, 3>(a, st) : ch == 2 ? launch_conv_strip<6, 2>(a, st)
-                                                                    : launch_conv_strip<6, 1>(a, st);
-      if (Cout_pad % 16 == 0 && Cout <= 16)
-        return ch == 3 ? launch_conv_strip<1, 3>(a, st) : ch == 2 ? launch_conv_strip<1, 2>(a, st)
-                                                                    : launch_conv_strip<1, 1>(a, st);
-    }
-    if (Cout_pad % 192 == 0 && Cout > 96) {
-      if (dma == 2 || dma == 4) return launch_conv_dma<12, 128, 4>(a, st);
-      if (dma == 5) return launch_conv_dma<12, 128, 2>(a, st);
-      if (dma == 7 && ((long)H * W) % 256 == 0) return launch_conv_dma<12, 256, 2>(a, st);
-      return launch_conv_dma<12, 128, 3>(a, st);
-    }
-    if (Cout_pad % 96 == 0 && Cout > 16) {
-      if (!m256) return dma == 2 ? launch_conv_dma<6, 128, 4>(a, st) : launch_conv_dma<6, 128, 3>(a, st);
-      if (dma == 4) return launch_conv_dma<6, 256, 4>(a, st);
-      if (dma == 6) return launch_conv_dma<6, 256, 2>(a, st);
-      return launch_conv_dma<6, 256, 3>(a, st);
-    }
-    if (Cout_pad % 16 == 0 && Cout <= 16) {
-      if (!m256) return launch_conv_dma<1, 128, 3>(a, st);
-      return dma == 6 ? launch_conv_dma<1, 256, 2>(a, st) : launch_conv_dma<1, 256, 3>(a, st);
-    }
+    // 256-row tiles for the 96-wide and head convs where a frame holds whole 256-pixel tiles (decode 241.5 vs
+    // 249.0 ms with 128-row tiles, SA_CONV_DMA=1; profiles/r04/README.md)
+    const bool m256 = dma == 2 && ((long)H * W) % 256 == 0;
+    if (Cout_pad % 192 == 0 && Cout > 96) return launch_conv_dma<12, 128, 3>(a, st);
+    if (Cout_pad % 96 == 0 && Cout > 16)
+      return m256 ? launch_conv_dma<6, 256, 3>(a, st) : launch_conv_dma<6, 128, 3>(a, st);
+    if (Cout_pad % 16 == 0 && Cout <= 16)
+      return m256 ? launch_conv_dma<1, 256, 3>(a, st) : launch_conv_dma<1, 128, 3>(a, st);
     return SA_ERR_ARG;
   }
   if (Cout_pad % 192 == 0 && Cout > 96) return launch_conv<12>(a, st);
