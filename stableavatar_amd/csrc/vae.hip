@@ -495,7 +495,7 @@ int launch_conv_dma(const ConvArgs& a, hipStream_t st) {
 }
 
 // SA_CONV_DMA (read per call so a test can compare the paths in one process): 0 the register-staged kernel for
-// every conv; 1 the LDS-DMA kernel on 128-row tiles; 2 (default) also 256-row tiles for the 96-wide / head convs
+// every conv; 1 the LDS-DMA kernel on 128-row tiles; 2 (default) 256-row tiles where a frame holds them
 int conv_dma_enabled() {
   const char* e = getenv("SA_CONV_DMA");
   return e ? atoi(e) : SA_CONV_DMA_DEFAULT;
@@ -665,12 +665,16 @@ extern "C" int sa_conv3d_cl(const void* x, int T, int H, int W, int Cin, int ups
   // N tile chosen so the packed weight rows (Cout_pad) cover whole tiles
   const int dma = conv_dma_enabled();
   if (dma && ((long)H * W) % BM == 0) {
-    // 256-row tiles for the 96-wide and head convs where a frame holds whole 256-pixel tiles (decode 241.5 vs
-    // 249.0 ms with 128-row tiles, SA_CONV_DMA=1; profiles/r04/README.md)
-    const bool m256 = dma == 2 && ((long)H * W) % 256 == 0;
-    if (Cout_pad % 192 == 0 && Cout > 96) return launch_conv_dma<12, 128, 3>(a, st);
-    if (Cout_pad % 96 == 0 && Cout > 16)
+    // 256-row tiles where a frame holds whole 256-pixel tiles: the 192-wide convs on a 2-stage ring (256 VGPRs,
+    // two workgroups per CU), the 96-wide and head convs on a 3-stage ring.  Decode 227 ms vs 239.5 with 128-row
+    // 192-wide tiles and 249 with 128-row tiles everywhere (SA_CONV_DMA=1); profiles/r04/README.md
+    const bool m256 = dma >= 2 && ((long)H * W) % 256 == 0;
+    if (Cout_pad % 192 == 0 && Cout > 96)
+      return m256 ? launch_conv_dma<12, 256, 2>(a, st) : launch_conv_dma<12, 128, 3>(a, st);
+    if (Cout_pad % 96 == 0 && Cout > 16) {
+      if (m256 && dma == 3) return launch_conv_dma<6, 256, 2>(a, st);  // A/B: 2-stage ring
       return m256 ? launch_conv_dma<6, 256, 3>(a, st) : launch_conv_dma<6, 128, 3>(a, st);
+    }
     if (Cout_pad % 16 == 0 && Cout <= 16)
       return m256 ? launch_conv_dma<1, 256, 3>(a, st) : launch_conv_dma<1, 128, 3>(a, st);
     return SA_ERR_ARG;
