@@ -671,10 +671,8 @@ extern "C" int sa_conv3d_cl(const void* x, int T, int H, int W, int Cin, int ups
     const bool m256 = dma >= 2 && ((long)H * W) % 256 == 0;
     if (Cout_pad % 192 == 0 && Cout > 96)
       return m256 ? launch_conv_dma<12, 256, 2>(a, st) : launch_conv_dma<12, 128, 3>(a, st);
-    if (Cout_pad % 96 == 0 && Cout > 16) {
-      if (m256 && dma == 3) return launch_conv_dma<6, 256, 2>(a, st);  // A/B: 2-stage ring
+    if (Cout_pad % 96 == 0 && Cout > 16)  // (a 2-stage ring here: 233.7 ms)
       return m256 ? launch_conv_dma<6, 256, 3>(a, st) : launch_conv_dma<6, 128, 3>(a, st);
-    }
     if (Cout_pad % 16 == 0 && Cout <= 16)
       return m256 ? launch_conv_dma<1, 256, 3>(a, st) : launch_conv_dma<1, 128, 3>(a, st);
     return SA_ERR_ARG;
