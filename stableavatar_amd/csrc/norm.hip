@@ -9,6 +9,10 @@
 #include "common.h"
 #include <cstdlib>
 
+#ifndef SA_LN_SHARED_DEFAULT
+#define SA_LN_SHARED_DEFAULT 8
+#endif
+
 namespace {
 
 template <typename TI>
@@ -76,7 +80,7 @@ __global__ __launch_bounds__(256) void layernorm_mod_kernel(LnArgs a) {
   for (int i = 0; i < MAXV; ++i)
     if (i < nch && (FIXED || i * 512 + lane * 8 < a.C)) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { const float d = v[i][j] - mean; q += d * d; }
+      for (int j = 0; j < 8; ++j) { const float d = v[i][j] - mean; q = __builtin_fmaf(d, d, q); }
     }
   const float rstd = rsqrtf(wave_sum(q) / a.C + a.eps);
   const long bo = (long)(row / a.rows_per_batch) * a.mod_bstride;
@@ -92,18 +96,18 @@ __global__ __launch_bounds__(256) void layernorm_mod_kernel(LnArgs a) {
         load8<float>(a.w + c0, w8);
         if (a.b) load8<float>(a.b + c0, b8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) y[j] = y[j] * w8[j] + (a.b ? b8[j] : 0.f);
+        for (int j = 0; j < 8; ++j) y[j] = __builtin_fmaf(y[j], w8[j], a.b ? b8[j] : 0.f);
       }
       if (a.scale) {
         load8<float>(a.scale + bo + c0, sc8);
         load8<float>(a.shift + bo + c0, sh8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) y[j] = y[j] * (1.f + sc8[j]) + sh8[j];
+        for (int j = 0; j < 8; ++j) y[j] = __builtin_fmaf(y[j], 1.f + sc8[j], sh8[j]);
       }
       if (a.gate) {
         load8<float>(a.gate + bo + c0, g8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) y[j] = v[i][j] + y[j] * g8[j];
+        for (int j = 0; j < 8; ++j) y[j] = __builtin_fmaf(y[j], g8[j], v[i][j]);
       }
       store8<TO>(out + c0, y);
     }
@@ -355,8 +359,97 @@ __global__ __launch_bounds__(256) void qkv_pack_kernel(PackArgs pa) {
   rms_rope_one<FIXED>(base + a.C, a.wk, a, lane, fi, hi_, wi, rot, PackOne<false>{&ps});
 }
 
+// The same LayerNorm with NW rows (one wave each) per workgroup sharing the per-batch modulation vectors
+// (affine w / b, AdaLN scale / shift, gate) through LDS: staged once per workgroup instead of every wave
+// reading up to 5 x C fp32 of them from L2 for its one row of C.  All NW rows lie in one batch row (the
+// launcher checks rows_per_batch % NW == 0).  Per-element arithmetic as layernorm_mod_kernel, every multiply-add
+// an explicit fma in both (so no contraction choice of the compiler's can tell them apart): bit-identical.
+template <typename TI, typename TO, int FIXED, int NW>
+__global__ __launch_bounds__(NW * 64) void layernorm_mod_shared_kernel(LnArgs a) {
+  constexpr int C = FIXED * 512;
+  __shared__ __attribute__((aligned(16))) float mod[5][C];
+  const int row0 = blockIdx.x * NW;
+  const long bo = (long)(row0 / a.rows_per_batch) * a.mod_bstride;
+  for (int i = threadIdx.x; i < C / 4; i += NW * 64) {
+    if (a.w) ((f32x4*)mod[0])[i] = ((const f32x4*)a.w)[i];
+    if (a.b) ((f32x4*)mod[1])[i] = ((const f32x4*)a.b)[i];
+    if (a.scale) {
+      ((f32x4*)mod[2])[i] = ((const f32x4*)(a.scale + bo))[i];
+      ((f32x4*)mod[3])[i] = ((const f32x4*)(a.shift + bo))[i];
+    }
+    if (a.gate) ((f32x4*)mod[4])[i] = ((const f32x4*)(a.gate + bo))[i];
+  }
+  __syncthreads();
+  const int row = row0 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= a.M) return;
+  const TI* x = (const TI*)a.x + (long)row * a.ldx;
+  float v[FIXED][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < FIXED; ++i) {
+    load8<TI>(x + i * 512 + lane * 8, v[i]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[i][j];
+  }
+  const float mean = wave_sum(s) / a.C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < FIXED; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { const float d = v[i][j] - mean; q = __builtin_fmaf(d, d, q); }
+  const float rstd = rsqrtf(wave_sum(q) / a.C + a.eps);
+  TO* out = (TO*)a.out + (long)row * a.ldo;
+#pragma unroll
+  for (int i = 0; i < FIXED; ++i) {
+    const int c0 = i * 512 + lane * 8;
+    float y[8], w8[8], b8[8], sc8[8], sh8[8], g8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) y[j] = (v[i][j] - mean) * rstd;
+    if (a.w) {
+      load8<float>(mod[0] + c0, w8);
+      if (a.b) load8<float>(mod[1] + c0, b8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y[j] = __builtin_fmaf(y[j], w8[j], a.b ? b8[j] : 0.f);
+    }
+    if (a.scale) {
+      load8<float>(mod[2] + c0, sc8);
+      load8<float>(mod[3] + c0, sh8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y[j] = __builtin_fmaf(y[j], 1.f + sc8[j], sh8[j]);
+    }
+    if (a.gate) {
+      load8<float>(mod[4] + c0, g8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y[j] = __builtin_fmaf(y[j], g8[j], v[i][j]);
+    }
+    store8<TO>(out + c0, y);
+  }
+}
+
+// SA_LN_SHARED: 0 one wave per row reading the modulation from L2 (layernorm_mod_kernel); 8 / 16 rows per
+// workgroup sharing it through LDS (read per call, for the A/B)
+inline int ln_shared_rows() {
+  const char* e = getenv("SA_LN_SHARED");
+  return e ? atoi(e) : SA_LN_SHARED_DEFAULT;
+}
+
 template <typename TI, typename TO>
 int launch_ln(const LnArgs& a, hipStream_t st) {
+  const int nw = ln_shared_rows();
+  const bool per_batch = a.scale || a.gate;  // batch-indexed vectors: a workgroup's rows must share the batch row
+  if (a.C == 1536 && nw > 0 && (!per_batch || a.rows_per_batch % nw == 0) && (per_batch || a.w)) {
+    if (nw == 16) {
+      hipLaunchKernelGGL((layernorm_mod_shared_kernel<TI, TO, 3, 16>), dim3((a.M + 15) / 16), dim3(1024), 0, st, a);
+      SA_LAUNCH_CHECK();
+      return SA_OK;
+    }
+    if (nw == 8) {
+      hipLaunchKernelGGL((layernorm_mod_shared_kernel<TI, TO, 3, 8>), dim3((a.M + 7) / 8), dim3(512), 0, st, a);
+      SA_LAUNCH_CHECK();
+      return SA_OK;
+    }
+  }
   if (a.C == 1536)
     hipLaunchKernelGGL((layernorm_mod_kernel<TI, TO, 3>), dim3((a.M + 3) / 4), dim3(256), 0, st, a);
   else if (a.C == 5120)

@@ -208,6 +208,29 @@ def main(which=("gemm", "attn")):
     if "dit14full" in which:  # BASELINE config 4's model: one whole 40-layer forward at 720p x 81 frames
         res.append(bench_dit14(layer_counts=(40,)))
         print(json.dumps(res[-1]), flush=True)
+    if "lnvar" in which:  # LayerNorm: one row per wave vs rows sharing the modulation through LDS (interleaved)
+        import os
+        x = torch.randn(M, 1536, device=dev)
+        em = torch.randn(3, 6, 1536, device=dev)
+        w, bb = torch.randn(1536, device=dev), torch.randn(1536, device=dev)
+        ob = torch.empty(M, 1536, device=dev, dtype=torch.bfloat16)
+        modes = {"adaln": dict(shift=em[:, 0], scale=em[:, 1], rows_per_batch=21504),
+                 "affine": dict(weight=w, bias=bb)}
+        nws = os.environ.get("SA_KB_LNVARS", "0,8,16").split(",")
+        for name, kw in modes.items():
+            times = {v: [] for v in nws}
+            for rnd in range(3):
+                for v in nws:
+                    os.environ["SA_LN_SHARED"] = v
+                    times[v].append(_time(lambda: ops.layernorm_mod(x, ob, 1e-6, **kw), iters=20, warmup=3))
+            os.environ.pop("SA_LN_SHARED", None)
+            r = {"kernel": f"layernorm_{name}", "M": M}
+            for v in nws:
+                ms = sorted(times[v])[1]
+                r[f"rows{v}_us"] = round(ms * 1e3, 1)
+                r[f"rows{v}_tbs"] = round(M * 1536 * 6 / ms / 1e9, 2)
+            res.append(r)
+            print(json.dumps(r), flush=True)
     if "ditvar" in which:  # in-situ A/B of attention variants inside full DiT forwards (interleaved)
         import os
         avars = tuple(int(v) for v in os.environ.get("SA_KB_AVARS", "1").split(","))

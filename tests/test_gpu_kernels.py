@@ -414,3 +414,35 @@ def test_attention_op_seam_drop_in(B, Lq, Lk, N, D):
     assert rel(out, ref) < 1e-2
     with pytest.raises(NotImplementedError):
         attention(q, k, v, causal=True)
+
+
+@pytest.mark.parametrize("in_bf16", [False, True])
+def test_layernorm_shared_modulation_bit_identical(in_bf16):
+    """layernorm_mod_shared_kernel (8 / 16 rows per workgroup sharing the modulation vectors through LDS) vs the
+    one-row-per-wave kernel: bit-identical in every mode the DiT uses (AdaLN modulate, affine, gated residual)"""
+    import os
+    from stableavatar_amd import ops
+    M, C, B, rpb = 1040, 1536, 2, 528  # 1040 = 65 x 16; rows_per_batch % 16 == 0
+    x = torch.randn(M, C, device=dev) * 3 + 1
+    if in_bf16:
+        x = x.bfloat16()
+    shift, scale, gate = (torch.randn(B, C, device=dev) for _ in range(3))
+    w, bb = torch.randn(C, device=dev), torch.randn(C, device=dev)
+    modes = [dict(shift=shift, scale=scale, rows_per_batch=rpb, dt=torch.bfloat16),
+             dict(weight=w, bias=bb, dt=torch.bfloat16), dict(weight=w, bias=bb, dt=torch.float32)]
+    if not in_bf16:
+        modes.append(dict(shift=shift, scale=scale, gate=gate, rows_per_batch=rpb, dt=torch.float32))
+    for mode in modes:
+        kw = dict(mode)
+        dt = kw.pop("dt")
+        outs = []
+        for nw in ("0", "8", "16"):
+            o = torch.empty(M, C, device=dev, dtype=dt)
+            os.environ["SA_LN_SHARED"] = nw
+            try:
+                ops.layernorm_mod(x, o, 1e-6, **kw)
+            finally:
+                os.environ.pop("SA_LN_SHARED", None)
+            torch.cuda.synchronize()
+            outs.append(o)
+        assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2]), sorted(kw)
