@@ -897,7 +897,17 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
     attn_half_block<BUF * TILE_BYTES, BUF * TILE_BYTES>(st, qf, ka, va, 0, a.nper, g, true);
     finish(2);
   };
-  const int nloop = vhalf ? ntot - 1 : ntot;
+  // likewise the image stream's last block when it holds at most 32 keys (CLIP: 257 = 4 x 64 + 1), when the vocal
+  // block is peeled too (so the loop still ends on a block boundary of the 3-stage ring)
+  const bool ihalf = vhalf && a.i_len % KVB != 0 && a.i_len % KVB <= KVB / 2;
+  auto img_half = [&](int jj, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // this block landed; the vocal block may still fly
+    __syncthreads();
+    attn_half_block<BUF * TILE_BYTES, BUF * TILE_BYTES>(st, qf, ka, va, nI - 1, a.i_len, g, nI == 1);
+    finish(1);
+  };
+  const int nloop = vhalf ? (ihalf ? ntot - 2 : ntot - 1) : ntot;
   stage(0, 0);
   if (1 < ntot) stage(1, 1);
   if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
@@ -907,6 +917,15 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
     step(j + 1, std::integral_constant<int, 1>{});
     if (j + 2 >= nloop) break;
     step(j + 2, std::integral_constant<int, 2>{});
+  }
+  if (ihalf) {
+    const int ji = ntot - 2;
+    if (ji % 3 == 0)
+      img_half(ji, std::integral_constant<int, 0>{});
+    else if (ji % 3 == 1)
+      img_half(ji, std::integral_constant<int, 1>{});
+    else
+      img_half(ji, std::integral_constant<int, 2>{});
   }
   if (vhalf) {
     const int jl = ntot - 1;
