@@ -370,6 +370,15 @@ __global__ __launch_bounds__(NW * 64) void layernorm_mod_shared_kernel(LnArgs a)
   __shared__ __attribute__((aligned(16))) float mod[5][C];
   const int row0 = blockIdx.x * NW;
   const long bo = (long)(row0 / a.rows_per_batch) * a.mod_bstride;
+  const int row = row0 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  // this wave's row is loaded before the staging barrier, so the HBM reads of every wave are in flight while
+  // the modulation vectors arrive from L2
+  const bool live = row < a.M;
+  const TI* x = (const TI*)a.x + (long)(live ? row : row0) * a.ldx;
+  float v[FIXED][8];
+#pragma unroll
+  for (int i = 0; i < FIXED; ++i) load8<TI>(x + i * 512 + lane * 8, v[i]);
   for (int i = threadIdx.x; i < C / 4; i += NW * 64) {
     if (a.w) ((f32x4*)mod[0])[i] = ((const f32x4*)a.w)[i];
     if (a.b) ((f32x4*)mod[1])[i] = ((const f32x4*)a.b)[i];
@@ -380,18 +389,12 @@ __global__ __launch_bounds__(NW * 64) void layernorm_mod_shared_kernel(LnArgs a)
     if (a.gate) ((f32x4*)mod[4])[i] = ((const f32x4*)(a.gate + bo))[i];
   }
   __syncthreads();
-  const int row = row0 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (row >= a.M) return;
-  const TI* x = (const TI*)a.x + (long)row * a.ldx;
-  float v[FIXED][8];
+  if (!live) return;
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < FIXED; ++i) {
-    load8<TI>(x + i * 512 + lane * 8, v[i]);
+  for (int i = 0; i < FIXED; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += v[i][j];
-  }
   const float mean = wave_sum(s) / a.C;
   float q = 0.f;
 #pragma unroll

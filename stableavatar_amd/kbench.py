@@ -231,6 +231,11 @@ def main(which=("gemm", "attn")):
                 r[f"rows{v}_tbs"] = round(M * 1536 * 6 / ms / 1e9, 2)
             res.append(r)
             print(json.dumps(r), flush=True)
+    if "ditenv" in which:  # in-situ A/B of an environment switch inside full DiT forwards (SA_KB_ENVVARS)
+        import os
+        res.append(bench_dit(env_variants=tuple(os.environ.get("SA_KB_ENVVARS", "SA_LN_SHARED=0,SA_LN_SHARED=8")
+                                                .split(","))))
+        print(json.dumps(res[-1]), flush=True)
     if "ditvar" in which:  # in-situ A/B of attention variants inside full DiT forwards (interleaved)
         import os
         avars = tuple(int(v) for v in os.environ.get("SA_KB_AVARS", "1").split(","))
@@ -284,7 +289,7 @@ def bench_dit14(layer_counts=(1, 2)):
             "tflops_forward_projected": round(fl_fwd / fwd40 / 1e9, 1)}
 
 
-def bench_dit(iters=3, attn_variants=None):
+def bench_dit(iters=3, attn_variants=None, env_variants=None):
     """One full 30-layer DiT forward at config 2 (B=3 CFG, 21 latent frames at 64x64, L=21504).
     attn_variants: time the forward under each self-attention schedule, interleaved rounds."""
     from . import synthetic
@@ -308,6 +313,20 @@ def bench_dit(iters=3, attn_variants=None):
 
     from .flops import dit_forward_flops
     fl = dit_forward_flops()
+    if env_variants:  # "K=V" settings of one environment switch read per call by the library, interleaved
+        import os
+        times = {v: [] for v in env_variants}
+        with torch.no_grad():
+            for _ in range(3):
+                for v in env_variants:
+                    k, _, val = v.partition("=")
+                    os.environ[k] = val
+                    times[v].append(_time(fwd, iters=2, warmup=1))
+                    os.environ.pop(k, None)
+        r = {"kernel": "dit_forward_env_ab", "tflop": round(fl / 1e12, 1)}
+        for v in env_variants:
+            r[f"{v}_ms"] = round(sorted(times[v])[1], 2)
+        return r
     if attn_variants:
         times = {v: [] for v in attn_variants}
         with torch.no_grad():
