@@ -751,23 +751,27 @@ __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
 // the text, image and per-frame vocal K/V streams one after the other through 3-stage K / V regions (each
 // block's DMA two blocks ahead), a separate online softmax per source (its first block sets the max), the
 // three bf16 outputs summed as the reference does
-__global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
+// NW waves x 32 queries per workgroup, NST-stage K / V ring (block j's DMA NST - 1 blocks ahead)
+template <int NW, int NST>
+__device__ __forceinline__ void attn_cross3_body(const Cross3Args& a) {
+  constexpr int QBW = NW * 32, PPW = 16 / NW;  // queries per workgroup, K (and V) 1-KB pieces per wave per block
+  constexpr int VBASE = NST * TILE_BYTES;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nx = gridDim.x, ny = gridDim.y;
   const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
   const int qb = flat % nx, h = (flat / nx) % ny, b = flat / (nx * ny);
-  if (qb * QB >= a.q_len) return;
+  if (qb * QBW >= a.q_len) return;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
   const int q_row0 = b * a.q_len;
-  const int frame = (a.tok_offset + qb * QB) / a.tpf;
+  const int frame = (a.tok_offset + qb * QBW) / a.tpf;
 
   // Q as the B operand (query tile qt, d chunk dc), prescaled by c; rows clamped to the segment
   bf16x8 qf[2][4];
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
-    const int qc = min(qb * QB + wave * 32 + qt * 16 + r16, a.q_len - 1);
+    const int qc = min(qb * QBW + wave * 32 + qt * 16 + r16, a.q_len - 1);
     const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * g;
 #pragma unroll
     for (int dc = 0; dc < 4; ++dc) {
@@ -784,10 +788,10 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
   // staging by buffer descriptors over each source's rows of this batch row (rows past the source read as
   // zeros and are masked): SGPR bases, per-lane 32-bit offsets, the block in soffset -- no 64-bit address math
   // per block (the round-3 kernel formed clamped 64-bit row addresses for every piece of every block)
-  int srow[2], kch[2], vch[2];
+  int srow[PPW], kch[PPW], vch[PPW];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    srow[i] = (wave * 2 + i) * 4 + (lane >> 4);
+  for (int i = 0; i < PPW; ++i) {
+    srow[i] = (wave * PPW + i) * 4 + (lane >> 4);
     kch[i] = r16 ^ (srow[i] & 15);
     vch[i] = r16 ^ ((srow[i] & 7) << 1);
   }
@@ -804,7 +808,7 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
       (void*)(a.kv + vrow0 * a.vs + h * D), (short)0, (int)(((long)a.nper - 1) * a.vs * 2 + 256), 0x00020000);
   const __amdgpu_buffer_rsrc_t rvv = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.vv + vrow0 * a.vs + h * D), (short)0, (int)(((long)a.nper - 1) * a.vs * 2 + 256), 0x00020000);
-  const uint32_t lds_k = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + wave * 2 * 1024);
+  const uint32_t lds_k = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + wave * PPW * 1024);
   auto stage = [&](int j, int buf) {
     __amdgpu_buffer_rsrc_t rk = rkt, rv = rvt;
     int st = (int)a.ts, blk = j;
@@ -815,12 +819,12 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
     }
     const int boff = blk * KVB * st * 2;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < PPW; ++i) {
       const int rowoff = srow[i] * st * 2;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, LDS_PTR((uintptr_t)(lds_k + buf * TILE_BYTES + i * 1024)), 16,
                                                rowoff + kch[i] * 16, boff, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rv, LDS_PTR((uintptr_t)(lds_k + X3_VBASE + buf * TILE_BYTES + i * 1024)), 16, rowoff + vch[i] * 16, boff, 0, 0);
+          rv, LDS_PTR((uintptr_t)(lds_k + VBASE + buf * TILE_BYTES + i * 1024)), 16, rowoff + vch[i] * 16, boff, 0, 0);
     }
   };
 
@@ -834,7 +838,7 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) {
       const int ch = 2 * dt + (p4 >> 1);
-      va[dt] = lds0 + X3_VBASE + row * 256 + ((ch ^ ((row & 7) << 1)) << 4) + 8 * (p4 & 1);
+      va[dt] = lds0 + VBASE + row * 256 + ((ch ^ ((row & 7) << 1)) << 4) + 8 * (p4 & 1);
     }
   }
 
@@ -875,12 +879,12 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
   // the next block was exposed at the barriers of these short streams)
   auto step = [&](int jj, auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
-    if (jj + 1 < ntot)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // block jj landed; jj+1 may still fly
+    if (NST > 2 && jj + 1 < ntot)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");  // block jj landed; jj+1 may still fly
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (jj + 2 < ntot) stage(jj + 2, (BUF + 2) % 3);
+    if (jj + NST - 1 < ntot) stage(jj + NST - 1, (BUF + NST - 1) % NST);
     const int src = jj < nT ? 0 : (jj < nT + nI ? 1 : 2);
     const int kb = src == 0 ? jj : (src == 1 ? jj - nT : jj - nT - nI);
     const int len = src == 0 ? a.t_len : (src == 1 ? a.i_len : a.nper);
@@ -902,45 +906,51 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
   const bool ihalf = vhalf && a.i_len % KVB != 0 && a.i_len % KVB <= KVB / 2;
   auto img_half = [&](int jj, auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // this block landed; the vocal block may still fly
+    if (NST > 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");  // this block landed; the vocal block may fly
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (NST == 2) stage(jj + 1, (BUF + 1) % NST);  // the vocal block, one ahead
     attn_half_block<BUF * TILE_BYTES, BUF * TILE_BYTES>(st, qf, ka, va, nI - 1, a.i_len, g, nI == 1);
     finish(1);
   };
   const int nloop = vhalf ? (ihalf ? ntot - 2 : ntot - 1) : ntot;
   stage(0, 0);
-  if (1 < ntot) stage(1, 1);
-  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-  for (int j = 0; j < nloop; j += 3) {
+  if (NST > 2 && 1 < ntot) stage(1, 1);
+  if (NW == 8 && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  for (int j = 0; j < nloop; j += NST) {
     step(j, std::integral_constant<int, 0>{});
     if (j + 1 >= nloop) break;
-    step(j + 1, std::integral_constant<int, 1>{});
-    if (j + 2 >= nloop) break;
-    step(j + 2, std::integral_constant<int, 2>{});
+    step(j + 1, std::integral_constant<int, 1 % NST>{});
+    if (NST > 2) {
+      if (j + 2 >= nloop) break;
+      step(j + 2, std::integral_constant<int, 2 % NST>{});
+    }
   }
   if (ihalf) {
     const int ji = ntot - 2;
-    if (ji % 3 == 0)
+    if (ji % NST == 0)
       img_half(ji, std::integral_constant<int, 0>{});
-    else if (ji % 3 == 1)
-      img_half(ji, std::integral_constant<int, 1>{});
+    else if (ji % NST == 1)
+      img_half(ji, std::integral_constant<int, 1 % NST>{});
     else
-      img_half(ji, std::integral_constant<int, 2>{});
+      img_half(ji, std::integral_constant<int, 2 % NST>{});
   }
   if (vhalf) {
     const int jl = ntot - 1;
-    if (jl % 3 == 0)
+    if (jl % NST == 0)
       last_half(jl, std::integral_constant<int, 0>{});
-    else if (jl % 3 == 1)
-      last_half(jl, std::integral_constant<int, 1>{});
+    else if (jl % NST == 1)
+      last_half(jl, std::integral_constant<int, 1 % NST>{});
     else
-      last_half(jl, std::integral_constant<int, 2>{});
+      last_half(jl, std::integral_constant<int, 2 % NST>{});
   }
 
   // 16-byte stores from permlane16-swapped column-group pairs, as the self-attention epilogue (T21)
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
-    const int qi = qb * QB + wave * 32 + qt * 16 + r16;
+    const int qi = qb * QBW + wave * 32 + qt * 16 + r16;
     bf16* op = a.o + (long)(q_row0 + min(qi, a.q_len - 1)) * a.os + h * D + 4 * (g & ~1) + 16 * (g & 1);
 #pragma unroll
     for (int dt = 0; dt < 8; dt += 2) {
@@ -951,6 +961,11 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) {
     }
   }
 }
+
+__global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) { attn_cross3_body<8, 3>(a); }
+// 4 waves x 32 queries, 2-stage ring (64 KB): two workgroups per CU, so one's prologue (Q from HBM) and epilogue
+// stores run beside the other's blocks
+__global__ __launch_bounds__(256, 2) void attn_cross3_w4_kernel(Cross3Args a) { attn_cross3_body<4, 2>(a); }
 
 __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) { attn_fwd_v6_body<8>(a); }
 __global__ __launch_bounds__(256, 2) void attn_fwd_v6_w4_kernel(AttnArgs a) { attn_fwd_v6_body<4>(a); }
@@ -1039,14 +1054,23 @@ extern "C" int sa_attn_cross3(const void* q, int64_t q_stride, const void* kt, c
     return SA_ERR_ARG;
   static const bool attr = [] {
     (void)hipFuncSetAttribute((const void*)attn_cross3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, X3_LDS);
+    (void)hipFuncSetAttribute((const void*)attn_cross3_w4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              4 * TILE_BYTES);
     return true;
   }();
   (void)attr;
   Cross3Args a{(const bf16*)q, q_stride, (const bf16*)kt, (const bf16*)vt, t_stride, t_len, (const bf16*)ki,
                (const bf16*)vi, i_stride, i_len, (const bf16*)kv, (const bf16*)vv, v_stride, nper,
                tokens_per_frame, n_frames, tok_offset, (bf16*)o, o_stride, q_len, scale * 1.4426950408889634f};
-  dim3 grid((q_len + QB - 1) / QB, heads, batch);
-  hipLaunchKernelGGL(attn_cross3_kernel, grid, dim3(512), X3_LDS, (hipStream_t)stream, a);
+  // 4-wave workgroups, two per CU (0.369-0.377 vs 0.390 ms per config-2 launch, same output; SA_X3_W4=0: 8 waves)
+  const char* w4 = getenv("SA_X3_W4");
+  if (!w4 || atoi(w4)) {
+    dim3 grid((q_len + 127) / 128, heads, batch);
+    hipLaunchKernelGGL(attn_cross3_w4_kernel, grid, dim3(256), 4 * TILE_BYTES, (hipStream_t)stream, a);
+  } else {
+    dim3 grid((q_len + QB - 1) / QB, heads, batch);
+    hipLaunchKernelGGL(attn_cross3_kernel, grid, dim3(512), X3_LDS, (hipStream_t)stream, a);
+  }
   SA_LAUNCH_CHECK();
   return SA_OK;
 }
