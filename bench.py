@@ -480,9 +480,96 @@ def barrier(world, dev):
         sync(dev)
 
 
+class ClockSampler:
+    """The GPU's graphics clock sampled every `period` s on a thread while the timed clips run (amdsmi: the SMU
+    metrics table's average gfx clock where the driver exposes it, else the current SCLK).  The device is matched
+    to this process's GPU by PCI bus id.  Reports mean / min / max MHz, or the reason it could not read."""
+
+    def __init__(self, dev, period=0.25):
+        import threading
+        self.period, self.samples, self.field, self.error = period, [], None, None
+        self._stop = threading.Event()
+        self._thr = None
+        self._read = None
+        try:
+            import amdsmi
+            amdsmi.amdsmi_init()
+            self._smi = amdsmi
+            props = torch.cuda.get_device_properties(dev)
+            bus = getattr(props, "pci_bus_id", None)
+            handles = amdsmi.amdsmi_get_processor_handles()
+            h = None
+            for x in handles:
+                bdf = amdsmi.amdsmi_get_gpu_device_bdf(x)  # "dddd:bb:dd.f"
+                if bus is not None and int(bdf.split(":")[1], 16) == int(bus):
+                    h = x
+            if h is None and len(handles) == 1:
+                h = handles[0]
+            if h is None:
+                raise RuntimeError(f"no amdsmi device with PCI bus {bus} among {len(handles)}")
+            self._h = h
+            self._read = self._probe()
+        except Exception as e:  # noqa: BLE001 -- a missing clock reading never fails the bench
+            self.error = f"{type(e).__name__}: {e}"[:200]
+
+    def _probe(self):
+        smi, h = self._smi, self._h
+        try:
+            m = smi.amdsmi_get_gpu_metrics_info(h)
+            for key in ("average_gfxclk_frequency", "current_gfxclk"):
+                v = m.get(key)
+                if isinstance(v, (int, float)) and 0 < v < 10000:
+                    self.field = f"gpu_metrics.{key}"
+                    return lambda: smi.amdsmi_get_gpu_metrics_info(h)[key]
+            v = m.get("current_gfxclks")
+            if isinstance(v, (list, tuple)) and any(isinstance(x, (int, float)) and 0 < x < 10000 for x in v):
+                self.field = "gpu_metrics.current_gfxclks (mean over XCDs)"
+
+                def rd():
+                    xs = [x for x in smi.amdsmi_get_gpu_metrics_info(h)["current_gfxclks"]
+                          if isinstance(x, (int, float)) and 0 < x < 10000]
+                    return sum(xs) / len(xs)
+                return rd
+        except Exception:  # noqa: BLE001
+            pass
+        self.field = "clock_info.GFX.clk"
+        return lambda: smi.amdsmi_get_clock_info(h, smi.AmdSmiClkType.GFX)["clk"]
+
+    def _loop(self):
+        while not self._stop.wait(self.period):
+            try:
+                self.samples.append(float(self._read()))
+            except Exception as e:  # noqa: BLE001
+                self.error = f"{type(e).__name__}: {e}"[:200]
+                return
+
+    def start(self):
+        if self._read is not None:
+            import threading
+            self._thr = threading.Thread(target=self._loop, daemon=True)
+            self._thr.start()
+
+    def stop(self):
+        if self._thr is not None:
+            self._stop.set()
+            self._thr.join(timeout=5)
+        try:
+            if self._read is not None:
+                self._smi.amdsmi_shut_down()
+        except Exception:  # noqa: BLE001
+            pass
+        s = self.samples
+        if not s:
+            return {"mean_mhz": None, "error": self.error or "no samples", "source": self.field}
+        return {"mean_mhz": round(sum(s) / len(s)), "min_mhz": round(min(s)), "max_mhz": round(max(s)),
+                "samples": len(s), "period_s": self.period, "source": f"amdsmi {self.field}"}
+
+
 def timed(work, steps, warmup, world, dev, events=False, before_timed=None):
     """W untimed warmup steps, then EXACTLY K steps between barriers; the max over ranks.
-    before_timed(warmup_seconds) runs after the warmup, before the opening barrier."""
+    before_timed(warmup_seconds) runs after the warmup, before the opening barrier.  events=True: the
+    self-attention events (roofline), the per-kernel-class HIP events (ktimer) and the SCLK samples of the timed
+    clips are recorded (work.kernels)."""
     with torch.no_grad():
         tw = time.perf_counter()
         for i in range(warmup):
@@ -492,18 +579,40 @@ def timed(work, steps, warmup, world, dev, events=False, before_timed=None):
         tw = time.perf_counter() - tw
         if before_timed is not None:
             before_timed(tw)
+        kt = clk = None
+        if events:
+            from stableavatar_amd.ktimer import KernelTimer
+            kt = KernelTimer() if dev.type == "cuda" and os.environ.get("SA_BENCH_KTIMER", "1") != "0" else None
+            clk = ClockSampler(dev) if dev.type == "cuda" and int(os.environ.get("RANK", "0")) == 0 else None
         barrier(world, dev)
         if events:
             work.start_events()
+            if kt is not None:
+                kt.__enter__()
+            if clk is not None:
+                clk.start()
         t0 = time.perf_counter()
         out = None
-        for i in range(steps):
-            out = work.step()
-            if steps > 1 and i + 1 < steps:  # no sync: the clips stay queued back to back
-                progress(f"timed {i + 1}/{steps} queued {time.perf_counter() - t0:.1f}s")
-        barrier(world, dev)
+        try:
+            for i in range(steps):
+                out = work.step()
+                if steps > 1 and i + 1 < steps:  # no sync: the clips stay queued back to back
+                    progress(f"timed {i + 1}/{steps} queued {time.perf_counter() - t0:.1f}s")
+            barrier(world, dev)
+        finally:
+            if kt is not None:
+                kt.__exit__(None, None, None)
         dt = time.perf_counter() - t0
         progress(f"timed {steps} steps {dt:.1f}s")
+        if events:
+            rec = kt.summary(steps) if kt is not None else {}
+            if rec:
+                rec["frac_of_ms_per_step"] = round(rec["sum_ms_per_clip"] / (dt / steps * 1e3), 4)
+            rec["sclk"] = clk.stop() if clk is not None else None
+            rec["note"] = ("per-kernel-class device time of the timed clips from one HIP event after every library "
+                           "launch on its stream (the interval since the stream's previous event, so each class "
+                           "includes the kernel boundary in front of it); ms per clip = mean over the timed clips")
+            work.kernels = rec
     if world > 1:
         import torch.distributed as dist
         tt = torch.tensor([dt], dtype=torch.float64, device=dev if dev.type == "cuda" else "cpu")
@@ -661,6 +770,8 @@ def run(args, world, rank, dev, work_factory=ClipWorkload, cpu=None):
         out["replicas"] = replicas
     if sp_check is not None:
         out["sp_check"] = sp_check
+    if getattr(work, "kernels", None):
+        out["kernels"] = work.kernels
     return out
 
 

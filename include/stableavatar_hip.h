@@ -24,7 +24,12 @@ enum {
   SA_EPI_F32 = 2,           /* C(f32)  = A·W^T + bias                                    */
   SA_EPI_RES_F32 = 3,       /* C(f32)  = R + (A·W^T + bias) * gate[row / rows_per_batch] */
   SA_EPI_GELU_ERF_BF16 = 4, /* C(bf16) = gelu_erf(A·W^T + bias)    (nn.GELU())           */
-  SA_EPI_SILU_F32 = 5       /* C(f32)  = silu(A·W^T + bias)                              */
+  SA_EPI_SILU_F32 = 5,      /* C(f32)  = silu(A·W^T + bias)                              */
+  SA_EPI_BF16_T = 6,        /* C^T(bf16): C[n * ldc + m] = A·W^T + bias (persistent kernel, K % 128 == 0,
+                               M % 4 == 0, ldc >= M): the V^T operand of sa_attn_fwd_ex kernel 4 */
+  SA_EPI_BF16_TP32 = 7      /* SA_EPI_BF16_T with row 32c + 4q + r at column 32c + 8(q & 3) + 4(q >> 2) + r
+                               (ldc >= M rounded up to 32): the V^T of sa_attn_fwd_ex kernel 3, the
+                               DiT's self-attention (wan_fantasy_transformer3d_1B.py:376-379 v projection) */
 };
 
 /* nn.Linear on bf16 activations (every Linear of wan/models/wan_fantasy_transformer3d_1B.py
@@ -51,13 +56,17 @@ int sa_gemm_bf16_ex(const void* A, int64_t lda, int64_t strideA, const void* W, 
  * sequence-parallel head exchange's receive buffer (one panel per head group) as the O-projection input
  * in place, replacing the all-gather of head outputs into token rows around wan/dist/wan_xfuser.py:72-115
  * (1B:1150-1151 after the USP attention).  a_panel_cols == 0 is sa_gemm_bf16_ex.
- * The buffer must stay readable for 256 rows (256 * lda elements) past the last panel's row M - 1: the last
- * panel's tail tile reads those rows (their products are never stored). */
+ * The buffer must stay readable for sa_gemm_panel_slack_rows() rows (x lda elements) past the last panel's
+ * row M - 1: the last panel's tail tile reads those rows (their products are never stored). */
 int sa_gemm_bf16_panels(const void* A, int64_t lda, int64_t strideA, const void* W, int64_t ldw, int64_t strideW,
                         const float* bias, void* C, int64_t ldc, int64_t strideC, int M, int N, int K, int batch,
                         int epilogue, const float* residual, int64_t ldr, int64_t strideR, const float* gate,
                         int64_t gate_bstride, int rows_per_batch, int kernel, int group_m, int64_t a_panel_cols,
                         int64_t a_panel_stride, void* stream);
+
+/* The tallest persistent GEMM tile (rows): the slack sa_gemm_bf16_panels needs past its A buffer's last
+ * panel row.  No GPU work; wan/dist/wan_xfuser.py has no counterpart (it all-gathers into token rows). */
+int sa_gemm_panel_slack_rows(void);
 
 /* attention(q,k,v,...) of wan/models/wan_fantasy_transformer3d_1B.py:158-207 (SDPA path, no mask,
  * q_lens/k_lens ignored) for head_dim 128.  Rows of q/k/v/o are flat [rows, stride] bf16 matrices,

@@ -18,6 +18,7 @@ SIGNATURES = {
     "sa_gemm_bf16": "pllpllpplliiiiipllplip",
     "sa_gemm_bf16_ex": "pllpllpplliiiiipllpliiip",
     "sa_gemm_bf16_panels": "pllpllpplliiiiipllpliiillp",
+    "sa_gemm_panel_slack_rows": "",
     "sa_attn_fwd": "pppppiiiillllfip",
     "sa_attn_fwd_ex": "pppppiiiillllfiip",
     "sa_attn_fwd_map": "pppppiiiillllfiipp",
@@ -56,6 +57,8 @@ SIGNATURES = {
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int32, "l": ctypes.c_int64, "f": ctypes.c_float}
 
 _lib = None
+# a ktimer.KernelTimer while a measurement records per-kernel-class time (bench.py); None otherwise
+_timer = None
 
 
 def header_symbols() -> list[str]:
@@ -90,7 +93,12 @@ class KernelError(RuntimeError):
 
 def call(name: str, *args):
     fn = getattr(lib(), name)
+    t = _timer
+    if t is not None:
+        t.before(name, args)
     rc = fn(*args)
+    if t is not None:
+        t.after(name, args)
     if rc != 0:
         kind = "bad argument" if rc == 1 else f"launch failure (hipError {rc - 2000})"
         raise KernelError(f"{name}: {kind} (rc={rc})")

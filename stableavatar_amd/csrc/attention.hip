@@ -504,6 +504,225 @@ __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2]
   }
 }
 
+// ---- V^T forms of the block (V read as V^T from a d-major producer layout, [H*128][Rv] bf16: row h*128 + d holds
+// d of head h for every key row), so each PV operand is ds_read_b128 instead of two ds_read_b64_tr_b16.
+// VMODE 1 (v6t): the v6 block with V^T staged 128 d-rows x 64 keys (128 B per d-row, 16-B chunk c of row d at
+//   position c ^ (d & 7)); the producer stores the keys of each 32-key chunk in P's permuted order (position 8g + j
+//   <-> key 4g + j, j < 4; 16 + 4g + j - 4, j >= 4), so a lane's 16x16x32 PV operand is one b128 read.
+// VMODE 2 (v12): the PV product on v_mfma_f32_32x32x16_bf16 (16 instead of 32 PV MFMAs per block: half the MFMA
+//   issue slots for the same pipe time), V^T in natural key order (chunk c of row d at position c ^ ((d >> 1) & 7):
+//   conflict-free for the 32-row operand reads).  P reaches the 32x32 B layout (lane = query l % 32, keys 8 (l/32) ..
+//   +7 of a 16-key step) from the 16x16 QK^T accumulators by one permlane16_swap per packed dword pair: lane row 0
+//   keeps its query-tile-0 keys 0-3 and takes row 1's tile-0 keys 4-7, row 1 takes row 0's tile-1 keys 0-3 (rows 2 /
+//   3 likewise with keys 8-15).  The row sums stay on the 16x16x32 ones-MFMA of v6 (same bf16 P, same sums).
+template <int VOFF, int C, int T0>
+__device__ __forceinline__ void v6t_read_v(u32x4* f, const uint32_t* vb) {
+  ds_b128<VOFF + (T0 + 0) * 2048>(f[0], vb[C]);
+  ds_b128<VOFF + (T0 + 1) * 2048>(f[1], vb[C]);
+  ds_b128<VOFF + (T0 + 2) * 2048>(f[2], vb[C]);
+  ds_b128<VOFF + (T0 + 3) * 2048>(f[3], vb[C]);
+}
+__device__ __forceinline__ void v6t_mma_v(f32x4 (&O)[8][2], int dt0, const u32x4* f, const bf16x8 (&pb)[2]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const bf16x8 a = v6_as_bf8(f[t]);
+    O[dt0 + t][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb[0], O[dt0 + t][0], 0, 0, 0);
+    O[dt0 + t][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb[1], O[dt0 + t][1], 0, 0, 0);
+  }
+}
+
+// the rescale of attn_v6_block (shared by the V^T forms): some row's max above the threshold (or the first block)
+// -> move the running max; ORESCALE(alpha[2]) rescales the output accumulators
+template <bool FIRST, class ORescale>
+__device__ __forceinline__ void v6_softmax_rescale(f32x4 (&S)[4][2], f32x4 (&L)[2], float (&negm)[2], f32x4 (&negm4)[2],
+                                                   ORescale orescale) {
+  if (FIRST || !__all(lanemax32(S) <= RESCALE_THR)) {  // wave-uniform
+    float mx[2], alpha[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) mx[qt] = rowmax64(S, qt);
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const float delta = FIRST ? mx[qt] : fmaxf(mx[qt], 0.f);
+      alpha[qt] = __builtin_amdgcn_exp2f(-delta);
+      if (!FIRST) L[qt] *= alpha[qt];
+      negm[qt] -= delta;
+      negm4[qt] = (f32x4){negm[qt], negm[qt], negm[qt], negm[qt]};
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) S[kt][qt][i] -= delta;
+    }
+    if (!FIRST) orescale(alpha);
+  }
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) S[kt][qt][i] = __builtin_amdgcn_exp2f(S[kt][qt][i]);
+}
+
+template <int KOFF>
+__device__ __forceinline__ void v6_qk(f32x4 (&S)[4][2], const f32x4 (&negm4)[2], const bf16x8 (&qf)[2][4],
+                                      const uint32_t* ka) {
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) S[kt][qt] = negm4[qt];
+  u32x4 k0[4], k1[4];
+  v6_read_k<KOFF, 0>(k0, ka);
+  v6_read_k<KOFF, 1>(k1, ka);
+  wait_k4<4>(k0);
+  v6_mma_k(S, 0, k0, qf);
+  v6_read_k<KOFF, 2>(k0, ka);
+  wait_k4<4>(k1);
+  v6_mma_k(S, 1, k1, qf);
+  v6_read_k<KOFF, 3>(k1, ka);
+  wait_k4<4>(k0);
+  v6_mma_k(S, 2, k0, qf);
+  wait_k4<0>(k1);
+  v6_mma_k(S, 3, k1, qf);
+}
+
+__device__ __forceinline__ void v6_tail_mask(f32x4 (&S)[4][2], int kb, int kv_len, int g) {
+  if (kb * KVB + KVB > kv_len) {
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (kb * KVB + kt * 16 + 4 * g + i >= kv_len) { S[kt][0][i] = -INFINITY; S[kt][1][i] = -INFINITY; }
+  }
+}
+
+template <int KOFF, int VOFF, bool FIRST>
+__device__ __forceinline__ void attn_v6t_block(V6State& st, const bf16x8 (&qf)[2][4], const uint32_t* ka,
+                                               const uint32_t* vb, int kb, int kv_len, int g) {
+  f32x4 S[4][2];
+  v6_qk<KOFF>(S, st.negm4, qf, ka);
+  u32x4 v0[4], v1[4];
+  v6t_read_v<VOFF, 0, 0>(v0, vb);
+  v6t_read_v<VOFF, 0, 4>(v1, vb);
+  v6_tail_mask(S, kb, kv_len, g);
+  v6_softmax_rescale<FIRST>(S, st.L, st.negm, st.negm4, [&](const float (&al)[2]) {
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st.O[dt][qt][i] *= al[qt];
+  });
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    bf16x8 pb[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[qt][j] = f2bf(S[2 * c][qt][j]);
+        pb[qt][4 + j] = f2bf(S[2 * c + 1][qt][j]);
+      }
+    {
+      bf16x8 ones;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+      st.L[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[0], st.L[0], 0, 0, 0);
+      st.L[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[1], st.L[1], 0, 0, 0);
+    }
+    if (c == 0) {
+      wait_k4<4>(v0);
+      v6t_mma_v(st.O, 0, v0, pb);
+      v6t_read_v<VOFF, 1, 0>(v0, vb);
+      wait_k4<4>(v1);
+      v6t_mma_v(st.O, 4, v1, pb);
+      v6t_read_v<VOFF, 1, 4>(v1, vb);
+    } else {
+      wait_k4<4>(v0);
+      v6t_mma_v(st.O, 0, v0, pb);
+      wait_k4<0>(v1);
+      v6t_mma_v(st.O, 4, v1, pb);
+    }
+  }
+}
+
+struct V12State {
+  f32x16 O[4];    // O^T d-tile dt (32 d x 32 queries): lane = query l % 32, d = 32 dt + 8 (i/4) + 4 (l/32) + i % 4
+  f32x4 L[2];     // row sums as in V6State (query tile qt = lanes' query qt*16 + l%16)
+  float negm[2];
+  f32x4 negm4[2];
+};
+
+// V^T fragments of 16-key step S for the 4 d-tiles (d-tile t at +4096: 32 d-rows x 128 B)
+template <int VOFF, int S>
+__device__ __forceinline__ void v12_read_v(u32x4* f, const uint32_t* vb) {
+  ds_b128<VOFF + 0 * 4096>(f[0], vb[S]);
+  ds_b128<VOFF + 1 * 4096>(f[1], vb[S]);
+  ds_b128<VOFF + 2 * 4096>(f[2], vb[S]);
+  ds_b128<VOFF + 3 * 4096>(f[3], vb[S]);
+}
+
+__device__ __forceinline__ void v12_mma_v(f32x16 (&O)[4], const u32x4* f, const bf16x8& pb) {
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) O[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v6_as_bf8(f[dt]), pb, O[dt], 0, 0, 0);
+}
+
+template <int KOFF, int VOFF, bool FIRST>
+__device__ __forceinline__ void attn_v12_block(V12State& st, const bf16x8 (&qf)[2][4], const uint32_t* ka,
+                                               const uint32_t* vb, int kb, int kv_len, int g, bool hi16) {
+  f32x4 S[4][2];
+  v6_qk<KOFF>(S, st.negm4, qf, ka);
+  u32x4 va[4], vc[4];
+  v12_read_v<VOFF, 0>(va, vb);
+  v6_tail_mask(S, kb, kv_len, g);
+  v6_softmax_rescale<FIRST>(S, st.L, st.negm, st.negm4, [&](const float (&al)[2]) {
+    const float a = hi16 ? al[1] : al[0];  // this lane's query in the 32x32 layout
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) st.O[dt][i] *= a;
+  });
+  // P in bf16, packed per (16-key tile, query tile): the v6 packing, so the row-sum MFMAs are v6's
+  u32x2 pk[4][2];
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const bf16x4 x = {f2bf(S[kt][qt][0]), f2bf(S[kt][qt][1]), f2bf(S[kt][qt][2]), f2bf(S[kt][qt][3])};
+      pk[kt][qt] = __builtin_bit_cast(u32x2, x);
+    }
+  {
+    bf16x8 ones;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+        st.L[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, v6_as_bf8(pk[2 * c][qt], pk[2 * c + 1][qt]), st.L[qt],
+                                                           0, 0, 0);
+  }
+  // P^T B operands of the four 16-key steps (32x32 layout)
+  bf16x8 pb[4];
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt) {
+    const auto x = __builtin_amdgcn_permlane16_swap(pk[kt][0][0], pk[kt][1][0], false, false);
+    const auto y = __builtin_amdgcn_permlane16_swap(pk[kt][0][1], pk[kt][1][1], false, false);
+    pb[kt] = __builtin_bit_cast(bf16x8, (u32x4){x[0], y[0], x[1], y[1]});
+  }
+  // O^T += V^T P^T, one 16-key step at a time: step s+1's V^T fragments are read (into the other buffer) before
+  // the wait for step s's, so they land under step s's MFMAs
+  v12_read_v<VOFF, 1>(vc, vb);
+  wait_k4<4>(va);
+  v12_mma_v(st.O, va, pb[0]);
+  v12_read_v<VOFF, 2>(va, vb);
+  wait_k4<4>(vc);
+  v12_mma_v(st.O, vc, pb[1]);
+  v12_read_v<VOFF, 3>(vc, vb);
+  wait_k4<4>(va);
+  v12_mma_v(st.O, va, pb[2]);
+  wait_k4<0>(vc);
+  v12_mma_v(st.O, vc, pb[3]);
+}
+
 // the fused cross-attention's last block of a source with at most 32 keys left (the image's 257th key, the 32
 // vocal keys of a frame): attn_v6_block on key tiles 0-1 only -- half the QK^T / PV MFMAs and exponentials
 __device__ __forceinline__ float rowmax32_c0(const f32x4 (&S)[2][2], int qt) {
@@ -643,16 +862,26 @@ __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
     }
   }
 
-  // staging: each wave moves 2 x 1-KB pieces (4 rows each) of K and of V per block; lane -> row
-  // (lane / 16), stored position lane % 16 holding source chunk (lane % 16) ^ swizzle(row)
   // K/V pieces: each wave moves 2 x 1-KB pieces (4 rows each) of K and of V per block; lane -> row
   // (lane / 16), stored position lane % 16 holding source chunk (lane % 16) ^ swizzle(row).  By
-  // buffer_load...lds from SGPR descriptors over exactly the segment's kv_len rows (rows past it read as
-  // zeros and are masked), per-lane 32-bit offsets and the block in soffset: no 64-bit address VALU
+  // buffer_load...lds from SGPR descriptors, per-lane 32-bit offsets and the block in soffset: no 64-bit
+  // address VALU.  The hardware range check covers voffset + the instruction offset, NOT soffset, so a
+  // descriptor over the whole segment does not bound a partial last block: that block is staged from a
+  // descriptor of its own (base = its first row, soffset 0) whose range ends at the segment's last row, so
+  // its rows past kv_len read as zeros (masked in S, and 0 x 0 in PV) instead of whatever follows
+  const int nkb = (kv_len + KVB - 1) / KVB;
+  const long tail0 = (long)(nkb - 1) * KVB;  // first row of the last block
   const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.k + (long)kv_row0 * a.ks + h * D), (short)0, (int)(((long)kv_len - 1) * a.ks * 2 + 256), 0x00020000);
   const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.v + (long)kv_row0 * a.vs + h * D), (short)0, (int)(((long)kv_len - 1) * a.vs * 2 + 256), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rkt = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.k + (kv_row0 + tail0) * a.ks + h * D), (short)0, (int)((kv_len - tail0 - 1) * a.ks * 2 + 256),
+      0x00020000);
+  const __amdgpu_buffer_rsrc_t rvt = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.v + (kv_row0 + tail0) * a.vs + h * D), (short)0, (int)((kv_len - tail0 - 1) * a.vs * 2 + 256),
+      0x00020000);
+  const bool ragged = kv_len % KVB != 0;
   int koff[PPW], voff[PPW];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
@@ -662,13 +891,15 @@ __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
   }
   const uint32_t lds_dma = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + wave * PPW * 1024);
   auto stage = [&](int kb, int buf) {
-    const int ks_off = kb * KVB * (int)a.ks * 2, vs_off = kb * KVB * (int)a.vs * 2;
+    const bool tail = ragged && kb == nkb - 1;  // wave-uniform
+    const int ks_off = tail ? 0 : kb * KVB * (int)a.ks * 2, vs_off = tail ? 0 : kb * KVB * (int)a.vs * 2;
+    const __amdgpu_buffer_rsrc_t bk = tail ? rkt : rk, bv = tail ? rvt : rv;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, LDS_PTR((uintptr_t)(lds_dma + buf * STAGE_BYTES + i * 1024)), 16,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(bk, LDS_PTR((uintptr_t)(lds_dma + buf * STAGE_BYTES + i * 1024)), 16,
                                                koff[i], ks_off, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rv, LDS_PTR((uintptr_t)(lds_dma + buf * STAGE_BYTES + TILE_BYTES + i * 1024)), 16, voff[i], vs_off, 0, 0);
+          bv, LDS_PTR((uintptr_t)(lds_dma + buf * STAGE_BYTES + TILE_BYTES + i * 1024)), 16, voff[i], vs_off, 0, 0);
     }
   };
 
@@ -696,7 +927,6 @@ __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
   st.negm[0] = st.negm[1] = 0.f;
   st.negm4[0] = st.negm4[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int nkb = (kv_len + KVB - 1) / KVB;
   stage(0, 0);
   if (NW == 8 && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -747,6 +977,204 @@ __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
   }
 }
 
+// self-attention reading V as V^T (attn_v6t_block / attn_v12_block above): 8 waves x 32 queries, the v6 ring and
+// K staging.  a.v = V^T [heads * 128][Rv] bf16 (row h*128 + d, a.vs = Rv >= the rows any segment reaches, rounded
+// up to 64; segments start on 32-key boundaries; every element of a row readable and finite through Rv: the
+// partial last block reads the keys past kv_len, masked to P = 0).  VMODE 1: keys permuted per 32 as P; VMODE 2:
+// natural key order.
+template <int VMODE>
+__device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
+  constexpr int NW = 8, QBW = NW * 32, PPW = 16 / NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nx = gridDim.x, ny = gridDim.y;
+  const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
+  const int qb = flat % nx, h = (flat / nx) % ny, seg = flat / (nx * ny);
+  const int* sg = a.segs + seg * 4;
+  const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
+  if (qb * QBW >= q_len) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (kv_len <= 0) {
+    if (!a.accumulate)
+      for (int i = tid; i < QBW * (D / 8); i += NW * 64) {
+        const int qi = qb * QBW + i / (D / 8);
+        if (qi < q_len) {
+          const int orow = a.orows ? a.orows[q_row0 + qi] : q_row0 + qi;
+          *(u32x4*)(a.o + (long)orow * a.os + h * D + (i % (D / 8)) * 8) = (u32x4){0u, 0u, 0u, 0u};
+        }
+      }
+    return;
+  }
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qc = min(qb * QBW + wave * 32 + qt * 16 + r16, q_len - 1);
+    const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * g;
+#pragma unroll
+    for (int dc = 0; dc < 4; ++dc) {
+      qf[qt][dc] = *(const bf16x8*)(qp + 32 * dc);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[qt][dc][j] = f2bf(bf2f(qf[qt][dc][j]) * a.c);
+    }
+  }
+  const int nkb = (kv_len + KVB - 1) / KVB;
+  const long tail0 = (long)(nkb - 1) * KVB;
+  const bool ragged = kv_len % KVB != 0;
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.k + (long)kv_row0 * a.ks + h * D), (short)0, (int)(((long)kv_len - 1) * a.ks * 2 + 256), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rkt = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.k + (kv_row0 + tail0) * a.ks + h * D), (short)0, (int)((kv_len - tail0 - 1) * a.ks * 2 + 256),
+      0x00020000);
+  // V^T: the head's 128 d-rows from key kv_row0, each through the segment's last block
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.v + (long)h * D * a.vs + kv_row0), (short)0, (int)(((long)(D - 1) * a.vs + (long)nkb * KVB) * 2),
+      0x00020000);
+  int koff[PPW], voff[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int srow = (wave * PPW + i) * 4 + (lane >> 4);
+    koff[i] = srow * (int)a.ks * 2 + ((r16 ^ (srow & 15)) << 4);
+    const int d = (wave * PPW + i) * 8 + (lane >> 3);  // a 1-KB piece = 8 d-rows x 128 B
+    const int sw = VMODE == 1 ? (d & 7) : ((d >> 1) & 7);
+    voff[i] = d * (int)a.vs * 2 + (((lane & 7) ^ sw) << 4);
+  }
+  const uint32_t lds_dma = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + wave * PPW * 1024);
+  auto stage = [&](int kb, int buf) {
+    const bool tail = ragged && kb == nkb - 1;
+    const int ks_off = tail ? 0 : kb * KVB * (int)a.ks * 2, vs_off = kb * KVB * 2;
+    const __amdgpu_buffer_rsrc_t bk = tail ? rkt : rk;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(bk, LDS_PTR((uintptr_t)(lds_dma + buf * STAGE_BYTES + i * 1024)), 16,
+                                               koff[i], ks_off, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rv, LDS_PTR((uintptr_t)(lds_dma + buf * STAGE_BYTES + TILE_BYTES + i * 1024)), 16, voff[i], vs_off, 0, 0);
+    }
+  };
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
+  uint32_t ka[4], vb[4];
+#pragma unroll
+  for (int dc = 0; dc < 4; ++dc) ka[dc] = lds0 + r16 * 256 + (((dc * 4 + g) ^ r16) << 4);
+  if constexpr (VMODE == 1) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) vb[c] = lds0 + r16 * 128 + (((4 * c + g) ^ (r16 & 7)) << 4);
+    vb[2] = vb[3] = 0;
+  } else {
+    const int d32 = lane & 31, hh = lane >> 5;
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) vb[s4] = lds0 + d32 * 128 + (((2 * s4 + hh) ^ ((d32 >> 1) & 7)) << 4);
+  }
+  const bool hi16 = (lane >> 4) & 1;
+
+  using State = std::conditional_t<VMODE == 2, V12State, V6State>;
+  State st;
+  if constexpr (VMODE == 2) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) st.O[dt][i] = 0.f;
+  } else {
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) st.O[dt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  st.L[0] = st.L[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  st.negm[0] = st.negm[1] = 0.f;
+  st.negm4[0] = st.negm4[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  auto block = [&](auto koffc, auto firstc, int kb) {
+    constexpr int KO = decltype(koffc)::value;
+    constexpr bool FI = decltype(firstc)::value;
+    if constexpr (VMODE == 2)
+      attn_v12_block<KO, KO + TILE_BYTES, FI>(st, qf, ka, vb, kb, kv_len, g, hi16);
+    else
+      attn_v6t_block<KO, KO + TILE_BYTES, FI>(st, qf, ka, vb, kb, kv_len, g);
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, STAGE_BYTES>;
+  stage(0, 0);
+  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (1 < nkb) stage(1, 1);
+  block(C0{}, std::true_type{}, 0);
+  for (int kb = 1; kb < nkb; kb += 2) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kb + 1 < nkb) stage(kb + 1, 0);
+    block(C1{}, std::false_type{}, kb);
+    if (kb + 1 >= nkb) break;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kb + 2 < nkb) stage(kb + 2, 1);
+    block(C0{}, std::false_type{}, kb + 1);
+  }
+
+  if constexpr (VMODE == 2) {
+    // lane l: query (l % 32), d = 32 dt + 8 (i / 4) + 4 (l / 32) + i % 4; a permlane32 swap per dword pair gives
+    // each lane 8 consecutive d (one 16-byte store): lanes < 32 d 16m + 0..7, lanes >= 32 d 16m + 8..15
+    const float inv = 1.0f / (hi16 ? st.L[1][0] : st.L[0][0]);  // a select: a dynamic index would put st in scratch
+    const int hh = lane >> 5;
+    const int qi = qb * QBW + wave * 32 + (lane & 31);
+    const int qrow = q_row0 + min(qi, q_len - 1);
+    const int orow = a.orows ? a.orows[qrow] : qrow;
+    bf16* op = a.o + (long)orow * a.os + h * D + 8 * hh;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const f32x16& O = st.O[dt];
+        const bf16x4 pa = {f2bf(O[8 * m] * inv), f2bf(O[8 * m + 1] * inv), f2bf(O[8 * m + 2] * inv),
+                           f2bf(O[8 * m + 3] * inv)};
+        const bf16x4 pc = {f2bf(O[8 * m + 4] * inv), f2bf(O[8 * m + 5] * inv), f2bf(O[8 * m + 6] * inv),
+                           f2bf(O[8 * m + 7] * inv)};
+        const u32x2 ga = __builtin_bit_cast(u32x2, pa), gc = __builtin_bit_cast(u32x2, pc);
+        const auto rx = __builtin_amdgcn_permlane32_swap(ga[0], gc[0], false, false);
+        const auto ry = __builtin_amdgcn_permlane32_swap(ga[1], gc[1], false, false);
+        u32x4 out = {rx[0], ry[0], rx[1], ry[1]};
+        bf16* p = op + dt * 32 + 16 * m;
+        if (a.accumulate) {
+          const bf16x8 ov = *(const bf16x8*)p;
+          bf16x8 nv = __builtin_bit_cast(bf16x8, out);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) nv[j] = f2bf(bf2f(ov[j]) + bf2f(nv[j]));
+          out = __builtin_bit_cast(u32x4, nv);
+        }
+        if (qi < q_len) *(u32x4*)p = out;
+      }
+  } else {
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const float inv = 1.0f / st.L[qt][0];
+      const int qi = qb * QBW + wave * 32 + qt * 16 + r16;
+      const int qrow = q_row0 + min(qi, q_len - 1);
+      const int orow = a.orows ? a.orows[qrow] : qrow;
+      bf16* op = a.o + (long)orow * a.os + h * D + 4 * (g & ~1) + 16 * (g & 1);
+#pragma unroll
+      for (int dt = 0; dt < 8; dt += 2) {
+        const f32x4& A = st.O[dt][qt];
+        const f32x4& B = st.O[dt + 1][qt];
+        const bf16x4 pa = {f2bf(A[0] * inv), f2bf(A[1] * inv), f2bf(A[2] * inv), f2bf(A[3] * inv)};
+        const bf16x4 pb = {f2bf(B[0] * inv), f2bf(B[1] * inv), f2bf(B[2] * inv), f2bf(B[3] * inv)};
+        const u32x2 ga = __builtin_bit_cast(u32x2, pa), gb = __builtin_bit_cast(u32x2, pb);
+        const auto rx = __builtin_amdgcn_permlane16_swap(ga[0], gb[0], false, false);
+        const auto ry = __builtin_amdgcn_permlane16_swap(ga[1], gb[1], false, false);
+        u32x4 out = {rx[0], ry[0], rx[1], ry[1]};
+        bf16* p = op + dt * 16;
+        if (a.accumulate) {
+          const bf16x8 ov = *(const bf16x8*)p;
+          bf16x8 nv = __builtin_bit_cast(bf16x8, out);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) nv[j] = f2bf(bf2f(ov[j]) + bf2f(nv[j]));
+          out = __builtin_bit_cast(u32x4, nv);
+        }
+        if (qi < q_len) *(u32x4*)p = out;
+      }
+    }
+  }
+}
+
 // the fused cross-attention on the self-attention block body: 8 waves x 32 queries of one query block,
 // the text, image and per-frame vocal K/V streams one after the other through 3-stage K / V regions (each
 // block's DMA two blocks ahead), a separate online softmax per source (its first block sets the max), the
@@ -785,9 +1213,12 @@ __device__ __forceinline__ void attn_cross3_body(const Cross3Args& a) {
   // (K rows chunk ^ (row & 15), V rows chunk ^ 2 (row & 7)); each wave moves 2 x 1-KB pieces of K and V
   const int nT = (a.t_len + KVB - 1) / KVB, nI = (a.i_len + KVB - 1) / KVB, nV = (a.nper + KVB - 1) / KVB;
   const int ntot = nT + nI + nV;
-  // staging by buffer descriptors over each source's rows of this batch row (rows past the source read as
-  // zeros and are masked): SGPR bases, per-lane 32-bit offsets, the block in soffset -- no 64-bit address math
-  // per block (the round-3 kernel formed clamped 64-bit row addresses for every piece of every block)
+  // staging by buffer descriptors rebased per block (SALU: base = the block's first row of this batch row's
+  // source, range = its rows up to the source's last), so rows past the source read as zeros and are masked;
+  // per-lane 32-bit offsets -- no 64-bit address VALU per block (the round-3 kernel formed clamped 64-bit row
+  // addresses for every piece of every block).  The block offset cannot travel in soffset: the hardware range
+  // check does not cover soffset, so the image stream's last block (257 = 4 x 64 + 1 keys) would read up to 63
+  // rows past the source
   int srow[PPW], kch[PPW], vch[PPW];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
@@ -796,35 +1227,32 @@ __device__ __forceinline__ void attn_cross3_body(const Cross3Args& a) {
     vch[i] = r16 ^ ((srow[i] & 7) << 1);
   }
   const long vrow0 = (long)(b * a.n_frames + frame) * a.nper;
-  const __amdgpu_buffer_rsrc_t rkt = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.kt + (long)b * a.t_len * a.ts + h * D), (short)0, (int)(((long)a.t_len - 1) * a.ts * 2 + 256), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rvt = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.vt + (long)b * a.t_len * a.ts + h * D), (short)0, (int)(((long)a.t_len - 1) * a.ts * 2 + 256), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rki = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.ki + (long)b * a.i_len * a.is + h * D), (short)0, (int)(((long)a.i_len - 1) * a.is * 2 + 256), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rvi = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.vi + (long)b * a.i_len * a.is + h * D), (short)0, (int)(((long)a.i_len - 1) * a.is * 2 + 256), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rkv = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.kv + vrow0 * a.vs + h * D), (short)0, (int)(((long)a.nper - 1) * a.vs * 2 + 256), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rvv = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.vv + vrow0 * a.vs + h * D), (short)0, (int)(((long)a.nper - 1) * a.vs * 2 + 256), 0x00020000);
+  const bf16* const kt0 = a.kt + (long)b * a.t_len * a.ts + h * D;
+  const bf16* const vt0 = a.vt + (long)b * a.t_len * a.ts + h * D;
+  const bf16* const ki0 = a.ki + (long)b * a.i_len * a.is + h * D;
+  const bf16* const vi0 = a.vi + (long)b * a.i_len * a.is + h * D;
+  const bf16* const kv0 = a.kv + vrow0 * a.vs + h * D;
+  const bf16* const vv0 = a.vv + vrow0 * a.vs + h * D;
   const uint32_t lds_k = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + wave * PPW * 1024);
   auto stage = [&](int j, int buf) {
-    __amdgpu_buffer_rsrc_t rk = rkt, rv = rvt;
-    int st = (int)a.ts, blk = j;
+    const bf16 *kb0 = kt0, *vb0 = vt0;
+    int st = (int)a.ts, blk = j, len = a.t_len;
     if (j >= nT + nI) {
-      rk = rkv; rv = rvv; st = (int)a.vs; blk = j - nT - nI;
+      kb0 = kv0; vb0 = vv0; st = (int)a.vs; blk = j - nT - nI; len = a.nper;
     } else if (j >= nT) {
-      rk = rki; rv = rvi; st = (int)a.is; blk = j - nT;
+      kb0 = ki0; vb0 = vi0; st = (int)a.is; blk = j - nT; len = a.i_len;
     }
-    const int boff = blk * KVB * st * 2;
+    const long r0 = (long)blk * KVB;
+    const int nrec = (int)((min((long)len - r0, (long)KVB) - 1) * st * 2 + 256);
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)(kb0 + r0 * st), (short)0, nrec, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(vb0 + r0 * st), (short)0, nrec, 0x00020000);
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int rowoff = srow[i] * st * 2;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, LDS_PTR((uintptr_t)(lds_k + buf * TILE_BYTES + i * 1024)), 16,
-                                               rowoff + kch[i] * 16, boff, 0, 0);
+                                               rowoff + kch[i] * 16, 0, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rv, LDS_PTR((uintptr_t)(lds_k + VBASE + buf * TILE_BYTES + i * 1024)), 16, rowoff + vch[i] * 16, boff, 0, 0);
+          rv, LDS_PTR((uintptr_t)(lds_k + VBASE + buf * TILE_BYTES + i * 1024)), 16, rowoff + vch[i] * 16, 0, 0, 0);
     }
   };
 
@@ -969,6 +1397,8 @@ __global__ __launch_bounds__(256, 2) void attn_cross3_w4_kernel(Cross3Args a) { 
 
 __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) { attn_fwd_v6_body<8>(a); }
 __global__ __launch_bounds__(256, 2) void attn_fwd_v6_w4_kernel(AttnArgs a) { attn_fwd_v6_body<4>(a); }
+__global__ __launch_bounds__(512) void attn_fwd_v6t_kernel(AttnArgs a) { attn_fwd_vt_body<1>(a); }
+__global__ __launch_bounds__(512) void attn_fwd_v12_kernel(AttnArgs a) { attn_fwd_vt_body<2>(a); }
 
 }  // namespace
 
@@ -988,11 +1418,14 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
   if (head_dim != D) return SA_ERR_ARG;
   if ((q_stride | k_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
   if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)o)) & 15) return SA_ERR_ARG;
-  if (kernel < 0 || kernel > 2) return SA_ERR_ARG;
+  if (kernel < 0 || kernel > 4) return SA_ERR_ARG;
+  if (kernel >= 3 && (v_stride % 64 || (((uintptr_t)v) & 127))) return SA_ERR_ARG;  // V^T rows: whole 64-key blocks
   static const bool attr = [] {  // one-time, thread-safe
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6_w4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_v6t_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_v12_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     return true;
   }();
   (void)attr;
@@ -1014,6 +1447,12 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
   if (kernel == 2) {
     dim3 grid((max_q_len + 127) / 128, heads, nseg);
     hipLaunchKernelGGL(attn_fwd_v6_w4_kernel, grid, dim3(256), LDS_BYTES, (hipStream_t)stream, a);
+  } else if (kernel == 3 || kernel == 4) {  // v = V^T [heads * 128][v_stride] (attn_fwd_vt_body)
+    dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
+    if (kernel == 3)
+      hipLaunchKernelGGL(attn_fwd_v6t_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(attn_fwd_v12_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
   } else {
     dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
     hipLaunchKernelGGL(attn_fwd_v6_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);

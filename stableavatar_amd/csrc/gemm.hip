@@ -20,7 +20,12 @@
 
 namespace {
 
-enum { EPI_BF16 = 0, EPI_GELU_BF16 = 1, EPI_F32 = 2, EPI_RES_F32 = 3, EPI_GELU_ERF_BF16 = 4, EPI_SILU_F32 = 5 };
+enum {
+  EPI_BF16 = 0, EPI_GELU_BF16 = 1, EPI_F32 = 2, EPI_RES_F32 = 3, EPI_GELU_ERF_BF16 = 4, EPI_SILU_F32 = 5,
+  EPI_BF16_T = 6,     // bf16 output stored transposed, C[n * ldc + m]
+  EPI_BF16_TP32 = 7   // ... with the rows of each 32-row chunk in the self-attention's P order (its V^T operand,
+                      // attention.hip VMODE 1): row 32c + 4q + r at column 32c + 8 (q & 3) + 4 (q >> 2) + r
+};
 
 struct GemmArgs {
   const bf16* A; long lda; long sA;
@@ -429,8 +434,14 @@ template <int OFF>
 __device__ __forceinline__ void s4_ds(u32x4& d, uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF));
 }
+// TR (EPI_BF16_T): operands in the natural order (C = A·W^T), so each lane holds 4 consecutive output ROWS of one
+// column -- 4 consecutive elements of a row of C^T
+template <bool TR = false>
 __device__ __forceinline__ void s4_mma(f32x4& c, const u32x4& w, const u32x4& x) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(w), "v"(x) : "memory");
+  if constexpr (TR)
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(x), "v"(w) : "memory");
+  else
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(w), "v"(x) : "memory");
 }
 template <int MI = 8>
 __device__ __forceinline__ void s4_wait_frags(u32x4 (&a)[8], u32x4 (&b)[8]) {
@@ -498,21 +509,21 @@ __device__ __forceinline__ void s5_dma_at(const S5Ctx& c, int ks, int ksa) {
   }
 }
 
-template <int RS, int RK, bool DMA, int DS, bool SPREAD = false, int MI = 8>
+template <int RS, int RK, bool DMA, int DS, bool SPREAD = false, int MI = 8, bool TR = false>
 __device__ __forceinline__ void s5_half(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&ac)[8], u32x4 (&bc)[8],
                                         u32x4 (&an)[8], u32x4 (&bn)[8], int ks, int ksa) {
 #define SA_S5_ROW(Q)                                                                        \
   if constexpr (Q < MI) {                                                                   \
-    s4_mma(acc[Q][0], bc[0], ac[Q]); s4_mma(acc[Q][1], bc[1], ac[Q]);                       \
+    s4_mma<TR>(acc[Q][0], bc[0], ac[Q]); s4_mma<TR>(acc[Q][1], bc[1], ac[Q]);               \
     if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q, MI>(c, an, bn); }                         \
     s5_dma_at<DS, Q, 0, DMA, SPREAD, MI>(c, ks, ksa);                                       \
-    s4_mma(acc[Q][2], bc[2], ac[Q]); s4_mma(acc[Q][3], bc[3], ac[Q]);                       \
+    s4_mma<TR>(acc[Q][2], bc[2], ac[Q]); s4_mma<TR>(acc[Q][3], bc[3], ac[Q]);               \
     if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 1, MI>(c, an, bn); }                     \
     s5_dma_at<DS, Q, 1, DMA, SPREAD, MI>(c, ks, ksa);                                       \
-    s4_mma(acc[Q][4], bc[4], ac[Q]); s4_mma(acc[Q][5], bc[5], ac[Q]);                       \
+    s4_mma<TR>(acc[Q][4], bc[4], ac[Q]); s4_mma<TR>(acc[Q][5], bc[5], ac[Q]);               \
     if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 2, MI>(c, an, bn); }                     \
     s5_dma_at<DS, Q, 2, DMA, SPREAD, MI>(c, ks, ksa);                                       \
-    s4_mma(acc[Q][6], bc[6], ac[Q]); s4_mma(acc[Q][7], bc[7], ac[Q]);                       \
+    s4_mma<TR>(acc[Q][6], bc[6], ac[Q]); s4_mma<TR>(acc[Q][7], bc[7], ac[Q]);               \
     if constexpr (Q < 4) { s5_read<RS, RK, 4 * Q + 3, MI>(c, an, bn); }                     \
     s5_dma_at<DS, Q, 3, DMA, SPREAD, MI>(c, ks, ksa);                                       \
   }
@@ -595,11 +606,47 @@ __device__ __forceinline__ void s7_f32_epilogue(const GemmArgs& g, f32x4 (&acc)[
   }
 }
 
+// EPI_BF16_T: the tile stored transposed, C[n * ldc + m] = bf16(acc + bias[n]).  With the natural-order MFMA (TR)
+// lane (fr, fc) of wave (wm, wn) holds in acc[i][j] rows m0 + wm*16*MI + i*16 + 4 fc + 0..3 of column n0 + wn*128 +
+// j*16 + fr: one 8-byte store of 4 consecutive elements of row n of C^T per (i, j), no LDS round trip.  Walked
+// column group j outer (its bias loaded once), row block i inner.  M % 4 == 0 (launcher), so a 4-row group is
+// wholly inside or outside the matrix.
+template <int MI = 8, bool P32 = false>
+__device__ __forceinline__ void s7_t_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8], int wm, int wn, int fr, int fc,
+                                              int m0, int n0, long bz) {
+  const int row0 = m0 + wm * 16 * MI + 4 * fc;  // + i * 16
+  bf16* const C = (bf16*)g.C + bz * g.sC;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int n = n0 + wn * 128 + j * 16 + fr;
+    const float b = (g.bias && n < g.N) ? g.bias[n] : 0.f;
+    if constexpr (MI == 8)
+      asm volatile("" : "+a"(acc[0][j]), "+a"(acc[1][j]), "+a"(acc[2][j]), "+a"(acc[3][j]), "+a"(acc[4][j]),
+                        "+a"(acc[5][j]), "+a"(acc[6][j]), "+a"(acc[7][j])::"memory");
+    else
+      asm volatile("" : "+a"(acc[0][j]), "+a"(acc[1][j]), "+a"(acc[2][j]), "+a"(acc[3][j]), "+a"(acc[4][j]),
+                        "+a"(acc[5][j])::"memory");
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = row0 + i * 16;
+      const f32x4 v = acc[i][j];
+      const bf16x4 o = {f2bf(v[0] + b), f2bf(v[1] + b), f2bf(v[2] + b), f2bf(v[3] + b)};
+      const int q = (m >> 2) & 7;  // the 4-row group inside its 32-row chunk
+      const int mc = P32 ? (m & ~31) + 8 * (q & 3) + 4 * (q >> 2) : m;
+      if (n < g.N && m < g.M) *(bf16x4*)(C + (long)n * g.ldc + mc) = o;
+    }
+  }
+}
+
 template <int EPI, int MI = 8>
 __device__ __forceinline__ void s7_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8], char* smem, int wave, int lane,
                                             int m0, int n0, long bz) {
   constexpr int BMT = 32 * MI;  // tile rows
   const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fc = lane >> 4;
+  if constexpr (EPI == EPI_BF16_T || EPI == EPI_BF16_TP32) {
+    s7_t_epilogue<MI, EPI == EPI_BF16_TP32>(g, acc, wm, wn, fr, fc, m0, n0, bz);
+    return;
+  }
   float* strip = (float*)(smem + S5_LDS + wave * S7_STRIP);
   const int er = lane >> 2, ec = (lane & 3) * 16;
   if constexpr (EPI == EPI_RES_F32 || EPI == EPI_F32 || EPI == EPI_SILU_F32) {
@@ -702,15 +749,15 @@ __device__ __forceinline__ int s8_ksa(const GemmArgs& g, int ks) {
   return ks;
 }
 
-template <int S, bool PANEL, int MI = 8>
+template <int S, bool PANEL, int MI = 8, bool TR = false>
 __device__ __forceinline__ void s8_step(const GemmArgs& g, const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8],
                                         u32x4 (&b0)[8], u32x4 (&a1)[8], u32x4 (&b1)[8], int ks) {
   s4_wait_frags<MI>(a0, b0);
-  s5_half<S, 1, false, 0, false, MI>(c, acc, a0, b0, a1, b1, 0, 0);
+  s5_half<S, 1, false, 0, false, MI, TR>(c, acc, a0, b0, a1, b1, 0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   s4_wait_frags<MI>(a1, b1);
   __builtin_amdgcn_s_barrier();
-  s5_half<S ^ 1, 0, true, S, true, MI>(c, acc, a1, b1, a0, b0, ks, s8_ksa<PANEL>(g, ks));
+  s5_half<S ^ 1, 0, true, S, true, MI, TR>(c, acc, a1, b1, a0, b0, ks, s8_ksa<PANEL>(g, ks));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -749,15 +796,15 @@ struct S9 {
   }
 };
 
-template <int STAGE_R, int STAGE_D, int MI, int S>
+template <int STAGE_R, int STAGE_D, int MI, int S, bool TR = false>
 __device__ __forceinline__ void s9_slot(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8], u32x4 (&b0)[8],
                                         u32x4 (&a1)[8], u32x4 (&b1)[8], int ks, int ksa) {
   using P = S9<MI>;
   constexpr int kh = S / P::NS, r = S % P::NS, Q = r / 8, j = r % 8;
   if constexpr (kh == 0)
-    s4_mma(acc[Q][j], b0[j], a0[Q]);
+    s4_mma<TR>(acc[Q][j], b0[j], a0[Q]);
   else
-    s4_mma(acc[Q][j], b1[j], a1[Q]);
+    s4_mma<TR>(acc[Q][j], b1[j], a1[Q]);
   constexpr int a = P::act(S);
   // reads of the current tile's second k half come from stage STAGE_R; the next tile's first half from STAGE_R ^ 1
   if constexpr (a >= 1 && a < 9)
@@ -790,19 +837,19 @@ __device__ __forceinline__ void s9_slot(const S5Ctx& c, f32x4 (&acc)[8][8], u32x
   }
 }
 
-template <int STAGE, int MI, int... Ss>
+template <int STAGE, int MI, bool TR, int... Ss>
 __device__ __forceinline__ void s9_slots(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8], u32x4 (&b0)[8],
                                          u32x4 (&a1)[8], u32x4 (&b1)[8], int ks, int ksa,
                                          std::integer_sequence<int, Ss...>) {
-  (s9_slot<STAGE, STAGE, MI, Ss>(c, acc, a0, b0, a1, b1, ks, ksa), ...);
+  (s9_slot<STAGE, STAGE, MI, Ss, TR>(c, acc, a0, b0, a1, b1, ks, ksa), ...);
 }
 
 // step on the K-tile in stage S; ks = the K-tile (x 128 B) the step's DMA fetches into stage S
-template <int S, bool PANEL, int MI = 8>
+template <int S, bool PANEL, int MI = 8, bool TR = false>
 __device__ __forceinline__ void s9_step(const GemmArgs& g, const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8],
                                         u32x4 (&b0)[8], u32x4 (&a1)[8], u32x4 (&b1)[8], int ks) {
   s4_wait_frags<MI>(a0, b0);
-  s9_slots<S, MI>(c, acc, a0, b0, a1, b1, ks, s8_ksa<PANEL>(g, ks), std::make_integer_sequence<int, S9<MI>::TOT>{});
+  s9_slots<S, MI, TR>(c, acc, a0, b0, a1, b1, ks, s8_ksa<PANEL>(g, ks), std::make_integer_sequence<int, S9<MI>::TOT>{});
 }
 
 // MI = 6: 192 x 256 tiles (4 waves x 96 x 128), for launches whose 256-row tile count leaves the last round over
@@ -811,6 +858,7 @@ __device__ __forceinline__ void s9_step(const GemmArgs& g, const S5Ctx& c, f32x4
 template <int EPI, bool PANEL = false, int MI = 8, int SCHED = 8>
 __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) {
   constexpr int BMT = 32 * MI;
+  constexpr bool TR = EPI == EPI_BF16_T || EPI == EPI_BF16_TP32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -891,9 +939,9 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
         c.rw = nx ? nrw : crw;
         const int ksd = (nx ? (has_next ? t + 2 - nk : nk - 1) : t + 2) * 128;
         if constexpr (SCHED == 9)
-          s9_step<0, PANEL, MI>(g, c, acc, a0, b0, a1, b1, ksd);
+          s9_step<0, PANEL, MI, TR>(g, c, acc, a0, b0, a1, b1, ksd);
         else
-          s8_step<0, PANEL, MI>(g, c, acc, a0, b0, a1, b1, ksd);
+          s8_step<0, PANEL, MI, TR>(g, c, acc, a0, b0, a1, b1, ksd);
       }
       {
         const bool nx = t + 3 >= nk;
@@ -901,9 +949,9 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
         c.rw = nx ? nrw : crw;
         const int ksd = (nx ? (has_next ? t + 3 - nk : nk - 1) : t + 3) * 128;
         if constexpr (SCHED == 9)
-          s9_step<1, PANEL, MI>(g, c, acc, a0, b0, a1, b1, ksd);
+          s9_step<1, PANEL, MI, TR>(g, c, acc, a0, b0, a1, b1, ksd);
         else
-          s8_step<1, PANEL, MI>(g, c, acc, a0, b0, a1, b1, ksd);
+          s8_step<1, PANEL, MI, TR>(g, c, acc, a0, b0, a1, b1, ksd);
       }
     }
     asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // MFMA -> v_accvgpr_read
@@ -981,8 +1029,9 @@ template <int EPI>
 int launch(const GemmArgs& g_in, int batch, int kernel, hipStream_t st) {
   // one-time per epilogue instantiation: allow the ping-pong kernel's dynamic LDS size
   static const bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
+    if constexpr (EPI != EPI_BF16_T && EPI != EPI_BF16_TP32)
+      (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                LDS_BYTES);
     return true;
   }();
   (void)attr;
@@ -995,9 +1044,14 @@ int launch(const GemmArgs& g_in, int batch, int kernel, hipStream_t st) {
   const bool s9 = kernel >= KERNEL_S9_AUTO;
   const bool forced = kernel == KERNEL_PERSISTENT || kernel == KERNEL_PERSISTENT192 || kernel == KERNEL_PERSISTENT_AUTO || s9;
   if (forced && !persistent_ok) return SA_ERR_ARG;
+  constexpr bool TOUT = EPI == EPI_BF16_T || EPI == EPI_BF16_TP32;
+  if constexpr (TOUT) {  // the transposed store exists in the persistent kernel only
+    if (!persistent_ok || kernel == KERNEL_PINGPONG || g.M % 4 || g.ldc % 4) return SA_ERR_ARG;
+    if (g.ldc < (EPI == EPI_BF16_TP32 ? (g.M + 31) / 32 * 32 : g.M)) return SA_ERR_ARG;
+  }
   const bool persistent = forced || (kernel == KERNEL_AUTO && persistent_ok);
   const int sched = s9 ? 9 : (kernel == KERNEL_PERSISTENT || kernel == KERNEL_PERSISTENT192) ? 8 : env_sched();
-  constexpr bool BF16_OUT = EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16;
+  constexpr bool BF16_OUT = EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16 || TOUT;
   if (g.group_m == 0) g.group_m = persistent ? (BF16_OUT ? 8 : 4) : (g.N >= 4096 ? 8 : 1);
   const int nn = (g.N + BN - 1) / BN, ncu = num_cus();
   const long n256 = (long)((g.M + 255) / 256) * nn * batch, n192 = (long)((g.M + 191) / 192) * nn * batch;
@@ -1017,11 +1071,16 @@ int launch(const GemmArgs& g_in, int batch, int kernel, hipStream_t st) {
     } else {
       return SA_ERR_ARG;
     }
+  } else if (TOUT) {
+    if (t192)
+      sched == 9 ? s8_launch<EPI, false, 6, 9>(g, batch, pgrid, st) : s8_launch<EPI, false, 6, 8>(g, batch, pgrid, st);
+    else
+      sched == 9 ? s8_launch<EPI, false, 8, 9>(g, batch, pgrid, st) : s8_launch<EPI, false, 8, 8>(g, batch, pgrid, st);
   } else if (persistent && t192) {
     sched == 9 ? s8_launch<EPI, false, 6, 9>(g, batch, pgrid, st) : s8_launch<EPI, false, 6, 8>(g, batch, pgrid, st);
   } else if (persistent) {
     sched == 9 ? s8_launch<EPI, false, 8, 9>(g, batch, pgrid, st) : s8_launch<EPI, false, 8, 8>(g, batch, pgrid, st);
-  } else {
+  } else if constexpr (!TOUT) {
     hipLaunchKernelGGL((gemm_pp_kernel<EPI, true>), dim3(nm * nn, 1, batch), dim3(512), LDS_BYTES, st, g);
   }
   SA_LAUNCH_CHECK();
@@ -1072,9 +1131,15 @@ extern "C" int sa_gemm_bf16_panels(const void* A, int64_t lda, int64_t strideA, 
     case EPI_RES_F32: return launch<EPI_RES_F32>(g, batch, kernel, st);
     case EPI_GELU_ERF_BF16: return launch<EPI_GELU_ERF_BF16>(g, batch, kernel, st);
     case EPI_SILU_F32: return launch<EPI_SILU_F32>(g, batch, kernel, st);
+    case EPI_BF16_T: return launch<EPI_BF16_T>(g, batch, kernel, st);
+    case EPI_BF16_TP32: return launch<EPI_BF16_TP32>(g, batch, kernel, st);
     default: return SA_ERR_ARG;
   }
 }
+
+// rows past the last panel's row M - 1 that the column-panel O-projection may read (its last tile's full height:
+// the panel offset travels in soffset, outside the buffer range check) -- callers size their slack from this
+extern "C" int sa_gemm_panel_slack_rows(void) { return BM; }
 
 extern "C" int sa_gemm_bf16_ex(const void* A, int64_t lda, int64_t strideA, const void* W, int64_t ldw,
                                int64_t strideW, const float* bias, void* C, int64_t ldc, int64_t strideC, int M, int N,

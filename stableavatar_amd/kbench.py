@@ -23,6 +23,23 @@ def _time(fn, iters=10, warmup=2):
     return s.elapsed_time(e) / iters
 
 
+def vt_layout(v, mode, rows_pad=64):
+    """V^T in the layout self-attention kernels 3 / 4 read (sa_attn_fwd_map): [H*128, Rv] bf16, row h*128 + d = d of
+    head h for every key row (rows padded with zeros to a multiple of rows_pad).  mode 3: the keys of each 32-key
+    chunk in P's permuted order (position 8g + j <- key 4g + j for j < 4, 16 + 4g + j - 4 for j >= 4); mode 4: natural
+    order.  Built by torch (tests / A-B only; the DiT's QKV GEMM writes it itself)."""
+    R, HD = v.shape
+    Rv = (R + rows_pad - 1) // rows_pad * rows_pad
+    vt = torch.zeros(HD, Rv, device=v.device, dtype=v.dtype)
+    vt[:, :R] = v.t()
+    if mode == 3:
+        p = torch.arange(32, device=v.device)
+        perm = torch.where(p % 8 < 4, 4 * (p // 8) + p % 8, 16 + 4 * (p // 8) + p % 8 - 4)
+        idx = (torch.arange(Rv, device=v.device) // 32) * 32 + perm[torch.arange(Rv, device=v.device) % 32]
+        vt = vt[:, idx].contiguous()
+    return vt
+
+
 def main(which=("gemm", "attn")):
     dev = "cuda"
     torch.manual_seed(0)
@@ -89,17 +106,28 @@ def main(which=("gemm", "attn")):
         q, k, v_ = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
         outs = {}
         variants = tuple(int(v) for v in os.environ.get("SA_KB_AVARS", "1").split(","))
+        vts = {m: vt_layout(v_, m) for m in (3, 4) if m in variants}  # kernels 3 / 4 read V^T
         times = {v: [] for v in variants}
         for rnd in range(3):
             for v in variants:
                 o = torch.empty(3 * L, H * D, device=dev, dtype=torch.bfloat16)
-                times[v].append(_time(lambda: ops.attention(q, k, v_, o, segs, 3, L, H, kernel=v), iters=3, warmup=1))
+                vin = vts.get(v, v_)
+                times[v].append(_time(lambda: ops.attention(q, k, vin, o, segs, 3, L, H, kernel=v), iters=3, warmup=1))
                 outs[v] = o.float()
+        # fp32 reference on a sample of query rows of every head (batch row 2)
+        qi = torch.arange(0, L, 997, device=dev)
+        ref = torch.empty(len(qi), H * D, device=dev)
+        for hh in range(H):
+            sl = slice(hh * D, (hh + 1) * D)
+            s_ = (q[2 * L + qi, sl].float() @ k[2 * L:, sl].float().t()) * D ** -0.5
+            ref[:, sl] = torch.softmax(s_, -1) @ v_[2 * L:, sl].float()
         fl = 4.0 * 3 * H * L * L * D
         r = {"kernel": "attn_self"}
         for v in variants:
             ms = sorted(times[v])[1]
             r[f"err_v{v}_v{variants[0]}"] = ((outs[v] - outs[variants[0]]).norm() / outs[variants[0]].norm()).item()
+            r[f"v{v}_bitident"] = bool(torch.equal(outs[v], outs[variants[0]]))
+            r[f"err_v{v}_fp32"] = ((outs[v][2 * L + qi] - ref).norm() / ref.norm()).item()
             r[f"v{v}_ms"] = round(ms, 3)
             r[f"v{v}_tflops"] = round(fl / ms / 1e9, 1)
         res.append(r)

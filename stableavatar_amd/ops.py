@@ -8,7 +8,7 @@ import torch
 
 from ._lib import call
 
-EPI_BF16, EPI_GELU_TANH_BF16, EPI_F32, EPI_RES_F32, EPI_GELU_ERF_BF16, EPI_SILU_F32 = range(6)
+EPI_BF16, EPI_GELU_TANH_BF16, EPI_F32, EPI_RES_F32, EPI_GELU_ERF_BF16, EPI_SILU_F32, EPI_BF16_T, EPI_BF16_TP32 = range(8)
 F32, BF16 = 0, 1
 
 
@@ -63,10 +63,15 @@ def linear(x, weight, bias=None, epilogue=EPI_BF16, out=None, residual=None, gat
             raise ValueError("linear: the column panels run past x's storage")
     assert weight.shape[1] == K and x.stride(1) == 1 and weight.stride(1) == 1
     f32_out = epilogue in (EPI_F32, EPI_RES_F32, EPI_SILU_F32)
-    if out is None:
+    if epilogue in (EPI_BF16_T, EPI_BF16_TP32):  # out = C^T [N, >= M] (row n = column n of the product: V^T)
+        if out is None:
+            out = torch.empty(N, (M + 63) // 64 * 64, device=x.device, dtype=torch.bfloat16)
+        if out.dtype != torch.bfloat16 or out.stride(1) != 1 or out.shape[0] != N or out.shape[1] < M:
+            raise ValueError(f"linear: EPI_BF16_T(P32) needs out bf16 [N, >= M], got {tuple(out.shape)}")
+    elif out is None:
         out = torch.empty(M, N, device=x.device, dtype=torch.float32 if f32_out else torch.bfloat16)
     assert out.dtype == (torch.float32 if f32_out else torch.bfloat16) and out.stride(1) == 1
-    if tuple(out.shape) != (M, N):
+    if epilogue not in (EPI_BF16_T, EPI_BF16_TP32) and tuple(out.shape) != (M, N):
         raise ValueError(f"linear: out shape {tuple(out.shape)} != {(M, N)}")
     if bias is not None:
         _check(bias, torch.float32, "linear.bias")
@@ -94,6 +99,9 @@ def bmm_nt(a, b, out, epilogue=EPI_F32, kernel=GEMM_AUTO):
 
 
 ATTN_AUTO = 0
+# kernel ids of sa_attn_fwd_ex that read V as V^T [H*128, Rv]: 3 = keys permuted per 32 in P's order (the QKV GEMM's
+# EPI_BF16_TP32 output), 4 = natural order with the PV product on 32x32x16 MFMAs (measured slower, kept for A/B)
+ATTN_VT_P32, ATTN_VT_PV32 = 3, 4
 
 
 def attention(q, k, v, out, segs, nseg, max_q_len, heads, head_dim=128, scale=None, accumulate=False,

@@ -65,6 +65,12 @@ def make_plan(world: int, rank: int, heads: int) -> SPPlan:
     return SPPlan(world, rank, heads, G, world // G)
 
 
+def _panel_slack_rows() -> int:
+    """Rows the column-panel O-projection may read past its last panel (sa_gemm_panel_slack_rows)."""
+    from . import _lib
+    return int(_lib.lib().sa_gemm_panel_slack_rows())
+
+
 def padded_len(seq_len: int, world: int) -> int:
     """1B:980-981: the token axis is padded up to a multiple of the SP degree."""
     return int(math.ceil(seq_len / world)) * world
@@ -162,9 +168,13 @@ class UlyssesExchange:
         self.Lq, self.Lp = G * Lc, N * Lc
         self.q = torch.empty(B * self.Lq, hgd, device=device, dtype=dtype)
         self.kv = torch.empty(B * self.Lp, 2 * hgd, device=device, dtype=dtype)
-        # + 256 rows of slack: the O-projection's last tile reads up to 256 rows past the last panel
-        # (sa_gemm_bf16_panels; the buffer range check does not cover the panel offset)
-        self.obuf = torch.empty(2 * G * B * Lc + 256, hgd, device=device, dtype=dtype)
+        # + slack rows: the O-projection's last tile reads up to its tile height past the last panel
+        # (sa_gemm_bf16_panels; the buffer range check does not cover the panel offset).  The slack comes from
+        # the library (sa_gemm_panel_slack_rows = the tallest GEMM tile), so a taller tile cannot outgrow it.
+        # On the per-row-stream path (transformer._sp_layer_rows) row b's O-projection tail tile also reads
+        # into row b+1's panel region while another stream may be writing it: benign, those rows' products are
+        # discarded (never stored), only their bytes are fetched.
+        self.obuf = torch.empty(2 * G * B * Lc + _panel_slack_rows(), hgd, device=device, dtype=dtype)
         self.pan = self.obuf[G * B * Lc:2 * G * B * Lc]
         self.remote = [d for d in range(N) if d != p.rank or self.loopback]
         self.sq = {d: torch.empty(B, Lc, hgd, device=device, dtype=dtype) for d in self.remote if d // G == p.part}

@@ -373,6 +373,9 @@ class WanTransformer3DFantasyModel(nn.Module):
             L = SimpleNamespace()
             L.w_qkv = cat_bf(p + "self_attn.q.weight", p + "self_attn.k.weight", p + "self_attn.v.weight")
             L.b_qkv = cat_f(p + "self_attn.q.bias", p + "self_attn.k.bias", p + "self_attn.v.bias")
+            # views for the single-GPU V^T path: q|k rows into the QKV rows, v into V^T (EPI_BF16_TP32)
+            L.w_qk, L.b_qk = L.w_qkv[:2 * self.dim], L.b_qkv[:2 * self.dim]
+            L.w_v, L.b_v = L.w_qkv[2 * self.dim:], L.b_qkv[2 * self.dim:]
             L.nq, L.nk = f32(p + "self_attn.norm_q.weight"), f32(p + "self_attn.norm_k.weight")
             L.w_o, L.b_o = bf(p + "self_attn.o.weight"), f32(p + "self_attn.o.bias")
             L.n3w, L.n3b = f32(p + "norm3.weight"), f32(p + "norm3.bias")
@@ -438,9 +441,17 @@ class WanTransformer3DFantasyModel(nn.Module):
                 qkv=torch.empty(M, 3 * dim, device=dev, dtype=torch.bfloat16),
                 att=torch.empty(M, dim, device=dev, dtype=torch.bfloat16),
                 ffn=torch.empty(M, self.ffn_dim, device=dev, dtype=torch.bfloat16),
+                vt=None,  # V^T [dim, M rounded up to 64] of the single-GPU self-attention, allocated on first use
             )
             self._ws = {key: ws}  # keep one shape at a time
         return ws
+
+    def _vt_attention(self, Lp, dev) -> bool:
+        """the single-GPU self-attention reads V as V^T written by the QKV GEMM's transposed epilogue (attention
+        kernel 3: 6.20 vs 6.41 ms per config-2 launch, bit-identical, profiles/r05/attn_ab_v6_v6t_v12_r5b.jsonl)
+        when the batch rows start on 32-key boundaries; SA_ATTN_VT=0 or an explicit attn_kernel keeps V in rows"""
+        return (dev.type == "cuda" and self.attn_kernel == 0 and Lp % 32 == 0
+                and os.environ.get("SA_ATTN_VT", "1") != "0")
 
     # ------------------------------------------------------------------ context (step-invariant)
 
@@ -812,6 +823,10 @@ class WanTransformer3DFantasyModel(nn.Module):
             use_cross3 = (ctx.img_len > 0 and G % 256 == 0 and (rank * Lc) % 256 == 0 and (rank + 1) * Lc <= S
                           and os.environ.get("SA_CROSS3", "1") != "0")
             x = ws.x
+            use_vt = not SP and self._vt_attention(Lp, dev)
+            if use_vt and ws.vt is None:
+                # zero-filled once: the pad columns past B * Lp are read (as P = 0 keys) by a partial last block
+                ws.vt = torch.zeros(dim, (ws.x.shape[0] + 63) // 64 * 64, device=dev, dtype=torch.bfloat16)
             kvv = torch.empty(B * n_fr * nper, 2 * dim, device=dev, dtype=torch.bfloat16)  # per-frame vocal K|V
             grid = (Fw, hp, wp)
             if sp_streams:
@@ -882,6 +897,17 @@ class WanTransformer3DFantasyModel(nn.Module):
                     a0, pnl = ex.panels()
                     ops.linear(a0, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2],
                                rows_per_batch=Lc, a_panels=pnl)
+                elif use_vt:
+                    # q|k into the QKV rows, v straight into V^T (keys in P's order per 32) for attention kernel 3
+                    ops.linear(ws.mod, L.w_qk, L.b_qk, ops.EPI_BF16, out=ws.qkv[:, :2 * dim])
+                    ops.linear(ws.mod, L.w_v, L.b_v, ops.EPI_BF16_TP32, out=ws.vt)
+                    ops.qk_rmsnorm_rope(ws.qkv, 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
+                    ev0 = self._record_event()
+                    ops.attention(ws.qkv[:, :dim], ws.qkv[:, dim:2 * dim], ws.vt, ws.att, segs_self, B, Lp, H_,
+                                  kernel=ops.ATTN_VT_P32)
+                    self._record_span(ev0, rows=B, batch=B)
+                    ops.linear(ws.att, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2],
+                               rows_per_batch=Lc)
                 else:
                     ops.linear(ws.mod, L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv)
                     ops.qk_rmsnorm_rope(ws.qkv, 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)

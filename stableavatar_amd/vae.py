@@ -241,8 +241,9 @@ class _ChainState:
         elif _gloo(self.group):
             self.sends.append((dist.isend(val, self.next_g, group=self.group), val))
         else:
+            # keep every Work batch_isend_irecv returns: finish() waits on all of them
             ws = dist.batch_isend_irecv([dist.P2POp(dist.isend, val, group=self.group, group_peer=self.rank + 1)])
-            self.sends.append((ws[0] if len(ws) == 1 else None, val))
+            self.sends.append((list(ws or []), val))
 
     def skip(self, key, like):
         prev = self.get(key, like)
@@ -252,8 +253,8 @@ class _ChainState:
 
     def finish(self):
         for w, _ in self.sends:
-            if w is not None:
-                w.wait()
+            for x in (w if isinstance(w, list) else [w]):
+                x.wait()
         self.sends = []
 
 

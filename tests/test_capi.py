@@ -13,7 +13,7 @@ def _header_decls():
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     out = {}
     for m in re.finditer(r"\bint\s+(sa_\w+)\s*\(([^)]*)\)\s*;", txt, flags=re.S):
-        params = [p.strip() for p in m.group(2).replace("\n", " ").split(",") if p.strip()]
+        params = [p.strip() for p in m.group(2).replace("\n", " ").split(",") if p.strip() and p.strip() != "void"]
         codes = ""
         for p in params:
             if "*" in p:

@@ -192,6 +192,36 @@ def test_dit_block_fullsize_vs_oracle():
     assert e < 2e-2 and cos > 0.9995, (e, cos)
 
 
+@pytest.mark.timeout(300)
+def test_dit_vt_attention_matches_row_v(monkeypatch):
+    """the single-GPU self-attention reading V^T from the QKV GEMM's transposed (P-order) epilogue == the V-rows
+    path at the config-2 shape (1 full-width layer, L = 21 504, B = 3): the GEMM products and the attention
+    arithmetic are the same, so the forward must agree to bf16 rounding of the V projection at most"""
+    from stableavatar_amd.transformer import WanTransformer3DFantasyModel, param_shapes
+    cfg = dict(DIT_FULL, num_layers=1)
+    m = WanTransformer3DFantasyModel(**cfg)
+    m.load_state_dict(synthetic.fill_state_dict(param_shapes(cfg), 53))
+    m = m.to(dev)
+    lat = synthetic.seeded_normal((1, 16, 21, 64, 64), 521)
+    x = torch.cat([lat] * 3).to(dev).bfloat16()
+    y = synthetic.seeded_normal((3, 20, 21, 64, 64), 522).to(dev).bfloat16()
+    ctx = [c.to(dev) for c in [synthetic.seeded_normal((24, 4096), 523)] * 2 + [synthetic.seeded_normal((31, 4096), 524)]]
+    clip = synthetic.seeded_normal((1, 257, 1280), 525).expand(3, -1, -1).contiguous().to(dev)
+    a = synthetic.seeded_normal((1, 167, 768), 526)
+    voc = torch.cat([torch.zeros_like(a), a, a]).to(dev)
+    t = torch.full((3,), 937.5, device=dev)
+    outs = {}
+    for vt in ("1", "0"):
+        monkeypatch.setenv("SA_ATTN_VT", vt)
+        with torch.no_grad():
+            outs[vt] = m(x=x, t=t, context=ctx, seq_len=L, clip_fea=clip, y=y, vocal_embeddings=voc,
+                         video_sample_n_frames=81).float()
+    assert next(iter(m._ws.values())).vt is not None  # the V^T path ran
+    e = rel(outs["1"], outs["0"])
+    print(f"DiT layer V^T vs V rows: rel-L2 {e:.2e}, bit-identical {torch.equal(outs['1'], outs['0'])}")
+    assert torch.equal(outs["1"], outs["0"]), e
+
+
 @pytest.mark.timeout(600)
 def test_dit_ragged_nonsquare_vs_oracle():
     """A non-square size whose token counts align with nothing: 240x416 video (30x52 latent, 15x26 = 390

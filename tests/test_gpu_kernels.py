@@ -78,6 +78,29 @@ def test_gemm_kernels(kernel, M, N, K):
     assert rel(o, a.float() @ bb.float().transpose(1, 2)) < 2e-3
 
 
+@pytest.mark.parametrize("M,N,K", [(1000, 384, 1536), (64512 // 8, 1536, 1536), (300, 130, 256)])
+def test_gemm_transposed_output(M, N, K):
+    """EPI_BF16_T (the QKV GEMM's V^T output for self-attention kernel 4): C^T[n, m] = bf16(x @ w^T + b)[m, n] vs the
+    row-major epilogue, ragged M / N tiles; the pad columns past M are left untouched"""
+    from stableavatar_amd import ops
+    x = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device=dev)
+    Rv = (M + 63) // 64 * 64
+    out = torch.full((N, Rv), 7.0, device=dev, dtype=torch.bfloat16)
+    ops.linear(x, w, b, ops.EPI_BF16_T, out=out)
+    y = ops.linear(x, w, b, ops.EPI_BF16)
+    print(f"EPI_BF16_T vs EPI_BF16 bit-identical: {torch.equal(out[:, :M].t(), y)}")
+    assert rel(out[:, :M].t(), y) < 1e-3
+    assert rel(out[:, :M].t(), x.float() @ w.float().t() + b) < 1e-2
+    assert (out[:, M:] == 7.0).all()
+    # P32: the rows of each 32-row chunk in the attention's P order = kbench.vt_layout(y, 3)
+    from stableavatar_amd.kbench import vt_layout
+    outp = torch.zeros(N, Rv, device=dev, dtype=torch.bfloat16)
+    ops.linear(x, w, b, ops.EPI_BF16_TP32, out=outp)
+    assert torch.equal(outp, vt_layout(out[:, :M].t().contiguous(), 3))
+
+
 def test_gemm_persistent_rejects_k192():
     """the persistent kernel needs K % 128 == 0: an explicit request is refused, auto falls back"""
     from stableavatar_amd import ops
@@ -128,6 +151,54 @@ def test_attention_segments(Lq, Lk, kernel):
     o2 = o.clone()
     ops.attention(q, k, v, o2, segs, B, Lq, H, accumulate=True, kernel=kernel)
     assert rel(o2, 2 * o.float()) < 1e-2
+
+
+@pytest.mark.parametrize("kernel", [3, 4], ids=["v6t_vt_perm32", "v12_vt_pv32x32"])
+@pytest.mark.parametrize("B,Lq,Lk", [(2, 300, 320), (2, 512, 256), (1, 256, 1000), (3, 64, 64)])
+def test_attention_vt_kernels(kernel, B, Lq, Lk):
+    """the self-attention forms that read V as V^T [H*128, Rv] (kernel 3: keys permuted per 32 as P; 4: the PV
+    product on 32x32x16 MFMAs, natural key order) vs fp32 torch, incl. a ragged last key block and accumulate"""
+    from stableavatar_amd import ops
+    from stableavatar_amd.kbench import vt_layout
+    H, D = 3, 128
+    q = torch.randn(B * Lq, H * D + 64, device=dev).bfloat16()[:, :H * D]
+    k = torch.randn(B * Lk, H * D, device=dev).bfloat16()
+    v = torch.randn(B * Lk, H * D, device=dev).bfloat16()
+    vt = vt_layout(v, kernel)
+    o = torch.empty(B * Lq, H * D, device=dev, dtype=torch.bfloat16)
+    segs = torch.tensor([[b * Lq, Lq, b * Lk, Lk] for b in range(B)], dtype=torch.int32, device=dev)
+    ops.attention(q, k, vt, o, segs, B, Lq, H, kernel=kernel)
+    for b in range(B):
+        for h in range(H):
+            sl = slice(h * D, (h + 1) * D)
+            ref = _ref_attn(q[b * Lq:(b + 1) * Lq, sl], k[b * Lk:(b + 1) * Lk, sl], v[b * Lk:(b + 1) * Lk, sl], D ** -0.5)
+            assert rel(o[b * Lq:(b + 1) * Lq, sl], ref) < 1e-2, (b, h)
+    o2 = o.clone()
+    ops.attention(q, k, vt, o2, segs, B, Lq, H, accumulate=True, kernel=kernel)
+    assert rel(o2, 2 * o.float()) < 1e-2
+
+
+@pytest.mark.parametrize("kernel", [3, 4], ids=["v6t_vt_perm32", "v12_vt_pv32x32"])
+def test_attention_vt_spike_rescale(kernel):
+    """the rescale branch of the V^T forms (the v12 form rescales its 32x32 accumulators with the lane's query)"""
+    from stableavatar_amd import ops
+    from stableavatar_amd.kbench import vt_layout
+    L, D = 512, 128
+    q = torch.randn(L, D, device=dev).bfloat16()
+    k = torch.randn(L, D, device=dev).bfloat16()
+    k[400] = q[5] * 4
+    k[440] = q[9] * 4
+    k[33] = q[20] * 2
+    ramp = torch.linspace(0.2, 3.0, L, device=dev)[:, None]
+    k[:, :] = (k.float() + ramp * q[17].float()).bfloat16()
+    v = torch.randn(L, D, device=dev).bfloat16()
+    o = torch.empty_like(q)
+    segs = torch.tensor([[0, L, 0, L]], dtype=torch.int32, device=dev)
+    ops.attention(q, k, vt_layout(v, kernel), o, segs, 1, L, 1, kernel=kernel)
+    ref = _ref_attn(q, k, v, D ** -0.5)
+    assert rel(o, ref) < 1e-2
+    for r in (5, 9, 17, 20):
+        assert rel(o[r], ref[r]) < 1e-2, r
 
 
 def test_attention_vocal_grouping():
@@ -199,6 +270,64 @@ def test_attention_cross3(tok_offset):
                 vo[r0:r0 + 64] = _ref_attn(qq[r0:r0 + 64], kvv[kr, sl], kvv[kr, sv], sc)
             ref = (t + i) + vo.bfloat16()
             assert rel(o[b * Lq:(b + 1) * Lq, sl], ref) < 1e-2, (b, h)
+
+
+def _nan_tail(rows, cols, pad=96):
+    """[rows, cols] bf16 random rows followed by `pad` rows of NaN in the same allocation"""
+    big = torch.full((rows + pad, cols), float("nan"), device=dev, dtype=torch.bfloat16)
+    big[:rows] = torch.randn(rows, cols, device=dev).bfloat16()
+    return big, big[:rows]
+
+
+@pytest.mark.parametrize("kernel", [1, 2], ids=["wg256", "wg128"])
+def test_attention_tail_block_stays_inside_segment(kernel):
+    """a partial last key block must not read the rows past its segment (the block offset in
+    soffset is outside the buffer range check): K/V rows past the last segment are NaN, the output must
+    match fp32 torch over the segment's keys only"""
+    from stableavatar_amd import ops
+    B, H, D, Lq, Lk = 2, 2, 128, 200, 257
+    q = torch.randn(B * Lq, H * D, device=dev).bfloat16()
+    _, k = _nan_tail(B * Lk, H * D)
+    _, v = _nan_tail(B * Lk, H * D)
+    o = torch.empty(B * Lq, H * D, device=dev, dtype=torch.bfloat16)
+    segs = torch.tensor([[b * Lq, Lq, b * Lk, Lk] for b in range(B)], dtype=torch.int32, device=dev)
+    ops.attention(q, k, v, o, segs, B, Lq, H, kernel=kernel)
+    assert torch.isfinite(o.float()).all()
+    b = B - 1
+    for h in range(H):
+        sl = slice(h * D, (h + 1) * D)
+        ref = _ref_attn(q[b * Lq:(b + 1) * Lq, sl], k[b * Lk:(b + 1) * Lk, sl], v[b * Lk:(b + 1) * Lk, sl], D ** -0.5)
+        assert rel(o[b * Lq:(b + 1) * Lq, sl], ref) < 1e-2, h
+
+
+def test_attention_cross3_tail_blocks_stay_inside_sources():
+    """fused cross-attention with every source's K/V followed by NaN rows: the image stream's last block (257 =
+    4 x 64 + 1 keys) and the vocal half block (17 of 32 keys) of the last batch row / last frame must read
+    zeros past their source, not the NaN that follows"""
+    from stableavatar_amd import ops
+    B, H, D, tpf, F, nper, tl, il = 2, 2, 128, 256, 2, 17, 512, 257
+    HD = H * D
+    Lq = F * tpf
+    q = torch.randn(B * Lq, HD, device=dev).bfloat16()
+    _, kvt = _nan_tail(B * tl, 2 * HD)
+    _, kvi = _nan_tail(B * il, 2 * HD)
+    _, kvv = _nan_tail(B * F * nper, 2 * HD)
+    o = torch.empty(B * Lq, HD, device=dev, dtype=torch.bfloat16)
+    ops.attention_cross3(q, kvt[:, :HD], kvt[:, HD:], tl, kvi[:, :HD], kvi[:, HD:], il, kvv[:, :HD], kvv[:, HD:],
+                         nper, tpf, F, o, B, Lq, H)
+    assert torch.isfinite(o.float()).all()
+    sc = D ** -0.5
+    b = B - 1
+    for h in range(H):
+        sl, sv = slice(h * D, (h + 1) * D), slice(HD + h * D, HD + (h + 1) * D)
+        qq = q[b * Lq:(b + 1) * Lq, sl]
+        t = _ref_attn(qq, kvt[b * tl:(b + 1) * tl, sl], kvt[b * tl:(b + 1) * tl, sv], sc).bfloat16()
+        i = _ref_attn(qq, kvi[b * il:(b + 1) * il, sl], kvi[b * il:(b + 1) * il, sv], sc).bfloat16()
+        vo = torch.empty(Lq, D, device=dev)
+        for f in range(F):
+            kr = slice((b * F + f) * nper, (b * F + f + 1) * nper)
+            vo[f * tpf:(f + 1) * tpf] = _ref_attn(qq[f * tpf:(f + 1) * tpf], kvv[kr, sl], kvv[kr, sv], sc)
+        assert rel(o[b * Lq:(b + 1) * Lq, sl], (t + i) + vo.bfloat16()) < 1e-2, h
 
 
 @pytest.mark.parametrize("D,H,segs", [
