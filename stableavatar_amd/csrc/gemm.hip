@@ -855,7 +855,8 @@ __device__ __forceinline__ void s9_step(const GemmArgs& g, const S5Ctx& c, f32x4
 // MI = 6: 192 x 256 tiles (4 waves x 96 x 128), for launches whose 256-row tile count leaves the last round over
 // the CUs mostly empty (the per-rank GEMMs of sequence parallelism: 8 064 rows at N = 8 fill 0.74 of a round of
 // 256 x 256 tiles, 0.98 of a round of 192 x 256)
-template <int EPI, bool PANEL = false, int MI = 8, int SCHED = 8>
+// NOEPI (measurement only, kernels 8 / 9 of sa_gemm_bf16_ex): the tile walk and K loop without the epilogue
+template <int EPI, bool PANEL = false, int MI = 8, int SCHED = 8, bool NOEPI = false>
 __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) {
   constexpr int BMT = 32 * MI;
   constexpr bool TR = EPI == EPI_BF16_T || EPI == EPI_BF16_TP32;
@@ -955,7 +956,7 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
       }
     }
     asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // MFMA -> v_accvgpr_read
-    s7_epilogue<EPI, MI>(g, acc, smem, wave, lane, m0, n0, bz);
+    if constexpr (!NOEPI) s7_epilogue<EPI, MI>(g, acc, smem, wave, lane, m0, n0, bz);
     if (!has_next) break;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -974,23 +975,25 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
 constexpr int KERNEL_AUTO = 0, KERNEL_PINGPONG = 1, KERNEL_PERSISTENT = 2, KERNEL_PERSISTENT192 = 3;
 constexpr int KERNEL_PERSISTENT_AUTO = 4;  // internal: the persistent kernel with the tile rows chosen as by auto
 // the s9 (three-barrier) schedule of the persistent kernel: tile rows by auto / 256 / 192
-constexpr int KERNEL_S9_AUTO = 5, KERNEL_S9 = 6, KERNEL_S9_192 = 7, KERNEL_MAX = 7;
+constexpr int KERNEL_S9_AUTO = 5, KERNEL_S9 = 6, KERNEL_S9_192 = 7;
+// measurement only: the s9 kernel with the epilogue removed (256- / 192-row tiles), output not written
+constexpr int KERNEL_S9_NOEPI = 8, KERNEL_S9_192_NOEPI = 9, KERNEL_MAX = 9;
 
 // dynamic-LDS opt-in of one persistent instantiation, once per process
-template <int EPI, bool PANEL, int MI, int SCHED>
+template <int EPI, bool PANEL, int MI, int SCHED, bool NOEPI = false>
 void s8_attr() {
   static const bool once = [] {
-    (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI, PANEL, MI, SCHED>,
+    (void)hipFuncSetAttribute((const void*)gemm_s8_kernel<EPI, PANEL, MI, SCHED, NOEPI>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, S7_LDS);
     return true;
   }();
   (void)once;
 }
 
-template <int EPI, bool PANEL, int MI, int SCHED>
+template <int EPI, bool PANEL, int MI, int SCHED, bool NOEPI = false>
 void s8_launch(const GemmArgs& g, int batch, dim3 grid, hipStream_t st) {
-  s8_attr<EPI, PANEL, MI, SCHED>();
-  hipLaunchKernelGGL((gemm_s8_kernel<EPI, PANEL, MI, SCHED>), grid, dim3(256), S7_LDS, st, g, batch);
+  s8_attr<EPI, PANEL, MI, SCHED, NOEPI>();
+  hipLaunchKernelGGL((gemm_s8_kernel<EPI, PANEL, MI, SCHED, NOEPI>), grid, dim3(256), S7_LDS, st, g, batch);
 }
 
 // the persistent schedule auto picks (SA_GEMM_SCHED=8|9 overrides, read once per process)
@@ -1036,6 +1039,22 @@ int launch(const GemmArgs& g_in, int batch, int kernel, hipStream_t st) {
   }();
   (void)attr;
   GemmArgs g = g_in;
+  if (kernel == KERNEL_S9_NOEPI || kernel == KERNEL_S9_192_NOEPI) {
+    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_RES_F32) {
+      if (g.K % 128 || (long)BM * g.lda * 2 >= 0x7fffffffL || (long)BN * g.ldw * 2 >= 0x7fffffffL) return SA_ERR_ARG;
+      if (g.group_m == 0) g.group_m = EPI == EPI_RES_F32 ? 4 : 8;
+      const int bmt = kernel == KERNEL_S9_NOEPI ? 256 : 192;
+      const int tiles = ((g.M + bmt - 1) / bmt) * ((g.N + BN - 1) / BN) * batch;
+      const dim3 grid(min(tiles, num_cus()));
+      if (kernel == KERNEL_S9_NOEPI)
+        s8_launch<EPI, false, 8, 9, true>(g, batch, grid, st);
+      else
+        s8_launch<EPI, false, 6, 9, true>(g, batch, grid, st);
+      SA_LAUNCH_CHECK();
+      return SA_OK;
+    }
+    return SA_ERR_ARG;
+  }
   // auto (measured, profiles/r01/gemm_ab_r4.md): the persistent one-wave-per-SIMD LDS-DMA kernel
   // wherever its K % 128 tiling and 32-bit buffer offsets apply (over the ping-pong: QKV +8-15 %,
   // cross-Q +7-10 %, FFN-up +3-4 %, FFN-down +4 %, O-proj +-1 %), else the ping-pong kernel (e.g. the

@@ -82,6 +82,8 @@ def main(which=("gemm", "attn")):
                     o = out.float()
                     if ref is None:
                         ref = o.clone()
+                    if int(vv) >= 8:  # the no-epilogue measurement kernels write nothing
+                        continue
                     err = ((o - ref).norm() / ref.norm()).item()
                     assert err < 1e-2, (name, v, err)
                     same.setdefault(v, True)

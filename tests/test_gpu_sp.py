@@ -162,6 +162,73 @@ def test_sp_rccl_path_degree1(overlap):
         assert same, (case, loop, err)
 
 
+def _rccl_fullsize_worker(port, overlap, qret):
+    """config-2 size on the RCCL transport: a 1-layer full-width 1.3B DiT (dim 1536, 12 heads, ffn 8960) at the
+    512^2 x 81f shape (L = 21 504 tokens, B = 3 CFG rows), Ulysses at degree 1 with loopback transfers (every Q/K/V
+    and head-output slab of the layer -- 3 x 21 504 tokens -- moved by RCCL P2P ops to this rank itself) in the
+    given exchange schedule, vs the single-GPU forward of the same process"""
+    os.environ["SA_SP_OVERLAP"] = overlap
+    import torch.distributed as dist
+    sys.path.insert(0, HERE)
+    from golden_cases import DIT_FULL
+    from stableavatar_amd import synthetic
+    from stableavatar_amd.transformer import WanTransformer3DFantasyModel, param_shapes
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda:0"))
+    try:
+        dev = "cuda"
+        cfg = dict(DIT_FULL, num_layers=1)
+        m = WanTransformer3DFantasyModel(**cfg)
+        m.load_state_dict(synthetic.fill_state_dict(param_shapes(cfg), 54))
+        m = m.to(dev)
+        L = 21504
+        lat = synthetic.seeded_normal((1, 16, 21, 64, 64), 531)
+        x = torch.cat([lat] * 3).to(dev).bfloat16()
+        y = synthetic.seeded_normal((3, 20, 21, 64, 64), 532).to(dev).bfloat16()
+        ctx = [c.to(dev) for c in [synthetic.seeded_normal((24, 4096), 533)] * 2 +
+               [synthetic.seeded_normal((31, 4096), 534)]]
+        clip = synthetic.seeded_normal((1, 257, 1280), 535).expand(3, -1, -1).contiguous().to(dev)
+        a = synthetic.seeded_normal((1, 167, 768), 536)
+        voc = torch.cat([torch.zeros_like(a), a, a]).to(dev)
+        t = torch.full((3,), 937.5, device=dev)
+
+        def fwd():
+            with torch.no_grad():
+                o = m(x=x, t=t, context=ctx, seq_len=L, clip_fea=clip, y=y, vocal_embeddings=voc,
+                      video_sample_n_frames=81).float()
+            torch.cuda.synchronize()
+            return o
+        m.disable_multi_gpus_inference()
+        single = fwd()
+        m.enable_multi_gpus_inference(loopback=True)
+        assert dist.get_backend() == "nccl" and m._sp_enabled
+        par = fwd()
+        ex = m._sp_ex[1]
+        qret.put([(torch.equal(par, single), ((par - single).norm() / single.norm()).item(), ex.loopback,
+                   len(ex.remote), tuple(ex.q.shape))])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("overlap", ["4", "0"], ids=["row_streams", "batched"])
+def test_sp_rccl_fullsize_degree1(overlap):
+    """BASELINE config 2's shape through the RCCL exchange (degree 1, loopback): bit-identical to one GPU"""
+    ctx = mp.get_context("spawn")
+    qret = ctx.Queue()
+    p = ctx.Process(target=_rccl_fullsize_worker, args=(_free_port(), overlap, qret))
+    p.start()
+    res = collect([p], qret, 1, timeout=360)[0]
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    same, err, ex_loop, n_remote, qshape = res[0]
+    print(f"RCCL degree 1 loopback, config-2 shape (L = 21504, B = 3, q slab {qshape}), overlap {overlap}: "
+          f"bit-identical {same} (rel {err:.1e})")
+    assert ex_loop and n_remote == 1
+    assert same, err
+
+
 def _rccl_dp_vae_worker(port, qret):
     """window parallelism's async all_gather_into_tensor (sp.all_gather_slots) on a one-rank RCCL group, and the VAE
     decode's causal-cache wavefront over 3 virtual ranks whose hand-offs are RCCL transfers to this rank itself"""

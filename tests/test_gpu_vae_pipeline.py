@@ -51,6 +51,33 @@ def test_vae_decode_vs_reference(name):
     assert psnr(out, g, 2.0) > 40.0 and rel(out, g) < 3e-2, (psnr(out, g, 2.0), rel(out, g))
 
 
+@pytest.mark.timeout(300)
+def test_vae_decode_fullsize_first_frames_vs_oracle():
+    """The config-2 decode at full size: the 81 x 512^2 clip's latents [16, 21, 64, 64] decoded by the HIP path
+    (full width dim 96, the bench's chunked decode with the causal caches carried) -- its first 9 output frames
+    (latent frames 0-2) vs the fp32 CPU oracle (oracle/vae.py, pinned to wan_vae.py:549-574 by the goldens) on those
+    3 latent frames: the decoder is causal, so they depend on nothing later.  PSNR >= 40 dB over [-1, 1]."""
+    from oracle import vae as ovae
+    from stableavatar_amd.vae import encoder_param_shapes, param_shapes
+    P = synthetic.fill_state_dict(dict(param_shapes(dim=96), **encoder_param_shapes(dim=96)), 61)
+    from stableavatar_amd.vae import AutoencoderKLWan
+    v = AutoencoderKLWan(dim=96)
+    v.load_state_dict(P, strict=True)
+    v = v.cuda()
+    z = synthetic.seeded_normal((16, 21, 64, 64), 611)
+    with torch.no_grad():
+        video = v.decode_clip(z.cuda())  # [3, 81, 512, 512]
+    torch.cuda.synchronize()
+    assert tuple(video.shape) == (3, 81, 512, 512) and torch.isfinite(video).all()
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    with torch.no_grad():
+        ref = ovae.decode(P, z[None, :, :3])[0]  # [3, 9, 512, 512]
+    got = video[:, :9].float().cpu()
+    p, r = psnr(got, ref, 2.0), rel(got, ref)
+    print(f"VAE decode 81x512^2, frames 0-8 vs fp32 oracle: PSNR {p:.2f} dB, rel-L2 {r:.2e}")
+    assert p >= 40.0, (p, r)
+
+
 @pytest.mark.parametrize("chunk", [1, 2, 3])
 def test_vae_chunked_decode_equals_whole_clip(chunk):
     """Long-clip decode (config 5) in chunks of latent frames with the causal cache carried between
