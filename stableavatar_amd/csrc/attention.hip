@@ -1175,6 +1175,256 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
   }
 }
 
+// ---- v13: the v6t block (V^T in P's order) as a two-phase ping-pong between the two waves of each SIMD.  In v6/v6t
+// the 8 waves pass one barrier per block together, so the two waves of a SIMD run QK^T, softmax and PV in step and
+// the matrix pipe idles through both softmaxes (at 3 140 cycles per block per SIMD against 2 176 of MFMA work,
+// the idle time is about both waves' softmax).  Here every block has two barrier-separated phases, and the wave
+// groups A (waves 0-3) and B (4-7, each SIMD's partners) alternate roles:
+//   phase X_j:  A  softmax of block j (rescale test, exponentials, P in bf16)  |  B  PV of block j-1, QK^T of block j
+//   phase Y_j:  A  PV of block j, QK^T of block j+1                           |  B  softmax of block j
+// so on each SIMD one wave's MFMAs (68 per phase) run beside the other's exponentials.  K_j is read by A in Y_{j-1}
+// and by B in X_j, V_j by A in Y_j and by B in X_{j+1}: after barrier Y_j the slots of K_j and V_{j-1} are free and
+// take the DMA of K_{j+2} and V_{j+1} (same 2-stage 64 KB ring), whose first reader (A, Y_{j+1}) comes one block
+// later -- each wave waits for its own pieces before barrier Y_{j+1}.  Same per-wave arithmetic and order as v6t:
+// bit-identical output.
+template <int VOFF>
+__device__ __forceinline__ void v13_pv(V6State& st, const bf16x8 (&pb)[2][2], const uint32_t* vb) {
+  u32x4 v0[4], v1[4];
+  v6t_read_v<VOFF, 0, 0>(v0, vb);
+  v6t_read_v<VOFF, 0, 4>(v1, vb);
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    st.L[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[c][0], st.L[0], 0, 0, 0);
+    st.L[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[c][1], st.L[1], 0, 0, 0);
+    if (c == 0) {
+      wait_k4<4>(v0);
+      v6t_mma_v(st.O, 0, v0, pb[0]);
+      v6t_read_v<VOFF, 1, 0>(v0, vb);
+      wait_k4<4>(v1);
+      v6t_mma_v(st.O, 4, v1, pb[0]);
+      v6t_read_v<VOFF, 1, 4>(v1, vb);
+    } else {
+      wait_k4<4>(v0);
+      v6t_mma_v(st.O, 0, v0, pb[1]);
+      wait_k4<0>(v1);
+      v6t_mma_v(st.O, 4, v1, pb[1]);
+    }
+  }
+}
+
+template <bool FIRST>
+__device__ __forceinline__ void v13_softmax(V6State& st, f32x4 (&S)[4][2], bf16x8 (&pb)[2][2], int kb, int kv_len,
+                                            int g) {
+  v6_tail_mask(S, kb, kv_len, g);
+  v6_softmax_rescale<FIRST>(S, st.L, st.negm, st.negm4, [&](const float (&al)[2]) {
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st.O[dt][qt][i] *= al[qt];
+  });
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[c][qt][j] = f2bf(S[2 * c][qt][j]);
+        pb[c][qt][4 + j] = f2bf(S[2 * c + 1][qt][j]);
+      }
+}
+
+// a phase boundary: the workgroup barrier without __syncthreads()'s release fence (which waits vmcnt(0), i.e. for
+// the K/V DMA issued half a block earlier), MFMAs kept on their side of it
+__device__ __forceinline__ void v13_sync() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS reads of the slots restaged after it
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ void attn_fwd_pp_body(const AttnArgs& a) {
+  constexpr int NW = 8, QBW = NW * 32, PPW = 16 / NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nx = gridDim.x, ny = gridDim.y;
+  const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
+  const int qb = flat % nx, h = (flat / nx) % ny, seg = flat / (nx * ny);
+  const int* sg = a.segs + seg * 4;
+  const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
+  if (qb * QBW >= q_len) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (kv_len <= 0) {
+    if (!a.accumulate)
+      for (int i = tid; i < QBW * (D / 8); i += NW * 64) {
+        const int qi = qb * QBW + i / (D / 8);
+        if (qi < q_len) {
+          const int orow = a.orows ? a.orows[q_row0 + qi] : q_row0 + qi;
+          *(u32x4*)(a.o + (long)orow * a.os + h * D + (i % (D / 8)) * 8) = (u32x4){0u, 0u, 0u, 0u};
+        }
+      }
+    return;
+  }
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool grpB = wave >= 4;  // waves w and w + 4 share a SIMD
+  const int g = lane >> 4, r16 = lane & 15;
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qc = min(qb * QBW + wave * 32 + qt * 16 + r16, q_len - 1);
+    const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * g;
+#pragma unroll
+    for (int dc = 0; dc < 4; ++dc) {
+      qf[qt][dc] = *(const bf16x8*)(qp + 32 * dc);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[qt][dc][j] = f2bf(bf2f(qf[qt][dc][j]) * a.c);
+    }
+  }
+  const int nkb = (kv_len + KVB - 1) / KVB;
+  const long tail0 = (long)(nkb - 1) * KVB;
+  const bool ragged = kv_len % KVB != 0;
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.k + (long)kv_row0 * a.ks + h * D), (short)0, (int)(((long)kv_len - 1) * a.ks * 2 + 256), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rkt = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.k + (kv_row0 + tail0) * a.ks + h * D), (short)0, (int)((kv_len - tail0 - 1) * a.ks * 2 + 256),
+      0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.v + (long)h * D * a.vs + kv_row0), (short)0, (int)(((long)(D - 1) * a.vs + (long)nkb * KVB) * 2),
+      0x00020000);
+  int koff[PPW], voff[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int srow = (wave * PPW + i) * 4 + (lane >> 4);
+    koff[i] = srow * (int)a.ks * 2 + ((r16 ^ (srow & 15)) << 4);
+    const int d = (wave * PPW + i) * 8 + (lane >> 3);
+    voff[i] = d * (int)a.vs * 2 + (((lane & 7) ^ (d & 7)) << 4);
+  }
+  const uint32_t lds_dma = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + wave * PPW * 1024);
+  // K_j in K slot j % 2 (stage offset 0 / STAGE_BYTES), V_j in V slot j % 2 (+TILE_BYTES)
+  auto stage_k = [&](int kb, int slot) {
+    const bool tail = ragged && kb == nkb - 1;
+    const int ks_off = tail ? 0 : kb * KVB * (int)a.ks * 2;
+    const __amdgpu_buffer_rsrc_t bk = tail ? rkt : rk;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(bk, LDS_PTR((uintptr_t)(lds_dma + slot * STAGE_BYTES + i * 1024)), 16,
+                                               koff[i], ks_off, 0, 0);
+  };
+  auto stage_v = [&](int kb, int slot) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rv, LDS_PTR((uintptr_t)(lds_dma + slot * STAGE_BYTES + TILE_BYTES + i * 1024)), 16, voff[i], kb * KVB * 2, 0,
+          0);
+  };
+  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
+  uint32_t ka[4], vb[2];
+#pragma unroll
+  for (int dc = 0; dc < 4; ++dc) ka[dc] = lds0 + r16 * 256 + (((dc * 4 + g) ^ r16) << 4);
+#pragma unroll
+  for (int c = 0; c < 2; ++c) vb[c] = lds0 + r16 * 128 + (((4 * c + g) ^ (r16 & 7)) << 4);
+
+  V6State st;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) st.O[dt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  st.L[0] = st.L[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  st.negm[0] = st.negm[1] = 0.f;
+  st.negm4[0] = st.negm4[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 S[4][2];
+  bf16x8 pb[2][2];
+
+  stage_k(0, 0);
+  stage_v(0, 0);
+  if (1 < nkb) stage_k(1, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // the two groups run separate loops (the same barriers, in the same number): with one loop and a branch per phase
+  // the compiler keeps both S and P live everywhere and spills
+  auto stage_y = [&](int j, auto parc) {  // after barrier Y_j: K_{j+2} into K_j's slot, V_{j+1} into V_{j-1}'s
+    constexpr int P = decltype(parc)::value;
+    if (j + 2 < nkb) stage_k(j + 2, P);
+    if (j + 1 < nkb) stage_v(j + 1, P ^ 1);
+  };
+  if (!grpB) {
+    v6_qk<0>(S, st.negm4, qf, ka);  // QK^T of block 0 (B's comes in X_0)
+    auto blockA = [&](auto parc, int j) {
+      constexpr int P = decltype(parc)::value;
+      constexpr int KN = (P ^ 1) * STAGE_BYTES, VO = P * STAGE_BYTES + TILE_BYTES;
+      v13_sync();  // X_j
+      if (j == 0) v13_softmax<true>(st, S, pb, j, kv_len, g);
+      else v13_softmax<false>(st, S, pb, j, kv_len, g);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of K_{j+1}, V_j
+      v13_sync();  // Y_j
+      stage_y(j, parc);
+      v13_pv<VO>(st, pb, vb);  // V_j
+      __builtin_amdgcn_sched_barrier(0);
+      if (j + 1 < nkb) v6_qk<KN>(S, st.negm4, qf, ka);  // K_{j+1}
+    };
+    for (int j = 0; j < nkb; j += 2) {
+      blockA(std::integral_constant<int, 0>{}, j);
+      if (j + 1 >= nkb) break;
+      blockA(std::integral_constant<int, 1>{}, j + 1);
+    }
+  } else {
+    __builtin_amdgcn_s_setprio(1);
+    auto blockB = [&](auto parc, int j) {
+      constexpr int P = decltype(parc)::value;
+      constexpr int KO = P * STAGE_BYTES, VP = (P ^ 1) * STAGE_BYTES + TILE_BYTES;
+      v13_sync();  // X_j
+      if (j > 0) v13_pv<VP>(st, pb, vb);  // V_{j-1}
+      __builtin_amdgcn_sched_barrier(0);
+      v6_qk<KO>(S, st.negm4, qf, ka);  // K_j
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      v13_sync();  // Y_j
+      stage_y(j, parc);
+      if (j == 0) v13_softmax<true>(st, S, pb, j, kv_len, g);
+      else v13_softmax<false>(st, S, pb, j, kv_len, g);
+    };
+    for (int j = 0; j < nkb; j += 2) {
+      blockB(std::integral_constant<int, 0>{}, j);
+      if (j + 1 >= nkb) break;
+      blockB(std::integral_constant<int, 1>{}, j + 1);
+    }
+    // PV of the last block (its V slot is not restaged)
+    if ((nkb - 1) % 2 == 0) v13_pv<TILE_BYTES>(st, pb, vb);
+    else v13_pv<STAGE_BYTES + TILE_BYTES>(st, pb, vb);
+  }
+
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const float inv = 1.0f / st.L[qt][0];
+    const int qi = qb * QBW + wave * 32 + qt * 16 + r16;
+    const int qrow = q_row0 + min(qi, q_len - 1);
+    const int orow = a.orows ? a.orows[qrow] : qrow;
+    bf16* op = a.o + (long)orow * a.os + h * D + 4 * (g & ~1) + 16 * (g & 1);
+#pragma unroll
+    for (int dt = 0; dt < 8; dt += 2) {
+      const f32x4& A = st.O[dt][qt];
+      const f32x4& B = st.O[dt + 1][qt];
+      const bf16x4 pa = {f2bf(A[0] * inv), f2bf(A[1] * inv), f2bf(A[2] * inv), f2bf(A[3] * inv)};
+      const bf16x4 pc = {f2bf(B[0] * inv), f2bf(B[1] * inv), f2bf(B[2] * inv), f2bf(B[3] * inv)};
+      const u32x2 ga = __builtin_bit_cast(u32x2, pa), gc = __builtin_bit_cast(u32x2, pc);
+      const auto rx = __builtin_amdgcn_permlane16_swap(ga[0], gc[0], false, false);
+      const auto ry = __builtin_amdgcn_permlane16_swap(ga[1], gc[1], false, false);
+      u32x4 out = {rx[0], ry[0], rx[1], ry[1]};
+      bf16* p = op + dt * 16;
+      if (a.accumulate) {
+        const bf16x8 ov = *(const bf16x8*)p;
+        bf16x8 nv = __builtin_bit_cast(bf16x8, out);
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) nv[jj] = f2bf(bf2f(ov[jj]) + bf2f(nv[jj]));
+        out = __builtin_bit_cast(u32x4, nv);
+      }
+      if (qi < q_len) *(u32x4*)p = out;
+    }
+  }
+}
+
 // the fused cross-attention on the self-attention block body: 8 waves x 32 queries of one query block,
 // the text, image and per-frame vocal K/V streams one after the other through 3-stage K / V regions (each
 // block's DMA two blocks ahead), a separate online softmax per source (its first block sets the max), the
@@ -1399,6 +1649,7 @@ __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) { attn_fwd
 __global__ __launch_bounds__(256, 2) void attn_fwd_v6_w4_kernel(AttnArgs a) { attn_fwd_v6_body<4>(a); }
 __global__ __launch_bounds__(512) void attn_fwd_v6t_kernel(AttnArgs a) { attn_fwd_vt_body<1>(a); }
 __global__ __launch_bounds__(512) void attn_fwd_v12_kernel(AttnArgs a) { attn_fwd_vt_body<2>(a); }
+__global__ __launch_bounds__(512) void attn_fwd_v13_kernel(AttnArgs a) { attn_fwd_pp_body(a); }
 
 }  // namespace
 
@@ -1418,7 +1669,7 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
   if (head_dim != D) return SA_ERR_ARG;
   if ((q_stride | k_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
   if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)o)) & 15) return SA_ERR_ARG;
-  if (kernel < 0 || kernel > 4) return SA_ERR_ARG;
+  if (kernel < 0 || kernel > 5) return SA_ERR_ARG;
   if (kernel >= 3 && (v_stride % 64 || (((uintptr_t)v) & 127))) return SA_ERR_ARG;  // V^T rows: whole 64-key blocks
   static const bool attr = [] {  // one-time, thread-safe
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
@@ -1426,6 +1677,7 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
                               LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6t_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v12_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_v13_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     return true;
   }();
   (void)attr;
@@ -1447,12 +1699,14 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
   if (kernel == 2) {
     dim3 grid((max_q_len + 127) / 128, heads, nseg);
     hipLaunchKernelGGL(attn_fwd_v6_w4_kernel, grid, dim3(256), LDS_BYTES, (hipStream_t)stream, a);
-  } else if (kernel == 3 || kernel == 4) {  // v = V^T [heads * 128][v_stride] (attn_fwd_vt_body)
+  } else if (kernel >= 3) {  // v = V^T [heads * 128][v_stride] (attn_fwd_vt_body / attn_fwd_pp_body)
     dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
     if (kernel == 3)
       hipLaunchKernelGGL(attn_fwd_v6t_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
-    else
+    else if (kernel == 4)
       hipLaunchKernelGGL(attn_fwd_v12_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(attn_fwd_v13_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
   } else {
     dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
     hipLaunchKernelGGL(attn_fwd_v6_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);

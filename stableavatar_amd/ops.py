@@ -38,6 +38,8 @@ def _check(t, dtype, name):
 GEMM_AUTO, GEMM_PINGPONG, GEMM_PERSISTENT, GEMM_PERSISTENT192 = 0, 1, 2, 3
 # the persistent kernel on the three-barrier (s9) K schedule: tile rows by auto / 256 / 192
 GEMM_S9_AUTO, GEMM_S9, GEMM_S9_192 = 5, 6, 7
+# the persistent kernel with each tile's epilogue deferred under the next tile's K loop (192-row tiles, K = 1536)
+GEMM_S10 = 10
 
 
 def linear(x, weight, bias=None, epilogue=EPI_BF16, out=None, residual=None, gate=None, rows_per_batch=0,

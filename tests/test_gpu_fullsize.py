@@ -142,11 +142,13 @@ def test_dit_gemm_fullsize(name, N, K, epi):
     # output in the same K order: bit-identical, here at M = 64 512, at the N = 8 per-rank M = 8 064, and at M
     # with a partial last tile of either height (12 285 = the per-rank M at 480x832, N = 8; 1 000)
     # and the three-barrier K schedule (GEMM_S9*, auto's default) computes the same products in the same order
+    # and the deferred-epilogue kernel (GEMM_S10: 192-row tiles, each tile's epilogue retired under the next tile's
+    # K loop from a bf16 stash of the Linear output) rounds and sums identically (K = 1536 shapes)
+    kerns = [ops.GEMM_PERSISTENT192, ops.GEMM_S9, ops.GEMM_S9_192] + ([ops.GEMM_S10] if K == 1536 else [])
     for Mx in (M, 3 * 2688, 3 * 4095, 1000):
         y2 = torch.empty(Mx, N, device=dev, dtype=y.dtype)
-        outs = [torch.empty_like(y2) for _ in range(3)]
-        for yy, kern in ((y2, ops.GEMM_PERSISTENT), (outs[0], ops.GEMM_PERSISTENT192), (outs[1], ops.GEMM_S9),
-                         (outs[2], ops.GEMM_S9_192)):
+        outs = [torch.empty_like(y2) for _ in kerns]
+        for yy, kern in [(y2, ops.GEMM_PERSISTENT)] + list(zip(outs, kerns)):
             if epi == "bf16":
                 ops.linear(x[:Mx], w, b, ops.EPI_BF16, out=yy, kernel=kern)
             elif epi == "gelu":
@@ -156,7 +158,7 @@ def test_dit_gemm_fullsize(name, N, K, epi):
                 ops.linear(x[:Mx], w, b, ops.EPI_RES_F32, out=yy, residual=yy, gate=gate, rows_per_batch=L, kernel=kern)
         torch.cuda.synchronize()
         for i, y3 in enumerate(outs):
-            assert torch.equal(y2, y3), (name, Mx, i)
+            assert torch.equal(y2, y3), (name, Mx, kerns[i])
 
 
 @pytest.mark.timeout(600)
