@@ -40,6 +40,8 @@ constexpr int KVB = 64;
 constexpr int TILE_BYTES = KVB * D * 2;      // 16 KB
 constexpr int STAGE_BYTES = 2 * TILE_BYTES;  // K + V
 constexpr int LDS_BYTES = 2 * STAGE_BYTES;   // 64 KB
+constexpr int V13_LDS = 3 * STAGE_BYTES;     // 96 KB: the ping-pong kernel's 3-stage ring
+constexpr int V13_VBASE = 3 * TILE_BYTES;    // its V region
 
 // 16-byte chunk swizzle for 256-B rows: conflict-free for both row (ds_read_b128) and
 // transposed (ds_read_b64_tr_b16) reads (cdna_hip_programming.md T10 form (b))
@@ -1182,37 +1184,62 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
 // groups A (waves 0-3) and B (4-7, each SIMD's partners) alternate roles:
 //   phase X_j:  A  softmax of block j (rescale test, exponentials, P in bf16)  |  B  PV of block j-1, QK^T of block j
 //   phase Y_j:  A  PV of block j, QK^T of block j+1                           |  B  softmax of block j
-// so on each SIMD one wave's MFMAs (68 per phase) run beside the other's exponentials.  K_j is read by A in Y_{j-1}
-// and by B in X_j, V_j by A in Y_j and by B in X_{j+1}: after barrier Y_j the slots of K_j and V_{j-1} are free and
-// take the DMA of K_{j+2} and V_{j+1} (same 2-stage 64 KB ring), whose first reader (A, Y_{j+1}) comes one block
-// later -- each wave waits for its own pieces before barrier Y_{j+1}.  Same per-wave arithmetic and order as v6t:
-// bit-identical output.
+// so on each SIMD one wave's MFMAs (68 per phase) run beside the other's exponentials.  The MFMA phase has one
+// wave per SIMD issuing, so its LDS operand latency is not covered by a partner: the softmax phase ends by reading
+// the first three operand sets of the wave's next MFMA phase (V13Frags), and the K / V ring has three stages so that
+// K_{j+1} and V_j are visible from barrier X_j on.  K_j and V_j sit in slot j % 3; after barrier Y_j every reader of
+// K_j and V_{j-1} is done, and their slots take the DMA of K_{j+3} and V_{j+2}, which each wave waits for (counted
+// vmcnt: the pieces issued after Y_{j+1} stay in flight) before barrier X_{j+2}.  Same per-wave arithmetic and order
+// as v6t: bit-identical output.
+// v13's operand fragments: three 16-register sets carry, in order, V chunk 0 d 0-63 / 64-127, V chunk 1 d 0-63 /
+// 64-127 of block j and K tiles 0-3 of block j + 1.  The first three are read at the end of the wave's softmax phase
+// (their data landed a phase earlier, 3-stage ring), so its MFMA phase opens with operands in registers; every later
+// set is read two sets (16 MFMAs) ahead of its use.
+struct V13Frags {
+  u32x4 f0[4], f1[4], f2[4];
+};
 template <int VOFF>
-__device__ __forceinline__ void v13_pv(V6State& st, const bf16x8 (&pb)[2][2], const uint32_t* vb) {
-  u32x4 v0[4], v1[4];
-  v6t_read_v<VOFF, 0, 0>(v0, vb);
-  v6t_read_v<VOFF, 0, 4>(v1, vb);
+__device__ __forceinline__ void v13_prefetch(V13Frags& fr, const uint32_t* vb) {
+  v6t_read_v<VOFF, 0, 0>(fr.f0, vb);
+  v6t_read_v<VOFF, 0, 4>(fr.f1, vb);
+  v6t_read_v<VOFF, 1, 0>(fr.f2, vb);
+}
+// the MFMA phase: PV of the softmaxed block j (V stage VOFF), then QK^T of block j + 1 (K stage KOFF; after the last
+// block a QK^T of a stale slot whose S is never used).  Same MFMA order per accumulator as v6t: bit-identical.
+template <int VOFF, int KOFF>
+__device__ __forceinline__ void v13_mfma_phase(V6State& st, const bf16x8 (&pb)[2][2], const uint32_t* vb,
+                                               f32x4 (&S)[4][2], const bf16x8 (&qf)[2][4], const uint32_t* ka,
+                                               V13Frags& fr) {
   bf16x8 ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+  st.L[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[0][0], st.L[0], 0, 0, 0);
+  st.L[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[0][1], st.L[1], 0, 0, 0);
+  wait_k4<0>(fr.f0);  // (landed before the phase's barrier)
+  v6t_mma_v(st.O, 0, fr.f0, pb[0]);
+  v6t_read_v<VOFF, 1, 4>(fr.f0, vb);  // V chunk 1, d 64-127
+  v6t_mma_v(st.O, 4, fr.f1, pb[0]);
+  v6_read_k<KOFF, 0>(fr.f1, ka);
+  st.L[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[1][0], st.L[0], 0, 0, 0);
+  st.L[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[1][1], st.L[1], 0, 0, 0);
+  v6t_mma_v(st.O, 0, fr.f2, pb[1]);
+  v6_read_k<KOFF, 1>(fr.f2, ka);
+  wait_k4<8>(fr.f0);
+  v6t_mma_v(st.O, 4, fr.f0, pb[1]);
+  v6_read_k<KOFF, 2>(fr.f0, ka);
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    st.L[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[c][0], st.L[0], 0, 0, 0);
-    st.L[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[c][1], st.L[1], 0, 0, 0);
-    if (c == 0) {
-      wait_k4<4>(v0);
-      v6t_mma_v(st.O, 0, v0, pb[0]);
-      v6t_read_v<VOFF, 1, 0>(v0, vb);
-      wait_k4<4>(v1);
-      v6t_mma_v(st.O, 4, v1, pb[0]);
-      v6t_read_v<VOFF, 1, 4>(v1, vb);
-    } else {
-      wait_k4<4>(v0);
-      v6t_mma_v(st.O, 0, v0, pb[1]);
-      wait_k4<0>(v1);
-      v6t_mma_v(st.O, 4, v1, pb[1]);
-    }
-  }
+  for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) S[kt][qt] = st.negm4[qt];
+  wait_k4<8>(fr.f1);
+  v6_mma_k(S, 0, fr.f1, qf);
+  v6_read_k<KOFF, 3>(fr.f1, ka);
+  wait_k4<8>(fr.f2);
+  v6_mma_k(S, 1, fr.f2, qf);
+  wait_k4<4>(fr.f0);
+  v6_mma_k(S, 2, fr.f0, qf);
+  wait_k4<0>(fr.f1);
+  v6_mma_k(S, 3, fr.f1, qf);
 }
 
 template <bool FIRST>
@@ -1247,8 +1274,24 @@ __device__ __forceinline__ void v13_sync() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+#ifdef SA_V13_STAMPS
+// measurement builds only (scripts/build_variant.sh ... -DSA_V13_STAMPS): per group (A, B) the summed s_memtime
+// cycles of the body's four parts (barrier 1, work 1, barrier 2, MFMA phase) over every wave of the launch
+__device__ unsigned long long g_v13_stamps[12];
+__device__ __forceinline__ uint64_t v13_now() {
+  const uint64_t t = __builtin_amdgcn_s_memtime();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  return t;
+}
+#define V13_STAMP(x) const uint64_t x = v13_now()
+#define V13_ACC(k, v) acc[k] += (v)
+#else
+#define V13_STAMP(x)
+#define V13_ACC(k, v)
+#endif
+
 __device__ __forceinline__ void attn_fwd_pp_body(const AttnArgs& a) {
-  constexpr int NW = 8, QBW = NW * 32, PPW = 16 / NW;
+  constexpr int NW = 8, QBW = NW * 32, PPA = 4;  // the K / V DMA is issued by group A only: 4 pieces per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nx = gridDim.x, ny = gridDim.y;
   const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
@@ -1294,38 +1337,47 @@ __device__ __forceinline__ void attn_fwd_pp_body(const AttnArgs& a) {
   const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.v + (long)h * D * a.vs + kv_row0), (short)0, (int)(((long)(D - 1) * a.vs + (long)nkb * KVB) * 2),
       0x00020000);
-  int koff[PPW], voff[PPW];
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    const int srow = (wave * PPW + i) * 4 + (lane >> 4);
-    koff[i] = srow * (int)a.ks * 2 + ((r16 ^ (srow & 15)) << 4);
-    const int d = (wave * PPW + i) * 8 + (lane >> 3);
-    voff[i] = d * (int)a.vs * 2 + (((lane & 7) ^ (d & 7)) << 4);
-  }
-  const uint32_t lds_dma = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + wave * PPW * 1024);
-  // K_j in K slot j % 2 (stage offset 0 / STAGE_BYTES), V_j in V slot j % 2 (+TILE_BYTES)
+  const uint32_t lds_dma = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + (wave & 3) * PPA * 1024);
+  // the per-lane DMA offsets are recomputed at every staging from the lane id (v_mbcnt), not kept across the loop:
+  // kept, hipcc spills them at this register pressure, and each reload's vmcnt(0) would wait for every DMA piece in
+  // flight (serialising the ring)
+  const int ks2 = (int)a.ks * 2, vs2 = (int)a.vs * 2;
+  auto lane_id = [] {  // volatile: not hoisted out of the loop
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+  };
+  // 3-stage ring (V13_LDS): K_j at slot * TILE_BYTES, V_j at V13_VBASE + slot * TILE_BYTES (K and V regions apart,
+  // so every ds_read offset from its region's read base stays below 64 KB)
   auto stage_k = [&](int kb, int slot) {
     const bool tail = ragged && kb == nkb - 1;
-    const int ks_off = tail ? 0 : kb * KVB * (int)a.ks * 2;
+    const int ks_off = tail ? 0 : kb * KVB * ks2;
     const __amdgpu_buffer_rsrc_t bk = tail ? rkt : rk;
+    const int ln = lane_id();
 #pragma unroll
-    for (int i = 0; i < PPW; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(bk, LDS_PTR((uintptr_t)(lds_dma + slot * STAGE_BYTES + i * 1024)), 16,
-                                               koff[i], ks_off, 0, 0);
+    for (int i = 0; i < PPA; ++i) {
+      const int srow = ((wave & 3) * PPA + i) * 4 + (ln >> 4);
+      const int koff = srow * ks2 + (((ln & 15) ^ (srow & 15)) << 4);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(bk, LDS_PTR((uintptr_t)(lds_dma + slot * TILE_BYTES + i * 1024)), 16,
+                                               koff, ks_off, 0, 0);
+    }
   };
   auto stage_v = [&](int kb, int slot) {
+    const int ln = lane_id();
 #pragma unroll
-    for (int i = 0; i < PPW; ++i)
+    for (int i = 0; i < PPA; ++i) {
+      const int d = ((wave & 3) * PPA + i) * 8 + (ln >> 3);
+      const int voff = d * vs2 + (((ln & 7) ^ (d & 7)) << 4);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rv, LDS_PTR((uintptr_t)(lds_dma + slot * STAGE_BYTES + TILE_BYTES + i * 1024)), 16, voff[i], kb * KVB * 2, 0,
-          0);
+          rv, LDS_PTR((uintptr_t)(lds_dma + V13_VBASE + slot * TILE_BYTES + i * 1024)), 16, voff, kb * KVB * 2, 0, 0);
+    }
   };
   const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
   uint32_t ka[4], vb[2];
 #pragma unroll
   for (int dc = 0; dc < 4; ++dc) ka[dc] = lds0 + r16 * 256 + (((dc * 4 + g) ^ r16) << 4);
 #pragma unroll
-  for (int c = 0; c < 2; ++c) vb[c] = lds0 + r16 * 128 + (((4 * c + g) ^ (r16 & 7)) << 4);
+  for (int c = 0; c < 2; ++c) vb[c] = lds0 + V13_VBASE + r16 * 128 + (((4 * c + g) ^ (r16 & 7)) << 4);
 
   V6State st;
 #pragma unroll
@@ -1338,62 +1390,107 @@ __device__ __forceinline__ void attn_fwd_pp_body(const AttnArgs& a) {
   f32x4 S[4][2];
   bf16x8 pb[2][2];
 
-  stage_k(0, 0);
-  stage_v(0, 0);
-  if (1 < nkb) stage_k(1, 1);
+  V13Frags fr;
+  // ring prologue: K_0, K_1, K_2, V_0 (K_j, V_j in slot j % 3)
+  if (!grpB) {
+    stage_k(0, 0);
+    stage_v(0, 0);
+    if (1 < nkb) stage_k(1, 1);
+  } else {
+    if (2 < nkb) stage_k(2, 2);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  // the two groups run separate loops (the same barriers, in the same number): with one loop and a branch per phase
-  // the compiler keeps both S and P live everywhere and spills
-  auto stage_y = [&](int j, auto parc) {  // after barrier Y_j: K_{j+2} into K_j's slot, V_{j+1} into V_{j-1}'s
-    constexpr int P = decltype(parc)::value;
-    if (j + 2 < nkb) stage_k(j + 2, P);
-    if (j + 1 < nkb) stage_v(j + 1, P ^ 1);
+  // Both groups run the same cyclic body [softmax_j + operand prefetch, PV_j + QK_{j+1}], group B one phase later:
+  // A's body opens with barrier X_j, B's with Y_j (B's QK_0 precedes it in phase X_0), so each SIMD pairs one wave's
+  // softmax with the other's MFMAs.  The K / V DMA rides in the softmax phases, after the softmax (that wave then
+  // waits at the barrier for its partner's MFMAs anyway; issued at the top of an MFMA phase by all eight waves the
+  // 32 pieces held each wave ~700 cycles): A issues V_{j+1} in X_j (into V_{j-2}'s slot, whose readers are done by
+  // X_j), landed before X_{j+1}, where A starts reading it; B issues K_{j+3} in Y_j (into K_j's slot, done by Y_j),
+  // landed before Y_{j+2}, ahead of its first reader (A's QK^T in Y_{j+2}).  4 pieces per wave per block each.
+  // Block 0 is peeled (its softmax sets the running max), so the loop bodies carry no first-block branch.
+#ifdef SA_V13_STAMPS
+  uint64_t acc[6] = {0, 0, 0, 0, 0, 0};
+#endif
+  auto body = [&](auto firstc, auto slotc, auto grpc, int j) {
+    constexpr bool FIRST = decltype(firstc)::value, GB = decltype(grpc)::value;
+    constexpr int SL = decltype(slotc)::value;
+    constexpr int KN = ((SL + 1) % 3) * TILE_BYTES, VO = SL * TILE_BYTES;
+    if constexpr (!GB) {
+      V13_STAMP(tw);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of V_j (issued in X_{j-1})
+      V13_STAMP(t0);
+      V13_ACC(4, t0 - tw);
+      v13_sync();  // X_j
+      V13_STAMP(t1);
+      v13_softmax<FIRST>(st, S, pb, j, kv_len, g);
+      v13_prefetch<VO>(fr, vb);
+      V13_STAMP(t2s);
+      if (j + 1 < nkb) stage_v(j + 1, (SL + 1) % 3);
+      V13_STAMP(t2);
+      V13_ACC(5, t2 - t2s);
+      v13_sync();  // Y_j
+      V13_STAMP(t3);
+      V13_ACC(0, t1 - t0); V13_ACC(1, t2 - t1); V13_ACC(2, t3 - t2);
+    } else {
+      // this wave's pieces of K_{j+1} (issued in Y_{j-2}) landed; those of K_{j+2} (Y_{j-1}) may fly
+      V13_STAMP(tw);
+      if (j + 2 < nkb)
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      V13_STAMP(t0);
+      V13_ACC(4, t0 - tw);
+      v13_sync();  // Y_j
+      V13_STAMP(t1);
+      v13_softmax<FIRST>(st, S, pb, j, kv_len, g);
+      v13_prefetch<VO>(fr, vb);
+      if (j + 3 < nkb) stage_k(j + 3, SL);
+      V13_STAMP(t2);
+      if (j + 1 < nkb) v13_sync();  // X_{j+1}
+      V13_STAMP(t3);
+      V13_ACC(0, t1 - t0); V13_ACC(1, t2 - t1); V13_ACC(2, t3 - t2);
+    }
+    // V_j, K_{j+1} (after the last block a QK^T of a stale slot, unused: no branch in the body)
+#ifdef SA_V13_STAMPS
+    const uint64_t t4 = v13_now();
+#endif
+    // the MFMA phase's wave first at the issue arbiter, the softmax wave in its gaps (6.31 / 6.29 vs 6.41 / 6.44 ms
+    // with B's static priority alone, profiles/r05/attn_ab_v13_variants_r5u_r5v.jsonl)
+    __builtin_amdgcn_s_setprio(2);
+    v13_mfma_phase<VO, KN>(st, pb, vb, S, qf, ka, fr);
+    __builtin_amdgcn_s_setprio(GB ? 1 : 0);
+#ifdef SA_V13_STAMPS
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    acc[3] += v13_now() - t4;
+#endif
+  };
+  const auto S0 = std::integral_constant<int, 0>{};
+  const auto S1 = std::integral_constant<int, 1>{};
+  const auto S2 = std::integral_constant<int, 2>{};
+  auto run = [&](auto grpc) {
+    body(std::true_type{}, S0, grpc, 0);
+    for (int j = 1; j < nkb; j += 3) {
+      body(std::false_type{}, S1, grpc, j);
+      if (j + 1 >= nkb) break;
+      body(std::false_type{}, S2, grpc, j + 1);
+      if (j + 2 >= nkb) break;
+      body(std::false_type{}, S0, grpc, j + 2);
+    }
   };
   if (!grpB) {
-    v6_qk<0>(S, st.negm4, qf, ka);  // QK^T of block 0 (B's comes in X_0)
-    auto blockA = [&](auto parc, int j) {
-      constexpr int P = decltype(parc)::value;
-      constexpr int KN = (P ^ 1) * STAGE_BYTES, VO = P * STAGE_BYTES + TILE_BYTES;
-      v13_sync();  // X_j
-      if (j == 0) v13_softmax<true>(st, S, pb, j, kv_len, g);
-      else v13_softmax<false>(st, S, pb, j, kv_len, g);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of K_{j+1}, V_j
-      v13_sync();  // Y_j
-      stage_y(j, parc);
-      v13_pv<VO>(st, pb, vb);  // V_j
-      __builtin_amdgcn_sched_barrier(0);
-      if (j + 1 < nkb) v6_qk<KN>(S, st.negm4, qf, ka);  // K_{j+1}
-    };
-    for (int j = 0; j < nkb; j += 2) {
-      blockA(std::integral_constant<int, 0>{}, j);
-      if (j + 1 >= nkb) break;
-      blockA(std::integral_constant<int, 1>{}, j + 1);
-    }
+    v6_qk<0>(S, st.negm4, qf, ka);  // QK^T of block 0 before X_0
+    run(std::false_type{});
   } else {
     __builtin_amdgcn_s_setprio(1);
-    auto blockB = [&](auto parc, int j) {
-      constexpr int P = decltype(parc)::value;
-      constexpr int KO = P * STAGE_BYTES, VP = (P ^ 1) * STAGE_BYTES + TILE_BYTES;
-      v13_sync();  // X_j
-      if (j > 0) v13_pv<VP>(st, pb, vb);  // V_{j-1}
-      __builtin_amdgcn_sched_barrier(0);
-      v6_qk<KO>(S, st.negm4, qf, ka);  // K_j
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      v13_sync();  // Y_j
-      stage_y(j, parc);
-      if (j == 0) v13_softmax<true>(st, S, pb, j, kv_len, g);
-      else v13_softmax<false>(st, S, pb, j, kv_len, g);
-    };
-    for (int j = 0; j < nkb; j += 2) {
-      blockB(std::integral_constant<int, 0>{}, j);
-      if (j + 1 >= nkb) break;
-      blockB(std::integral_constant<int, 1>{}, j + 1);
-    }
-    // PV of the last block (its V slot is not restaged)
-    if ((nkb - 1) % 2 == 0) v13_pv<TILE_BYTES>(st, pb, vb);
-    else v13_pv<STAGE_BYTES + TILE_BYTES>(st, pb, vb);
+    v13_sync();  // X_0
+    v6_qk<0>(S, st.negm4, qf, ka);
+    run(std::true_type{});
   }
+#ifdef SA_V13_STAMPS
+  if (lane == 0)
+    for (int k = 0; k < 6; ++k) atomicAdd(&g_v13_stamps[(grpB ? 6 : 0) + k], (unsigned long long)acc[k]);
+#endif
 
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
@@ -1677,7 +1774,7 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
                               LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6t_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v12_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_v13_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_v13_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, V13_LDS);
     return true;
   }();
   (void)attr;
@@ -1706,7 +1803,7 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
     else if (kernel == 4)
       hipLaunchKernelGGL(attn_fwd_v12_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
     else
-      hipLaunchKernelGGL(attn_fwd_v13_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+      hipLaunchKernelGGL(attn_fwd_v13_kernel, grid, dim3(512), V13_LDS, (hipStream_t)stream, a);
   } else {
     dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
     hipLaunchKernelGGL(attn_fwd_v6_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
@@ -1767,3 +1864,14 @@ extern "C" int sa_attn_cross3(const void* q, int64_t q_stride, const void* kt, c
   SA_LAUNCH_CHECK();
   return SA_OK;
 }
+
+#ifdef SA_V13_STAMPS
+extern "C" int sa_debug_v13_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_v13_stamps), sizeof(unsigned long long) * 12) != hipSuccess) return SA_ERR_ARG;
+  if (reset) {
+    const unsigned long long z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_v13_stamps), z, sizeof(z)) != hipSuccess) return SA_ERR_ARG;
+  }
+  return SA_OK;
+}
+#endif
