@@ -28,7 +28,8 @@ enum {
   SA_EPI_BF16_T = 6,        /* C^T(bf16): C[n * ldc + m] = A·W^T + bias (persistent kernel, K % 128 == 0,
                                M % 4 == 0, ldc >= M): the V^T operand of sa_attn_fwd_ex kernel 4 */
   SA_EPI_BF16_TP32 = 7      /* SA_EPI_BF16_T with row 32c + 4q + r at column 32c + 8(q & 3) + 4(q >> 2) + r
-                               (ldc >= M rounded up to 32): the V^T of sa_attn_fwd_ex kernel 3, the
+                               (ldc >= M rounded up to 32, ldc and strideC % 8 == 0, C 16-B aligned:
+                               16-byte stores): the V^T of sa_attn_fwd_ex kernel 3, the
                                DiT's self-attention (wan_fantasy_transformer3d_1B.py:376-379 v projection) */
 };
 

@@ -73,6 +73,23 @@ constexpr int LDS_BYTES = 2 * STAGE_BYTES;      // 128 KB
 // byte offset of 16-byte chunk c of row r in a [rows][64] bf16 tile (128-B rows)
 __device__ __forceinline__ int swz128(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 
+// Output store cache policy of the persistent kernels' epilogues (A/B builds: -DSA_STORE_POLICY=<aux>, the
+// buffer-store cache-policy bits, gfx950: 1 sc0, 2 nt, 16 sc1).  -1 (default): bf16 rows non-temporal, fp32 plain.
+// sc1 stores leave no copy in the XCD's L2 (MI355X_MICROARCH.md store table), so a tile's output burst does not
+// evict the K-slices the XCD's other tiles are still reading.
+#ifndef SA_STORE_POLICY
+#define SA_STORE_POLICY -1
+#endif
+template <class T>
+__device__ __forceinline__ void store16(T* base_uniform, long elem_off, u32x4 v) {
+  if constexpr (SA_STORE_POLICY < 0) {
+    *(u32x4*)(base_uniform + elem_off) = v;
+  } else {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base_uniform, (short)0, -1, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(elem_off * (long)sizeof(T)), 0, SA_STORE_POLICY);
+  }
+}
+
 // apply the epilogue to NC consecutive columns of one output row and store them
 template <int EPI, int NC, bool BIAS = true>
 __device__ __forceinline__ void epi_row(const GemmArgs& g, float* v, long bz, int grow, int gcol) {
@@ -120,7 +137,10 @@ __device__ __forceinline__ void epi_row(const GemmArgs& g, float* v, long bz, in
           // non-temporal 16-byte stores (global_store ... nt): the epilogue's store burst drains faster
           // (isolated: cross-Q 0.238 vs 0.286 ms, QKV 0.833 vs 0.873, FFN-up 1.535 vs 1.632; in the
           // 30-layer forward 0.4-0.8 % -- the consumers then read more of it from HBM; profiles/r03 r3n)
-          __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), (u32x4*)(C + 8 * h));
+          if constexpr (SA_STORE_POLICY < 0)
+            __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), (u32x4*)(C + 8 * h));
+          else
+            store16((bf16*)g.C + bz * g.sC, (long)grow * g.ldc + gcol + 8 * h, __builtin_bit_cast(u32x4, o));
         }
       } else {
 #pragma unroll
@@ -598,7 +618,7 @@ __device__ __forceinline__ void s7_f32_epilogue(const GemmArgs& g, f32x4 (&acc)[
         if constexpr (RES) t = rb[st % AH][e] + t * (TILE_GATE ? gj[j % 3][e] : gb[PER_ROW_GATE ? st % AH : 0][e]);
         v[e] = t;
       }
-      *(f32x4*)((float*)g.C + bz * g.sC + (long)(row0 + i * 16) * g.ldc + col + j * 16) = v;
+      store16((float*)g.C + bz * g.sC, (long)(row0 + i * 16) * g.ldc + col + j * 16, __builtin_bit_cast(u32x4, v));
       if constexpr (RES) {
         if (st + AH < 8 * MI) fetch(st + AH);
       }
@@ -626,14 +646,34 @@ __device__ __forceinline__ void s7_t_epilogue(const GemmArgs& g, f32x4 (&acc)[8]
     else
       asm volatile("" : "+a"(acc[0][j]), "+a"(acc[1][j]), "+a"(acc[2][j]), "+a"(acc[3][j]), "+a"(acc[4][j]),
                         "+a"(acc[5][j])::"memory");
+    if constexpr (P32) {
+      // P's order puts row 32c + 4 fc + r of the even block at position 32c + 8 fc + r and the same row of the odd
+      // block (+16) at 32c + 8 fc + 4 + r (the tile's rows start on a 32-row boundary: m0, 96 and 128 are multiples
+      // of 32): one lane's acc[2c][j] and acc[2c + 1][j] fill 8 consecutive positions, one 16-byte store (half the
+      // store instructions of the 8-byte form, same bytes)
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int m = row0 + i * 16;
-      const f32x4 v = acc[i][j];
-      const bf16x4 o = {f2bf(v[0] + b), f2bf(v[1] + b), f2bf(v[2] + b), f2bf(v[3] + b)};
-      const int q = (m >> 2) & 7;  // the 4-row group inside its 32-row chunk
-      const int mc = P32 ? (m & ~31) + 8 * (q & 3) + 4 * (q >> 2) : m;
-      if (n < g.N && m < g.M) *(bf16x4*)(C + (long)n * g.ldc + mc) = o;
+      for (int i = 0; i < MI; i += 2) {
+        const int m = row0 + i * 16;
+        const f32x4 v = acc[i][j], w = acc[i + 1][j];
+        const bf16x8 o = {f2bf(v[0] + b), f2bf(v[1] + b), f2bf(v[2] + b), f2bf(v[3] + b),
+                          f2bf(w[0] + b), f2bf(w[1] + b), f2bf(w[2] + b), f2bf(w[3] + b)};
+        bf16* p = C + (long)n * g.ldc + (m & ~31) + 8 * fc;
+        if (n < g.N) {
+          if (m + 16 < g.M) {
+            *(u32x4*)p = __builtin_bit_cast(u32x4, o);
+          } else if (m < g.M) {
+            *(bf16x4*)p = (bf16x4){o[0], o[1], o[2], o[3]};
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int m = row0 + i * 16;
+        const f32x4 v = acc[i][j];
+        const bf16x4 o = {f2bf(v[0] + b), f2bf(v[1] + b), f2bf(v[2] + b), f2bf(v[3] + b)};
+        if (n < g.N && m < g.M) *(bf16x4*)(C + (long)n * g.ldc + m) = o;
+      }
     }
   }
 }
@@ -1489,6 +1529,8 @@ int launch(const GemmArgs& g_in, int batch, int kernel, hipStream_t st) {
   if constexpr (TOUT) {  // the transposed store exists in the persistent kernel only
     if (!persistent_ok || kernel == KERNEL_PINGPONG || g.M % 4 || g.ldc % 4) return SA_ERR_ARG;
     if (g.ldc < (EPI == EPI_BF16_TP32 ? (g.M + 31) / 32 * 32 : g.M)) return SA_ERR_ARG;
+    // P32 stores 16-byte pieces of C^T rows
+    if (EPI == EPI_BF16_TP32 && (g.ldc % 8 || g.sC % 8 || ((uintptr_t)g.C & 15))) return SA_ERR_ARG;
   }
   const bool persistent = forced || (kernel == KERNEL_AUTO && persistent_ok);
   const int sched = s9 ? 9 : (kernel == KERNEL_PERSISTENT || kernel == KERNEL_PERSISTENT192) ? 8 : env_sched();

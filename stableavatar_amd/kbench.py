@@ -54,13 +54,17 @@ def main(which=("gemm", "attn")):
                                       (M, 8960, 1536, ops.EPI_GELU_TANH_BF16, "ffn_up"),
                                       (M, 1536, 8960, ops.EPI_RES_F32, "ffn_down"),
                                       (M, 1536, 8960, ops.EPI_BF16, "ffn_down_bf16"),
+                                      (M, 1536, 1536, ops.EPI_BF16_TP32, "v_t"),
                                       (8192, 8192, 8192, ops.EPI_BF16, "sq8192")]:
             if os.environ.get("SA_KB_SHAPES") and name not in os.environ["SA_KB_SHAPES"].split(","):
                 continue
             x = (torch.rand(Mx, K, device=dev) * 2 - 1).bfloat16()
             w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).bfloat16()
             b = torch.randn(N, device=dev)
-            out = torch.empty(Mx, N, device=dev, dtype=torch.float32 if epi == ops.EPI_RES_F32 else torch.bfloat16)
+            if epi == ops.EPI_BF16_TP32:  # the V^T operand of self-attention: [N, M rounded up to 64]
+                out = torch.empty(N, (Mx + 63) // 64 * 64, device=dev, dtype=torch.bfloat16)
+            else:
+                out = torch.empty(Mx, N, device=dev, dtype=torch.float32 if epi == ops.EPI_RES_F32 else torch.bfloat16)
             gate = torch.randn(3, N, device=dev)
             ref = None
             times = {v: [] for v in gvars}

@@ -241,10 +241,15 @@ def test_attention_spike_rescale(kernel):
         assert rel(o[r], ref[r]) < 1e-2, r
 
 
+X3_KERNELS = pytest.mark.parametrize("x3k", ["1", "2", "3"], ids=["w4", "w8", "persistent"])
+
+
+@X3_KERNELS
 @pytest.mark.parametrize("tok_offset", [0, 256])
-def test_attention_cross3(tok_offset):
+def test_attention_cross3(tok_offset, x3k, monkeypatch):
     """fused text + image + per-frame vocal cross-attention (1B:556-603) vs fp32 torch with the
-    reference's bf16 sum (bf16(text) + bf16(img)) + bf16(vocal)"""
+    reference's bf16 sum (bf16(text) + bf16(img)) + bf16(vocal); every kernel (SA_X3_KERNEL)"""
+    monkeypatch.setenv("SA_X3_KERNEL", x3k)
     from stableavatar_amd import ops
     B, H, D, tpf, F, nper, tl, il = 2, 2, 128, 256, 3, 17, 512, 257
     Lq = F * tpf - tok_offset
@@ -300,10 +305,12 @@ def test_attention_tail_block_stays_inside_segment(kernel):
         assert rel(o[b * Lq:(b + 1) * Lq, sl], ref) < 1e-2, h
 
 
-def test_attention_cross3_tail_blocks_stay_inside_sources():
+@X3_KERNELS
+def test_attention_cross3_tail_blocks_stay_inside_sources(x3k, monkeypatch):
     """fused cross-attention with every source's K/V followed by NaN rows: the image stream's last block (257 =
     4 x 64 + 1 keys) and the vocal half block (17 of 32 keys) of the last batch row / last frame must read
     zeros past their source, not the NaN that follows"""
+    monkeypatch.setenv("SA_X3_KERNEL", x3k)
     from stableavatar_amd import ops
     B, H, D, tpf, F, nper, tl, il = 2, 2, 128, 256, 2, 17, 512, 257
     HD = H * D
@@ -575,3 +582,43 @@ def test_layernorm_shared_modulation_bit_identical(in_bf16):
             torch.cuda.synchronize()
             outs.append(o)
         assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2]), sorted(kw)
+
+
+@pytest.mark.parametrize("q_len,tok_offset", [(21504, 0), (21504 - 300, 256)], ids=["config2", "ragged"])
+def test_attention_cross3_kernels_bit_identical_fullsize(q_len, tok_offset, monkeypatch):
+    """the 4-wave, 8-wave and persistent cross-attention kernels give the same output bytes at the config-2 shape
+    (3 CFG rows x 12 heads x 84 query tiles: the persistent kernel walks ~12 tiles per workgroup, its ring and Q
+    prefetch crossing tile seams), and the ragged last tile keeps the rows past q_len untouched"""
+    from stableavatar_amd import ops
+    B, H, D, nper, nfr, tl, il = 3, 12, 128, 32, 21, 512, 257
+    tpf = 21504 // nfr
+    HD = H * D
+    torch.manual_seed(3)
+    q = torch.randn(B * q_len, HD, device=dev).bfloat16()
+    kvt = torch.randn(B * tl, 2 * HD, device=dev).bfloat16()
+    kvi = torch.randn(B * il, 2 * HD, device=dev).bfloat16()
+    kvv = torch.randn(B * nfr * nper, 2 * HD, device=dev).bfloat16()
+    outs = {}
+    for k in ("1", "2", "3"):
+        monkeypatch.setenv("SA_X3_KERNEL", k)
+        o = torch.full((B * q_len + 64, HD), 7.0, device=dev, dtype=torch.bfloat16)
+        ops.attention_cross3(q, kvt[:, :HD], kvt[:, HD:], tl, kvi[:, :HD], kvi[:, HD:], il, kvv[:, :HD], kvv[:, HD:],
+                             nper, tpf, nfr, o[:B * q_len], B, q_len, H, tok_offset=tok_offset)
+        torch.cuda.synchronize()
+        assert (o[B * q_len:] == 7.0).all(), k
+        outs[k] = o[:B * q_len]
+    assert torch.isfinite(outs["1"].float()).all()
+    assert torch.equal(outs["2"], outs["1"]) and torch.equal(outs["3"], outs["1"])
+    # one row per (batch row, head) against fp32 torch
+    sc = D ** -0.5
+    for b in range(B):
+        r = b * q_len + (q_len - 1 if b == B - 1 else 1234)
+        f = (tok_offset + r - b * q_len) // tpf
+        for h in (0, H - 1):
+            sl, sv = slice(h * D, (h + 1) * D), slice(HD + h * D, HD + (h + 1) * D)
+            qq = q[r:r + 1, sl]
+            t = _ref_attn(qq, kvt[b * tl:(b + 1) * tl, sl], kvt[b * tl:(b + 1) * tl, sv], sc).bfloat16()
+            i = _ref_attn(qq, kvi[b * il:(b + 1) * il, sl], kvi[b * il:(b + 1) * il, sv], sc).bfloat16()
+            kr = slice((b * nfr + f) * nper, (b * nfr + f + 1) * nper)
+            vo = _ref_attn(qq, kvv[kr, sl], kvv[kr, sv], sc).bfloat16()
+            assert rel(outs["1"][r:r + 1, sl], (t + i) + vo) < 1e-2, (b, h)
