@@ -93,7 +93,6 @@ struct Cross3Args {
   bf16* o; long os;
   int q_len;
   float c;
-  int heads, batch;  // the persistent kernel's tile list (the others take them from the grid)
 };
 
 // ---- small-query attention for head dims the MFMA kernel does not take (vocal projector, D=192 for
@@ -1655,62 +1654,87 @@ __device__ __forceinline__ void attn_cross3_body(const Cross3Args& a) {
     reset();
   };
 
-  // Block j sits in ring slot j % NST, chosen at run time through the LDS read bases (kas / vas): one copy of the
-  // block body.  With a copy per slot (the slot as the ds_read immediate offset, round 4) hipcc spilled 118 (8 waves)
-  // / 152 (4 waves) VGPRs to scratch: every copy's temporaries live across the unrolled loop.
-  uint32_t kas[4], vas[8];
-  auto at_slot = [&](int slot) {
-    const uint32_t so = (uint32_t)slot * TILE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) kas[i] = ka[i] + so;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) vas[i] = va[i] + so;
-  };
-  // block j's DMA issued NST - 1 blocks ahead (with one block of lead the L2 latency of the next block was exposed
-  // at the barriers of these short streams)
-  auto step = [&](int jj) {
+  // block j in stage j % 3, its DMA issued two blocks ahead (with one block of lead the L2 latency of
+  // the next block was exposed at the barriers of these short streams)
+  auto step = [&](int jj, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
     if (NST > 2 && jj + 1 < ntot)
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");  // block jj landed; jj+1 may still fly
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (jj + NST - 1 < ntot) stage(jj + NST - 1, (jj + NST - 1) % NST);
+    if (jj + NST - 1 < ntot) stage(jj + NST - 1, (BUF + NST - 1) % NST);
     const int src = jj < nT ? 0 : (jj < nT + nI ? 1 : 2);
     const int kb = src == 0 ? jj : (src == 1 ? jj - nT : jj - nT - nI);
     const int len = src == 0 ? a.t_len : (src == 1 ? a.i_len : a.nper);
-    at_slot(jj % NST);
-    attn_v6_block<0, 0, false>(st, qf, kas, vas, kb, len, g, kb == 0);
+    attn_v6_block<BUF * TILE_BYTES, BUF * TILE_BYTES, false>(st, qf, ka, va, kb, len, g, kb == 0);
     if (jj == nT - 1 || jj == nT + nI - 1 || jj == ntot - 1) finish(src);
   };
-  // the vocal stream's single block when a frame has at most 32 audio tokens (StableAvatar: 32), and the image
-  // stream's last block when it holds at most 32 keys (CLIP: 257 = 4 x 64 + 1) while the vocal block is peeled too:
-  // peeled out of the loop as half blocks (key tiles 0-1: half the MFMAs and exponentials of a 64-key block)
+  // the vocal stream's single block when a frame has at most 32 audio tokens (StableAvatar: 32): peeled out of
+  // the loop as a half block (key tiles 0-1: half the MFMAs and exponentials of a 64-key block)
   const bool vhalf = nV == 1 && a.nper <= KVB / 2;
+  auto last_half = [&](int jj, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    attn_half_block<BUF * TILE_BYTES, BUF * TILE_BYTES>(st, qf, ka, va, 0, a.nper, g, true);
+    finish(2);
+  };
+  // likewise the image stream's last block when it holds at most 32 keys (CLIP: 257 = 4 x 64 + 1), when the vocal
+  // block is peeled too (so the loop still ends on a block boundary of the 3-stage ring)
   const bool ihalf = vhalf && a.i_len % KVB != 0 && a.i_len % KVB <= KVB / 2;
-  auto half = [&](bool voc) {
-    const int jj = voc ? ntot - 1 : ntot - 2;
-    if (!voc && NST > 2)
+  auto img_half = [&](int jj, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    if (NST > 2)
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");  // this block landed; the vocal block may fly
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (!voc && NST == 2) stage(jj + 1, (jj + 1) % NST);  // the vocal block, one ahead
-    at_slot(jj % NST);
-    attn_half_block<0, 0>(st, qf, kas, vas, voc ? 0 : nI - 1, voc ? a.nper : a.i_len, g, voc || nI == 1);
-    finish(voc ? 2 : 1);
+    if (NST == 2) stage(jj + 1, (BUF + 1) % NST);  // the vocal block, one ahead
+    attn_half_block<BUF * TILE_BYTES, BUF * TILE_BYTES>(st, qf, ka, va, nI - 1, a.i_len, g, nI == 1);
+    finish(1);
   };
   const int nloop = vhalf ? (ihalf ? ntot - 2 : ntot - 1) : ntot;
   if (NW == 8 && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
 #ifndef SA_X3_REPS
 #define SA_X3_REPS 1  // measurement builds only: > 1 runs the block stream that many times per tile (timing only)
 #endif
+#if SA_X3_REPS > 1
   for (int rep = 0; rep < SA_X3_REPS; ++rep) {
-    if (rep) __syncthreads();
-    stage(0, 0);
-    if (NST > 2 && 1 < ntot) stage(1, 1);
-    for (int j = 0; j < nloop; ++j) step(j);
-    for (int hb = ihalf ? 0 : 1; hb < (vhalf ? 2 : 0); ++hb) half(hb == 1);
+  if (rep) __syncthreads();
+#endif
+  stage(0, 0);
+  if (NST > 2 && 1 < ntot) stage(1, 1);
+  for (int j = 0; j < nloop; j += NST) {
+    step(j, std::integral_constant<int, 0>{});
+    if (j + 1 >= nloop) break;
+    step(j + 1, std::integral_constant<int, 1 % NST>{});
+    if (NST > 2) {
+      if (j + 2 >= nloop) break;
+      step(j + 2, std::integral_constant<int, 2 % NST>{});
+    }
   }
+  if (ihalf) {
+    const int ji = ntot - 2;
+    if (ji % NST == 0)
+      img_half(ji, std::integral_constant<int, 0>{});
+    else if (ji % NST == 1)
+      img_half(ji, std::integral_constant<int, 1 % NST>{});
+    else
+      img_half(ji, std::integral_constant<int, 2 % NST>{});
+  }
+  if (vhalf) {
+    const int jl = ntot - 1;
+    if (jl % NST == 0)
+      last_half(jl, std::integral_constant<int, 0>{});
+    else if (jl % NST == 1)
+      last_half(jl, std::integral_constant<int, 1 % NST>{});
+    else
+      last_half(jl, std::integral_constant<int, 2 % NST>{});
+  }
+#if SA_X3_REPS > 1
+  }
+#endif
 
   // 16-byte stores from permlane16-swapped column-group pairs, as the self-attention epilogue (T21)
 #pragma unroll
@@ -1727,244 +1751,7 @@ __device__ __forceinline__ void attn_cross3_body(const Cross3Args& a) {
   }
 }
 
-// ---- persistent fused cross-attention (round 5): one 8-wave workgroup per CU walks a contiguous run of query tiles
-// (256 queries of one (batch row, head); consecutive tiles share their text and image K/V).  Per tile the block
-// stream of attn_cross3_body<8, 3> (3-stage ring from slot 0, the image tail and vocal block as peeled half blocks:
-// the same arithmetic in the same order, the same output bytes), and around it
-//   * the next tile's Q DMA'd (K's row swizzle) into a 64-KB LDS region at the tile's first step and read back into
-//     registers at the seam (96 KB of ring + 64 KB of Q = the CU's 160 KB): no HBM round trip in a tile's prologue;
-//   * the next tile's first block DMA'd during the vocal block (when that block's slot is not slot 0).
-// The non-persistent kernels pay a Q load from HBM, a ring fill and a store drain per tile: 18 % of the launch
-// (profiles/r05/attn_cross3_overhead_anatomy_r5x.jsonl: 2 x 0.386 - 0.703 ms).
-constexpr int X3P_QBASE = X3_LDS, X3P_LDS = X3_LDS + 256 * 256;  // 96 KB ring + 64 KB Q = 160 KB
-#ifndef X3_AUTO_PERSISTENT
-#define X3_AUTO_PERSISTENT 0
-#endif
-
-__device__ __forceinline__ void attn_cross3_p_body(const Cross3Args& a) {
-  constexpr int NW = 8, NST = 3, QBW = NW * 32, PPW = 16 / NW, QPW = 8;  // QPW: Q pieces per wave
-  constexpr int VBASE = NST * TILE_BYTES;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nqb = (a.q_len + QBW - 1) / QBW;
-  const int T = a.batch * a.heads * nqb;
-  const int P = gridDim.x;
-  const int w = xcd_remap(blockIdx.x, P);  // one XCD takes a contiguous run of tiles
-  const int t_begin = (int)((long)w * T / P), t_end = (int)((long)(w + 1) * T / P);
-  if (t_begin >= t_end) return;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, r16 = lane & 15;
-  const int nT = (a.t_len + KVB - 1) / KVB, nI = (a.i_len + KVB - 1) / KVB, nV = (a.nper + KVB - 1) / KVB;
-  const int ntot = nT + nI + nV;
-  const bool vhalf = nV == 1 && a.nper <= KVB / 2;
-  const bool ihalf = vhalf && a.i_len % KVB != 0 && a.i_len % KVB <= KVB / 2;
-  const int nloop = vhalf ? (ihalf ? ntot - 2 : ntot - 1) : ntot;
-  // the next tile's block 0 goes into slot 0 during the last step when that step's block sits elsewhere
-  const bool early0 = vhalf && (ntot - 1) % NST != 0;
-
-  int srow[PPW], kch[PPW], vch[PPW];
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    srow[i] = (wave * PPW + i) * 4 + (lane >> 4);
-    kch[i] = r16 ^ (srow[i] & 15);
-    vch[i] = r16 ^ ((srow[i] & 7) << 1);
-  }
-  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
-  const uint32_t lds_k = __builtin_amdgcn_readfirstlane(lds0 + wave * PPW * 1024);
-  const uint32_t lds_q = __builtin_amdgcn_readfirstlane(lds0 + X3P_QBASE + wave * QPW * 1024);
-  int b = 0, h = 0, qb = 0;  // the current tile
-  auto set_tile = [&](int t) {
-    qb = t % nqb;
-    h = (t / nqb) % a.heads;
-    b = t / (nqb * a.heads);
-  };
-  set_tile(t_begin);
-  // block j of tile (bb, hh, qq) into ring slot buf (attn_cross3_body's stage)
-  auto stage = [&](int bb, int hh, int qq, int j, int buf) {
-    const bf16 *kb0, *vb0;
-    int st, blk, len;
-    if (j >= nT + nI) {
-      const int frame = (a.tok_offset + qq * QBW) / a.tpf;
-      const long off = (long)(bb * a.n_frames + frame) * a.nper * a.vs + hh * D;
-      kb0 = a.kv + off; vb0 = a.vv + off; st = (int)a.vs; blk = j - nT - nI; len = a.nper;
-    } else if (j >= nT) {
-      const long off = (long)bb * a.i_len * a.is + hh * D;
-      kb0 = a.ki + off; vb0 = a.vi + off; st = (int)a.is; blk = j - nT; len = a.i_len;
-    } else {
-      const long off = (long)bb * a.t_len * a.ts + hh * D;
-      kb0 = a.kt + off; vb0 = a.vt + off; st = (int)a.ts; blk = j; len = a.t_len;
-    }
-    const long r0 = (long)blk * KVB;
-    const int nrec = (int)((min((long)len - r0, (long)KVB) - 1) * st * 2 + 256);
-    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)(kb0 + r0 * st), (short)0, nrec, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(vb0 + r0 * st), (short)0, nrec, 0x00020000);
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const int rowoff = srow[i] * st * 2;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, LDS_PTR((uintptr_t)(lds_k + buf * TILE_BYTES + i * 1024)), 16,
-                                               rowoff + kch[i] * 16, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rv, LDS_PTR((uintptr_t)(lds_k + VBASE + buf * TILE_BYTES + i * 1024)), 16, rowoff + vch[i] * 16, 0, 0, 0);
-    }
-  };
-  // tile t's Q rows into the Q region (row r, 16-B chunk c at r * 256 + ((c ^ (r & 15)) << 4)); rows past the batch
-  // row's queries read as zeros (their outputs are not stored)
-  auto stage_q = [&](int t) {
-    const int qq = t % nqb, hh = (t / nqb) % a.heads, bb = t / (nqb * a.heads);
-    const int rows = min(a.q_len - qq * QBW, QBW);
-    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.q + ((long)bb * a.q_len + (long)qq * QBW) * a.qs + hh * D), (short)0,
-        (int)((rows - 1) * a.qs * 2 + 256), 0x00020000);
-#pragma unroll
-    for (int i = 0; i < QPW; ++i) {
-      const int row = (wave * QPW + i) * 4 + (lane >> 4);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rq, LDS_PTR((uintptr_t)(lds_q + i * 1024)), 16,
-                                               row * (int)a.qs * 2 + ((r16 ^ (row & 15)) << 4), 0, 0, 0);
-    }
-  };
-
-  uint32_t ka[4], va[8];
-#pragma unroll
-  for (int dc = 0; dc < 4; ++dc) ka[dc] = lds0 + r16 * 256 + (((dc * 4 + g) ^ r16) << 4);
-  {
-    const int q4 = r16 >> 2, p4 = r16 & 3;
-    const int row = 4 * g + q4;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      const int ch = 2 * dt + (p4 >> 1);
-      va[dt] = lds0 + VBASE + row * 256 + ((ch ^ ((row & 7) << 1)) << 4) + 8 * (p4 & 1);
-    }
-  }
-
-  V6State st;
-  auto reset = [&]() {
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) st.O[dt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    st.L[0] = st.L[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    st.negm[0] = st.negm[1] = 0.f;
-    st.negm4[0] = st.negm4[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  };
-  bf16x4 acc[8][2];  // running (text + img) + vocal, bf16 as in the reference
-  auto finish = [&](int src) {
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const float inv = 1.0f / st.L[qt][0];
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) {
-        bf16x4 x;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) x[i] = f2bf(st.O[dt][qt][i] * inv);
-        if (src == 0) {
-          acc[dt][qt] = x;
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[dt][qt][i] = f2bf(bf2f(acc[dt][qt][i]) + bf2f(x[i]));
-        }
-      }
-    }
-    reset();
-  };
-
-  uint32_t kas[4], vas[8];
-  auto at_slot = [&](int slot) {
-    const uint32_t so = (uint32_t)slot * TILE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) kas[i] = ka[i] + so;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) vas[i] = va[i] + so;
-  };
-  bf16x8 qf[2][4];
-  stage_q(t_begin);
-  stage(b, h, qb, 0, 0);
-  if (nloop > 1 || ntot > 1) stage(b, h, qb, 1, 1);
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // attn_cross3_body<8, 3>'s static priority of waves 4-7
-  bool staged0 = true;  // this tile's block 0 is already in flight
-  for (int t = t_begin; t < t_end; ++t) {
-    const bool q_next = t + 1 < t_end;
-    if (t != t_begin) {
-      set_tile(t);
-      if (!staged0) stage(b, h, qb, 0, 0);
-      stage(b, h, qb, 1, 1);
-    }
-    // this tile's Q (and block 0, the last tile's stores): everything but block 1's pieces
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    __syncthreads();
-    {
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-        for (int dc = 0; dc < 4; ++dc) {
-          const int row = wave * 32 + qt * 16 + r16;
-          qf[qt][dc] = *(const bf16x8*)(smem + X3P_QBASE + row * 256 + (((dc * 4 + g) ^ r16) << 4));
-#pragma unroll
-          for (int j = 0; j < 8; ++j) qf[qt][dc][j] = f2bf(bf2f(qf[qt][dc][j]) * a.c);
-        }
-    }
-    reset();
-    // block jj in slot jj % 3 (chosen at run time through the LDS read bases, as attn_cross3_body), its DMA two
-    // blocks ahead; the next tile's Q DMA at step 0 (after every wave read Q)
-    auto step = [&](int jj) {
-      if (jj + 1 < ntot) {
-        if (jj == 1 && q_next)
-          asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // block 1 landed; the next Q and block 2 may fly
-        else
-          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // block jj landed; jj+1 may still fly
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __syncthreads();
-      if (jj == 0 && q_next) stage_q(t + 1);
-      if (jj + NST - 1 < ntot) stage(b, h, qb, jj + NST - 1, (jj + NST - 1) % NST);
-      const int src = jj < nT ? 0 : (jj < nT + nI ? 1 : 2);
-      const int kb = src == 0 ? jj : (src == 1 ? jj - nT : jj - nT - nI);
-      const int len = src == 0 ? a.t_len : (src == 1 ? a.i_len : a.nper);
-      at_slot(jj % NST);
-      attn_v6_block<0, 0, false>(st, qf, kas, vas, kb, len, g, kb == 0);
-      if (jj == nT - 1 || jj == nT + nI - 1 || jj == ntot - 1) finish(src);
-    };
-    auto half = [&](bool voc) {
-      const int jj = voc ? ntot - 1 : ntot - 2;
-      if (!voc) {
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // this block landed; the vocal block may fly
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __syncthreads();
-      if (voc) {
-        staged0 = early0 && q_next;
-        if (staged0) {  // slot 0 is free (its last block finished before this barrier): the next tile's block 0
-          const int tn = t + 1;
-          stage(tn / (nqb * a.heads), (tn / nqb) % a.heads, tn % nqb, 0, 0);
-        }
-      }
-      at_slot(jj % NST);
-      attn_half_block<0, 0>(st, qf, kas, vas, voc ? 0 : nI - 1, voc ? a.nper : a.i_len, g, voc || nI == 1);
-      finish(voc ? 2 : 1);
-    };
-    for (int j = 0; j < nloop; ++j) step(j);
-    for (int hb = ihalf ? 0 : 1; hb < (vhalf ? 2 : 0); ++hb) half(hb == 1);
-    if (!vhalf) staged0 = false;
-    // 16-byte stores (attn_cross3_body's epilogue), left in flight under the next tile's first blocks
-    const int q_row0 = b * a.q_len;
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const int qi = qb * QBW + wave * 32 + qt * 16 + r16;
-      bf16* op = a.o + (long)(q_row0 + min(qi, a.q_len - 1)) * a.os + h * D + 4 * (g & ~1) + 16 * (g & 1);
-#pragma unroll
-      for (int dt = 0; dt < 8; dt += 2) {
-        const u32x2 ga = __builtin_bit_cast(u32x2, acc[dt][qt]), gb = __builtin_bit_cast(u32x2, acc[dt + 1][qt]);
-        const auto rx = __builtin_amdgcn_permlane16_swap(ga[0], gb[0], false, false);
-        const auto ry = __builtin_amdgcn_permlane16_swap(ga[1], gb[1], false, false);
-        if (qi < a.q_len) *(u32x4*)(op + dt * 16) = (u32x4){rx[0], ry[0], rx[1], ry[1]};
-      }
-    }
-  }
-}
-
 __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) { attn_cross3_body<8, 3>(a); }
-__global__ __launch_bounds__(512) void attn_cross3_p_kernel(Cross3Args a) { attn_cross3_p_body(a); }
 // 4 waves x 32 queries, 2-stage ring (64 KB): two workgroups per CU, so one's prologue (Q from HBM) and epilogue
 // stores run beside the other's blocks
 __global__ __launch_bounds__(256, 2) void attn_cross3_w4_kernel(Cross3Args a) { attn_cross3_body<4, 2>(a); }
@@ -2078,35 +1865,10 @@ extern "C" int sa_attn_cross3(const void* q, int64_t q_stride, const void* kt, c
   (void)attr;
   Cross3Args a{(const bf16*)q, q_stride, (const bf16*)kt, (const bf16*)vt, t_stride, t_len, (const bf16*)ki,
                (const bf16*)vi, i_stride, i_len, (const bf16*)kv, (const bf16*)vv, v_stride, nper,
-               tokens_per_frame, n_frames, tok_offset, (bf16*)o, o_stride, q_len, scale * 1.4426950408889634f,
-               heads, batch};
-  // SA_X3_KERNEL: 1 = 4-wave workgroups, two per CU; 2 = 8 waves; 3 = persistent (8 waves, one per CU, 160 KB LDS:
-  // needs at least 3 K/V blocks per tile); unset / 0 = auto
-  const int x3k = [] {  // read per call (tests switch it inside one process)
-    const char* e = getenv("SA_X3_KERNEL");
-    if (e) return atoi(e);
-    const char* w4 = getenv("SA_X3_W4");  // round-4 switch: 0 = the 8-wave kernel
-    return (w4 && !atoi(w4)) ? 2 : 0;
-  }();
-  const int ntot = (t_len + KVB - 1) / KVB + (i_len + KVB - 1) / KVB + (nper + KVB - 1) / KVB;
-  int kern = x3k;
-  if (kern == 3 && ntot < 3) return SA_ERR_ARG;
-  if (kern == 0) kern = X3_AUTO_PERSISTENT && ntot >= 3 ? 3 : 1;
-  if (kern == 3) {
-    static const bool pattr = [] {
-      (void)hipFuncSetAttribute((const void*)attn_cross3_p_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                X3P_LDS);
-      return true;
-    }();
-    (void)pattr;
-    int dev = 0, ncu = 256;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                 hipSuccess || ncu <= 0)
-      ncu = 256;
-    const long tiles = (long)batch * heads * ((q_len + QB - 1) / QB);
-    hipLaunchKernelGGL(attn_cross3_p_kernel, dim3((unsigned)min(tiles, (long)ncu)), dim3(512), X3P_LDS,
-                       (hipStream_t)stream, a);
-  } else if (kern == 1) {
+               tokens_per_frame, n_frames, tok_offset, (bf16*)o, o_stride, q_len, scale * 1.4426950408889634f};
+  // 4-wave workgroups, two per CU (0.369-0.377 vs 0.390 ms per config-2 launch, same output; SA_X3_W4=0: 8 waves)
+  const char* w4 = getenv("SA_X3_W4");
+  if (!w4 || atoi(w4)) {
     dim3 grid((q_len + 127) / 128, heads, batch);
     hipLaunchKernelGGL(attn_cross3_w4_kernel, grid, dim3(256), 4 * TILE_BYTES, (hipStream_t)stream, a);
   } else {
