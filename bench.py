@@ -36,7 +36,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "denoised frames/sec, Wan-1.3B 512²×81f audio-driven, 1/2/4/8 MI355X"
 PEAK_BF16 = 2.5e15  # dense bf16 MFMA, MI355X_MICROARCH.md
-ATTN_KERNEL_NAME = "attn_fwd_v6_kernel"
+ATTN_KERNEL_NAME = "attn_fwd_v6t_kernel"  # the V^T form (round 5); profiles/pmc_attn_traffic.json must name it
 
 
 def parse(argv=None):
@@ -755,7 +755,7 @@ def run(args, world, rank, dev, work_factory=ClipWorkload, cpu=None):
                       "dit_forwards_per_clip": n_fwd, "parallelism": parallelism,
                       "vae_decode": "split over the ranks" if (shared and world > 1 and args.vae_parallel)
                       else "whole clip on every rank" if world > 1 else "one GPU"},
-           "roofline": {"bound": "mfma", "kernel": f"{ATTN_KERNEL_NAME} (self-attention, flash, D=128)",
+           "roofline": {"bound": "mfma", "kernel": f"{ATTN_KERNEL_NAME} (self-attention, flash, D=128, V^T operand)",
                         "achieved": round(achieved / 1e12, 1) if achieved else None, "peak": PEAK_BF16 / 1e12,
                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16, 4) if achieved else None,
                         "traffic": round(traffic * attn_share) if traffic else None, "traffic_source": traffic_src,

@@ -6,7 +6,7 @@ set -u
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $c --kernel-include-regex "attn_fwd_v6_kernel|gemm_s8_kernel" --output-format csv \
+  timeout -k 10 300 rocprofv3 --pmc $c --kernel-include-regex "attn_fwd_v6t_kernel|gemm_s8_kernel" --output-format csv \
     -d gpurun_out/pmcb_$c -o run -- python bench.py --steps 1 --warmup 0 --sample-steps 2 --no-cpu-baseline \
     --no-encode > gpurun_out/pmcb_$c.log 2>&1
   rc=$?; echo "pmc $c rc=$rc"; tail -2 gpurun_out/pmcb_$c.log; [ $rc -ne 0 ] && exit $rc
