@@ -984,7 +984,10 @@ __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
 // up to 64; segments start on 32-key boundaries; every element of a row readable and finite through Rv: the
 // partial last block reads the keys past kv_len, masked to P = 0).  VMODE 1: keys permuted per 32 as P; VMODE 2:
 // natural key order.
-template <int VMODE>
+// NST: K/V ring stages.  2: block kb+1's DMA issued at block kb (one block of lead, vmcnt(0) + __syncthreads()
+// per block); 3 (kernel 6): block kb+2's DMA at block kb, a counted vmcnt that leaves block kb+1's pieces in flight
+// and a bare s_barrier (no release fence, which would wait for them)
+template <int VMODE, int NST = 2>
 __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
   constexpr int NW = 8, QBW = NW * 32, PPW = 16 / NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1042,16 +1045,20 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
     voff[i] = d * (int)a.vs * 2 + (((lane & 7) ^ sw) << 4);
   }
   const uint32_t lds_dma = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + wave * PPW * 1024);
+  // LDS: 2 stages as K | V pairs; 3 stages as a K region and a V region (V13_VBASE), so every ds_read immediate
+  // offset from its region's read base stays below 64 KB
   auto stage = [&](int kb, int buf) {
     const bool tail = ragged && kb == nkb - 1;
     const int ks_off = tail ? 0 : kb * KVB * (int)a.ks * 2, vs_off = kb * KVB * 2;
     const __amdgpu_buffer_rsrc_t bk = tail ? rkt : rk;
+    const int kdst = NST == 3 ? buf * TILE_BYTES : buf * STAGE_BYTES;
+    const int vdst = NST == 3 ? V13_VBASE + buf * TILE_BYTES : buf * STAGE_BYTES + TILE_BYTES;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(bk, LDS_PTR((uintptr_t)(lds_dma + buf * STAGE_BYTES + i * 1024)), 16,
-                                               koff[i], ks_off, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rv, LDS_PTR((uintptr_t)(lds_dma + buf * STAGE_BYTES + TILE_BYTES + i * 1024)), 16, voff[i], vs_off, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(bk, LDS_PTR((uintptr_t)(lds_dma + kdst + i * 1024)), 16, koff[i],
+                                               ks_off, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, LDS_PTR((uintptr_t)(lds_dma + vdst + i * 1024)), 16, voff[i],
+                                               vs_off, 0, 0);
     }
   };
   const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
@@ -1060,7 +1067,7 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
   for (int dc = 0; dc < 4; ++dc) ka[dc] = lds0 + r16 * 256 + (((dc * 4 + g) ^ r16) << 4);
   if constexpr (VMODE == 1) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c) vb[c] = lds0 + r16 * 128 + (((4 * c + g) ^ (r16 & 7)) << 4);
+    for (int c = 0; c < 2; ++c) vb[c] = lds0 + (NST == 3 ? V13_VBASE : 0) + r16 * 128 + (((4 * c + g) ^ (r16 & 7)) << 4);
     vb[2] = vb[3] = 0;
   } else {
     const int d32 = lane & 31, hh = lane >> 5;
@@ -1086,31 +1093,74 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
   st.negm[0] = st.negm[1] = 0.f;
   st.negm4[0] = st.negm4[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
   auto block = [&](auto koffc, auto firstc, int kb) {
-    constexpr int KO = decltype(koffc)::value;
+    constexpr int KO = decltype(koffc)::value;  // 2 stages: the stage's byte offset; 3 stages: the slot's
+    constexpr int VO = NST == 3 ? KO : KO + TILE_BYTES;
     constexpr bool FI = decltype(firstc)::value;
     if constexpr (VMODE == 2)
-      attn_v12_block<KO, KO + TILE_BYTES, FI>(st, qf, ka, vb, kb, kv_len, g, hi16);
+      attn_v12_block<KO, VO, FI>(st, qf, ka, vb, kb, kv_len, g, hi16);
     else
-      attn_v6t_block<KO, KO + TILE_BYTES, FI>(st, qf, ka, vb, kb, kv_len, g);
+      attn_v6t_block<KO, VO, FI>(st, qf, ka, vb, kb, kv_len, g);
   };
   using C0 = std::integral_constant<int, 0>;
   using C1 = std::integral_constant<int, STAGE_BYTES>;
-  stage(0, 0);
-  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (1 < nkb) stage(1, 1);
-  block(C0{}, std::true_type{}, 0);
-  for (int kb = 1; kb < nkb; kb += 2) {
+  if constexpr (NST == 2) {
+    stage(0, 0);
+    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (kb + 1 < nkb) stage(kb + 1, 0);
-    block(C1{}, std::false_type{}, kb);
-    if (kb + 1 >= nkb) break;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kb + 2 < nkb) stage(kb + 2, 1);
-    block(C0{}, std::false_type{}, kb + 1);
+    if (1 < nkb) stage(1, 1);
+    block(C0{}, std::true_type{}, 0);
+    for (int kb = 1; kb < nkb; kb += 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (kb + 1 < nkb) stage(kb + 1, 0);
+      block(C1{}, std::false_type{}, kb);
+      if (kb + 1 >= nkb) break;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (kb + 2 < nkb) stage(kb + 2, 1);
+      block(C0{}, std::false_type{}, kb + 1);
+    }
+  } else {
+    using S1 = std::integral_constant<int, TILE_BYTES>;
+    using S2 = std::integral_constant<int, 2 * TILE_BYTES>;
+    // block kb in slot kb % 3; its DMA issued two blocks ahead.  The barrier follows this wave's LDS reads of the
+    // slot restaged after it (lgkmcnt(0)); other waves' pieces of block kb are covered by their own vmcnt before it
+    auto sync = [] {
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto wait_block = [&](int kb) {  // block kb landed (this wave's pieces); kb+1's may still fly
+      if (kb + 1 < nkb)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    stage(0, 0);
+    if (1 < nkb) stage(1, 1);
+    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+    wait_block(0);
+    sync();
+    if (2 < nkb) stage(2, 2);
+    block(C0{}, std::true_type{}, 0);
+    for (int kb = 1; kb < nkb; kb += 3) {
+      wait_block(kb);
+      sync();
+      if (kb + 2 < nkb) stage(kb + 2, 0);
+      block(S1{}, std::false_type{}, kb);
+      if (kb + 1 >= nkb) break;
+      wait_block(kb + 1);
+      sync();
+      if (kb + 3 < nkb) stage(kb + 3, 1);
+      block(S2{}, std::false_type{}, kb + 1);
+      if (kb + 2 >= nkb) break;
+      wait_block(kb + 2);
+      sync();
+      if (kb + 4 < nkb) stage(kb + 4, 2);
+      block(C0{}, std::false_type{}, kb + 2);
+    }
   }
 
   if constexpr (VMODE == 2) {
@@ -1761,6 +1811,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_v6_w4_kernel(AttnArgs a) { at
 __global__ __launch_bounds__(512) void attn_fwd_v6t_kernel(AttnArgs a) { attn_fwd_vt_body<1>(a); }
 __global__ __launch_bounds__(512) void attn_fwd_v12_kernel(AttnArgs a) { attn_fwd_vt_body<2>(a); }
 __global__ __launch_bounds__(512) void attn_fwd_v13_kernel(AttnArgs a) { attn_fwd_pp_body(a); }
+__global__ __launch_bounds__(512) void attn_fwd_v6t3_kernel(AttnArgs a) { attn_fwd_vt_body<1, 3>(a); }
 
 }  // namespace
 
@@ -1780,7 +1831,7 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
   if (head_dim != D) return SA_ERR_ARG;
   if ((q_stride | k_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
   if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)o)) & 15) return SA_ERR_ARG;
-  if (kernel < 0 || kernel > 5) return SA_ERR_ARG;
+  if (kernel < 0 || kernel > 6) return SA_ERR_ARG;
   if (kernel >= 3 && (v_stride % 64 || (((uintptr_t)v) & 127))) return SA_ERR_ARG;  // V^T rows: whole 64-key blocks
   static const bool attr = [] {  // one-time, thread-safe
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
@@ -1789,6 +1840,8 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6t_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v12_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v13_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, V13_LDS);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_v6t3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              3 * STAGE_BYTES);
     return true;
   }();
   (void)attr;
@@ -1816,6 +1869,8 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
       hipLaunchKernelGGL(attn_fwd_v6t_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
     else if (kernel == 4)
       hipLaunchKernelGGL(attn_fwd_v12_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+    else if (kernel == 6)
+      hipLaunchKernelGGL(attn_fwd_v6t3_kernel, grid, dim3(512), 3 * STAGE_BYTES, (hipStream_t)stream, a);
     else
       hipLaunchKernelGGL(attn_fwd_v13_kernel, grid, dim3(512), V13_LDS, (hipStream_t)stream, a);
   } else {

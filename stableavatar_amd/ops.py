@@ -103,7 +103,7 @@ def bmm_nt(a, b, out, epilogue=EPI_F32, kernel=GEMM_AUTO):
 ATTN_AUTO = 0
 # kernel ids of sa_attn_fwd_ex that read V as V^T [H*128, Rv]: 3 = keys permuted per 32 in P's order (the QKV GEMM's
 # EPI_BF16_TP32 output), 4 = natural order with the PV product on 32x32x16 MFMAs (measured slower, kept for A/B)
-ATTN_VT_P32, ATTN_VT_PV32 = 3, 4
+ATTN_VT_P32, ATTN_VT_PV32, ATTN_VT_P32_3STAGE = 3, 4, 6  # 6: kernel 3 on a 3-stage K/V ring (A/B)
 
 
 def attention(q, k, v, out, segs, nseg, max_q_len, heads, head_dim=128, scale=None, accumulate=False,
