@@ -3,7 +3,9 @@ with a tiny synthetic model tree written in the layout the reference reads: wan_
 DiT config.json + safetensors at the root (transformer_subpath ./), the StableAvatar transformer3d-square.pt
 overlay ({"state_dict": ...}), Wan2.1_VAE.pth, umT5 .pth, the open-CLIP .pth (visual + a text-tower key that
 is ignored), a tokenizer directory and a wav2vec2 directory (transformers save_pretrained), a reference PNG
-and a 16 kHz WAV.  Checks the written video's shape and range."""
+and a 16 kHz WAV.  Checks that the command line reaches the pipeline with the reference's call arguments
+(inference.py:544-568), that the written video is that call's output, and that the call is deterministic (the same
+pipeline re-run with the captured arguments gives the same bytes)."""
 import json
 import os
 
@@ -85,11 +87,22 @@ def _write_tree(root):
 
 
 @pytest.mark.timeout(600)
-def test_inference_cli_end_to_end(tmp_path):
+def test_inference_cli_end_to_end(tmp_path, monkeypatch):
+    from stableavatar_amd import inference
     from stableavatar_amd.inference import main
+    from stableavatar_amd.pipeline import WanI2VTalkingInferenceLongPipeline
     root = str(tmp_path)
     _write_tree(root)
     out_dir = os.path.join(root, "output")
+    calls = []
+    orig = WanI2VTalkingInferenceLongPipeline.__call__
+
+    def spy(self, *a, **kw):
+        out = orig(self, *a, **kw)
+        calls.append((self, a, kw, out.videos.detach().float().cpu().clone()))
+        return out
+
+    monkeypatch.setattr(WanI2VTalkingInferenceLongPipeline, "__call__", spy)
     main(["--config_path", os.path.join(root, "config.yaml"), "--pretrained_model_name_or_path", root,
           "--transformer_path", os.path.join(root, "transformer3d-square.pt"),
           "--pretrained_wav2vec_path", os.path.join(root, "wav2vec"),
@@ -99,9 +112,26 @@ def test_inference_cli_end_to_end(tmp_path):
           "--motion_frame", "25", "--sample_steps", "2", "--width", "64", "--height", "64",
           "--overlap_window_length", "2", "--clip_sample_n_frames", "17", "--GPU_memory_mode", "model_full_load",
           "--sample_text_guide_scale", "3.0", "--sample_audio_guide_scale", "5.0"])
+    # the reference's call (inference.py:544-568): the CLI's flags mapped to the pipeline arguments
+    assert len(calls) == 1
+    pipe, a, kw, video = calls[0]
+    assert a[0] == "a woman is singing"
+    assert kw["negative_prompt"] == inference.NEGATIVE_PROMPT
+    want = dict(num_frames=17, height=64, width=64, guidance_scale=6.0, num_inference_steps=2, text_guide_scale=3.0,
+                audio_guide_scale=5.0, motion_frame=25, fps=25, sr=16000, seed=42, overlap_window_length=2,
+                clip_length=17, cond_file_path=os.path.join(root, "reference.png"))
+    for k_, v_ in want.items():
+        assert kw[k_] == v_, (k_, kw[k_], v_)
+    assert kw["vocal_input_values"].shape == (24 * 640,)  # 16 kHz audio as written (no resampling needed)
     if os.path.exists(os.path.join(out_dir, "video.npy")):
         v = np.load(os.path.join(out_dir, "video.npy"))
         assert v.shape == (1, 3, 21, 64, 64) and np.isfinite(v).all() and v.min() >= 0 and v.max() <= 1
         assert len(os.listdir(os.path.join(out_dir, "animated_images"))) == 21
+        assert np.array_equal(v, video.numpy()), "the saved video is the pipeline call's output"
     else:
         assert os.path.exists(os.path.join(out_dir, "video_without_audio.mp4"))
+    # deterministic: the same pipeline, the captured arguments and a fresh generator at the same seed
+    kw2 = dict(kw, generator=torch.Generator(device=kw["generator"].device).manual_seed(42))
+    with torch.no_grad():
+        again = orig(pipe, *a, **kw2).videos.float().cpu()
+    assert torch.equal(again, video)
