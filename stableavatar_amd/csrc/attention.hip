@@ -984,12 +984,27 @@ __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
 // up to 64; segments start on 32-key boundaries; every element of a row readable and finite through Rv: the
 // partial last block reads the keys past kv_len, masked to P = 0).  VMODE 1: keys permuted per 32 as P; VMODE 2:
 // natural key order.
+#if defined(SA_V13_STAMPS) || defined(SA_V6T_STAMPS)
+// measurement builds only (scripts/build_variant.sh ... -DSA_V13_STAMPS / -DSA_V6T_STAMPS): summed s_memtime cycles
+// per wave group over every wave of the launch (v13: barrier 1, work 1, barrier 2, MFMA phase; v6t: the DMA wait,
+// the barrier, the block loop, the blocks)
+__device__ unsigned long long g_v13_stamps[12];
+__device__ __forceinline__ uint64_t v13_now() {
+  const uint64_t t = __builtin_amdgcn_s_memtime();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  return t;
+}
+#endif
+
 // NST: K/V ring stages.  2: block kb+1's DMA issued at block kb (one block of lead, vmcnt(0) + __syncthreads()
 // per block); 3 (kernel 6): block kb+2's DMA at block kb, a counted vmcnt that leaves block kb+1's pieces in flight
 // and a bare s_barrier (no release fence, which would wait for them)
-template <int VMODE, int NST = 2>
+// DMAW: the waves that issue the K / V DMA (8: every wave, 2 + 2 pieces per block; 4: waves 4-7 only, 4 + 4 pieces:
+// kernel 7).  Waves 4-7 run at s_setprio 1 and reach each block's barrier ~800 cycles before waves 0-3
+// (profiles/r05/attn_v6t_barrier_anatomy_r5.json), so the issue slots of the DMA move to the waves that wait anyway.
+template <int VMODE, int NST = 2, int DMAW = 8>
 __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
-  constexpr int NW = 8, QBW = NW * 32, PPW = 16 / NW;
+  constexpr int NW = 8, QBW = NW * 32, PPW = 16 / DMAW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nx = gridDim.x, ny = gridDim.y;
   const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
@@ -1035,19 +1050,21 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
   const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.v + (long)h * D * a.vs + kv_row0), (short)0, (int)(((long)(D - 1) * a.vs + (long)nkb * KVB) * 2),
       0x00020000);
+  const int dw = DMAW == 8 ? wave : wave - 4;  // this wave's DMA share (waves 0-3 have none when DMAW == 4)
   int koff[PPW], voff[PPW];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
-    const int srow = (wave * PPW + i) * 4 + (lane >> 4);
+    const int srow = (dw * PPW + i) * 4 + (lane >> 4);
     koff[i] = srow * (int)a.ks * 2 + ((r16 ^ (srow & 15)) << 4);
-    const int d = (wave * PPW + i) * 8 + (lane >> 3);  // a 1-KB piece = 8 d-rows x 128 B
+    const int d = (dw * PPW + i) * 8 + (lane >> 3);  // a 1-KB piece = 8 d-rows x 128 B
     const int sw = VMODE == 1 ? (d & 7) : ((d >> 1) & 7);
     voff[i] = d * (int)a.vs * 2 + (((lane & 7) ^ sw) << 4);
   }
-  const uint32_t lds_dma = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + wave * PPW * 1024);
+  const uint32_t lds_dma = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + dw * PPW * 1024);
   // LDS: 2 stages as K | V pairs; 3 stages as a K region and a V region (V13_VBASE), so every ds_read immediate
   // offset from its region's read base stays below 64 KB
   auto stage = [&](int kb, int buf) {
+    if (DMAW == 4 && wave < 4) return;  // wave-uniform
     const bool tail = ragged && kb == nkb - 1;
     const int ks_off = tail ? 0 : kb * KVB * (int)a.ks * 2, vs_off = kb * KVB * 2;
     const __amdgpu_buffer_rsrc_t bk = tail ? rkt : rk;
@@ -1110,17 +1127,44 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
     __syncthreads();
     if (1 < nkb) stage(1, 1);
     block(C0{}, std::true_type{}, 0);
+#ifdef SA_V6T_STAMPS
+    uint64_t sacc[3] = {0, 0, 0};  // DMA wait, barrier, loop
+    const uint64_t tl0 = v13_now();
+#define V6T_SYNC()                                    \
+  {                                                   \
+    const uint64_t ta = v13_now();                    \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+    const uint64_t tb = v13_now();                    \
+    __syncthreads();                                  \
+    const uint64_t tc = v13_now();                    \
+    sacc[0] += tb - ta;                               \
+    sacc[1] += tc - tb;                               \
+  }
+#else
+#define V6T_SYNC()                                    \
+  {                                                   \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+    __syncthreads();                                  \
+  }
+#endif
     for (int kb = 1; kb < nkb; kb += 2) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      V6T_SYNC();
       if (kb + 1 < nkb) stage(kb + 1, 0);
       block(C1{}, std::false_type{}, kb);
       if (kb + 1 >= nkb) break;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      V6T_SYNC();
       if (kb + 2 < nkb) stage(kb + 2, 1);
       block(C0{}, std::false_type{}, kb + 1);
     }
+#undef V6T_SYNC
+#ifdef SA_V6T_STAMPS
+    sacc[2] = v13_now() - tl0;
+    if (lane == 0) {
+      const int gi = __builtin_amdgcn_readfirstlane(tid >> 6) >= 4 ? 6 : 0;
+      for (int k = 0; k < 3; ++k) atomicAdd(&g_v13_stamps[gi + k], (unsigned long long)sacc[k]);
+      atomicAdd(&g_v13_stamps[gi + 3], (unsigned long long)(nkb - 1));
+    }
+#endif
   } else {
     using S1 = std::integral_constant<int, TILE_BYTES>;
     using S2 = std::integral_constant<int, 2 * TILE_BYTES>;
@@ -1325,14 +1369,6 @@ __device__ __forceinline__ void v13_sync() {
 }
 
 #ifdef SA_V13_STAMPS
-// measurement builds only (scripts/build_variant.sh ... -DSA_V13_STAMPS): per group (A, B) the summed s_memtime
-// cycles of the body's four parts (barrier 1, work 1, barrier 2, MFMA phase) over every wave of the launch
-__device__ unsigned long long g_v13_stamps[12];
-__device__ __forceinline__ uint64_t v13_now() {
-  const uint64_t t = __builtin_amdgcn_s_memtime();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  return t;
-}
 #define V13_STAMP(x) const uint64_t x = v13_now()
 #define V13_ACC(k, v) acc[k] += (v)
 #else
@@ -1812,6 +1848,7 @@ __global__ __launch_bounds__(512) void attn_fwd_v6t_kernel(AttnArgs a) { attn_fw
 __global__ __launch_bounds__(512) void attn_fwd_v12_kernel(AttnArgs a) { attn_fwd_vt_body<2>(a); }
 __global__ __launch_bounds__(512) void attn_fwd_v13_kernel(AttnArgs a) { attn_fwd_pp_body(a); }
 __global__ __launch_bounds__(512) void attn_fwd_v6t3_kernel(AttnArgs a) { attn_fwd_vt_body<1, 3>(a); }
+__global__ __launch_bounds__(512) void attn_fwd_v6th_kernel(AttnArgs a) { attn_fwd_vt_body<1, 2, 4>(a); }
 
 }  // namespace
 
@@ -1831,7 +1868,7 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
   if (head_dim != D) return SA_ERR_ARG;
   if ((q_stride | k_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
   if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)o)) & 15) return SA_ERR_ARG;
-  if (kernel < 0 || kernel > 6) return SA_ERR_ARG;
+  if (kernel < 0 || kernel > 7) return SA_ERR_ARG;
   if (kernel >= 3 && (v_stride % 64 || (((uintptr_t)v) & 127))) return SA_ERR_ARG;  // V^T rows: whole 64-key blocks
   static const bool attr = [] {  // one-time, thread-safe
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
@@ -1842,6 +1879,7 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
     (void)hipFuncSetAttribute((const void*)attn_fwd_v13_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, V13_LDS);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6t3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               3 * STAGE_BYTES);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_v6th_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     return true;
   }();
   (void)attr;
@@ -1871,6 +1909,8 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
       hipLaunchKernelGGL(attn_fwd_v12_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
     else if (kernel == 6)
       hipLaunchKernelGGL(attn_fwd_v6t3_kernel, grid, dim3(512), 3 * STAGE_BYTES, (hipStream_t)stream, a);
+    else if (kernel == 7)
+      hipLaunchKernelGGL(attn_fwd_v6th_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
     else
       hipLaunchKernelGGL(attn_fwd_v13_kernel, grid, dim3(512), V13_LDS, (hipStream_t)stream, a);
   } else {
@@ -1934,7 +1974,7 @@ extern "C" int sa_attn_cross3(const void* q, int64_t q_stride, const void* kt, c
   return SA_OK;
 }
 
-#ifdef SA_V13_STAMPS
+#if defined(SA_V13_STAMPS) || defined(SA_V6T_STAMPS)
 extern "C" int sa_debug_v13_stamps(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_v13_stamps), sizeof(unsigned long long) * 12) != hipSuccess) return SA_ERR_ARG;
   if (reset) {
