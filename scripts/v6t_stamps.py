@@ -14,7 +14,7 @@ from stableavatar_amd import _lib, ops  # noqa: E402
 from stableavatar_amd.kbench import vt_layout  # noqa: E402
 
 L, H, D = 21504, 12, 128
-KERN = int(os.environ.get("SA_STAMPS_KERNEL", "3"))  # 3: v6t, 7: DMA on waves 4-7 only
+KERN = int(os.environ.get("SA_STAMPS_KERNEL", "3"))  # the V^T kernel to stamp (3: v6t)
 dev = "cuda"
 qkv = torch.randn(3 * L, 3 * H * D, device=dev).bfloat16()
 segs = torch.tensor([[b * L, L, b * L, L] for b in range(3)], dtype=torch.int32, device=dev)

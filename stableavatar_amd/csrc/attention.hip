@@ -999,12 +999,9 @@ __device__ __forceinline__ uint64_t v13_now() {
 // NST: K/V ring stages.  2: block kb+1's DMA issued at block kb (one block of lead, vmcnt(0) + __syncthreads()
 // per block); 3 (kernel 6): block kb+2's DMA at block kb, a counted vmcnt that leaves block kb+1's pieces in flight
 // and a bare s_barrier (no release fence, which would wait for them)
-// DMAW: the waves that issue the K / V DMA (8: every wave, 2 + 2 pieces per block; 4: waves 4-7 only, 4 + 4 pieces:
-// kernel 7).  Waves 4-7 run at s_setprio 1 and reach each block's barrier ~800 cycles before waves 0-3
-// (profiles/r05/attn_v6t_barrier_anatomy_r5.json), so the issue slots of the DMA move to the waves that wait anyway.
-template <int VMODE, int NST = 2, int DMAW = 8>
+template <int VMODE, int NST = 2>
 __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
-  constexpr int NW = 8, QBW = NW * 32, PPW = 16 / DMAW;
+  constexpr int NW = 8, QBW = NW * 32, PPW = 16 / NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nx = gridDim.x, ny = gridDim.y;
   const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
@@ -1050,7 +1047,7 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
   const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.v + (long)h * D * a.vs + kv_row0), (short)0, (int)(((long)(D - 1) * a.vs + (long)nkb * KVB) * 2),
       0x00020000);
-  const int dw = DMAW == 8 ? wave : wave - 4;  // this wave's DMA share (waves 0-3 have none when DMAW == 4)
+  const int dw = wave;  // this wave's share of the K / V pieces
   int koff[PPW], voff[PPW];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
@@ -1064,7 +1061,6 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
   // LDS: 2 stages as K | V pairs; 3 stages as a K region and a V region (V13_VBASE), so every ds_read immediate
   // offset from its region's read base stays below 64 KB
   auto stage = [&](int kb, int buf) {
-    if (DMAW == 4 && wave < 4) return;  // wave-uniform
     const bool tail = ragged && kb == nkb - 1;
     const int ks_off = tail ? 0 : kb * KVB * (int)a.ks * 2, vs_off = kb * KVB * 2;
     const __amdgpu_buffer_rsrc_t bk = tail ? rkt : rk;
@@ -1848,7 +1844,6 @@ __global__ __launch_bounds__(512) void attn_fwd_v6t_kernel(AttnArgs a) { attn_fw
 __global__ __launch_bounds__(512) void attn_fwd_v12_kernel(AttnArgs a) { attn_fwd_vt_body<2>(a); }
 __global__ __launch_bounds__(512) void attn_fwd_v13_kernel(AttnArgs a) { attn_fwd_pp_body(a); }
 __global__ __launch_bounds__(512) void attn_fwd_v6t3_kernel(AttnArgs a) { attn_fwd_vt_body<1, 3>(a); }
-__global__ __launch_bounds__(512) void attn_fwd_v6th_kernel(AttnArgs a) { attn_fwd_vt_body<1, 2, 4>(a); }
 
 }  // namespace
 
@@ -1868,7 +1863,7 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
   if (head_dim != D) return SA_ERR_ARG;
   if ((q_stride | k_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
   if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)o)) & 15) return SA_ERR_ARG;
-  if (kernel < 0 || kernel > 7) return SA_ERR_ARG;
+  if (kernel < 0 || kernel > 6) return SA_ERR_ARG;
   if (kernel >= 3 && (v_stride % 64 || (((uintptr_t)v) & 127))) return SA_ERR_ARG;  // V^T rows: whole 64-key blocks
   static const bool attr = [] {  // one-time, thread-safe
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
@@ -1879,7 +1874,6 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
     (void)hipFuncSetAttribute((const void*)attn_fwd_v13_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, V13_LDS);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6t3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               3 * STAGE_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_v6th_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     return true;
   }();
   (void)attr;
@@ -1909,8 +1903,6 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
       hipLaunchKernelGGL(attn_fwd_v12_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
     else if (kernel == 6)
       hipLaunchKernelGGL(attn_fwd_v6t3_kernel, grid, dim3(512), 3 * STAGE_BYTES, (hipStream_t)stream, a);
-    else if (kernel == 7)
-      hipLaunchKernelGGL(attn_fwd_v6th_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
     else
       hipLaunchKernelGGL(attn_fwd_v13_kernel, grid, dim3(512), V13_LDS, (hipStream_t)stream, a);
   } else {
