@@ -1064,8 +1064,8 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
     const bool tail = ragged && kb == nkb - 1;
     const int ks_off = tail ? 0 : kb * KVB * (int)a.ks * 2, vs_off = kb * KVB * 2;
     const __amdgpu_buffer_rsrc_t bk = tail ? rkt : rk;
-    const int kdst = NST == 3 ? buf * TILE_BYTES : buf * STAGE_BYTES;
-    const int vdst = NST == 3 ? V13_VBASE + buf * TILE_BYTES : buf * STAGE_BYTES + TILE_BYTES;
+    const int kdst = NST >= 3 ? buf * TILE_BYTES : buf * STAGE_BYTES;
+    const int vdst = NST >= 3 ? NST * TILE_BYTES + buf * TILE_BYTES : buf * STAGE_BYTES + TILE_BYTES;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(bk, LDS_PTR((uintptr_t)(lds_dma + kdst + i * 1024)), 16, koff[i],
@@ -1080,7 +1080,8 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
   for (int dc = 0; dc < 4; ++dc) ka[dc] = lds0 + r16 * 256 + (((dc * 4 + g) ^ r16) << 4);
   if constexpr (VMODE == 1) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c) vb[c] = lds0 + (NST == 3 ? V13_VBASE : 0) + r16 * 128 + (((4 * c + g) ^ (r16 & 7)) << 4);
+    for (int c = 0; c < 2; ++c)
+      vb[c] = lds0 + (NST >= 3 ? NST * TILE_BYTES : 0) + r16 * 128 + (((4 * c + g) ^ (r16 & 7)) << 4);
     vb[2] = vb[3] = 0;
   } else {
     const int d32 = lane & 31, hh = lane >> 5;
@@ -1107,7 +1108,7 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
   st.negm4[0] = st.negm4[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
   auto block = [&](auto koffc, auto firstc, int kb) {
     constexpr int KO = decltype(koffc)::value;  // 2 stages: the stage's byte offset; 3 stages: the slot's
-    constexpr int VO = NST == 3 ? KO : KO + TILE_BYTES;
+    constexpr int VO = NST >= 3 ? KO : KO + TILE_BYTES;
     constexpr bool FI = decltype(firstc)::value;
     if constexpr (VMODE == 2)
       attn_v12_block<KO, VO, FI>(st, qf, ka, vb, kb, kv_len, g, hi16);
