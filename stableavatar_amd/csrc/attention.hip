@@ -1268,266 +1268,6 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
   }
 }
 
-// ---- v14 (kernel 7): the whole block on v_mfma_f32_32x32x16_bf16.  Per wave and 64-key block: 16 QK^T + 16 PV
-// MFMAs (32 cycles each, each holding vector issue for 8) instead of v6t's 68 16x16x32 ones (16 cycles, 8 held):
-// 256 instead of 544 issue cycles of MFMA per wave, the rest of the block's issue (32 v_exp, 16 v_maximum3, 16
-// v_cvt_pk, 32 ds_read_b128, the DMA) unchanged -- v6t is issue-bound (two waves' ~2 800 issue cycles per block
-// against 2 176 of matrix pipe, 3 120 measured), this form is pipe-bound by design.
-//   S^T tile kt (32 keys x 32 queries) = K_kt Q^T: lane l holds query l % 32, keys 32 kt + 8 (i / 4) + 4 h + i % 4
-//   (h = l / 32, i < 16); the -m initial accumulator and every softmax quantity are per lane (one query per lane,
-//   the row max over the two lane halves by one permlane32 swap).
-//   P^T as the PV B operand of 16-key step s: the lane's own 8 values of S[s / 2][8 (s % 2) .. +7], i.e. k-index
-//   8 h + j <- key 16 s + 4 h + j (j < 4), 16 s + 8 + 4 h + j - 4 (j >= 4): V^T is stored in that key order per 16
-//   keys (P16 order), so no lane exchange is needed.  V^T staged and read as kernel 4's (32 d-rows per MFMA).
-//   Row sums in fp32 on the VALU from the fp32 P (kernel 3 sums the bf16 P on the matrix pipe: not bit-identical).
-struct V14State {
-  f32x16 O[4];  // O^T d-tile dt: lane = query l % 32, d = 32 dt + 8 (i / 4) + 4 h + i % 4
-  float lsum;   // this lane's half of its query's row sum
-  float negm;   // -m of this lane's query
-};
-
-template <int KOFF, int VOFF, bool FIRST>
-__device__ __forceinline__ void attn_v14_block(V14State& st, const bf16x8 (&qf)[8], const uint32_t* ka,
-                                               const uint32_t* vb, int kb, int kv_len, int h) {
-  f32x16 S[2];
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) S[kt][i] = st.negm;
-  // K fragments (32 keys x 16 d per MFMA) in groups of 4 d-steps, one group ahead
-  u32x4 k0[4], k1[4];
-  ds_b128<KOFF + 0>(k0[0], ka[0]); ds_b128<KOFF + 0>(k0[1], ka[1]);
-  ds_b128<KOFF + 0>(k0[2], ka[2]); ds_b128<KOFF + 0>(k0[3], ka[3]);
-  ds_b128<KOFF + 0>(k1[0], ka[4]); ds_b128<KOFF + 0>(k1[1], ka[5]);
-  ds_b128<KOFF + 0>(k1[2], ka[6]); ds_b128<KOFF + 0>(k1[3], ka[7]);
-  wait_k4<4>(k0);
-#pragma unroll
-  for (int s = 0; s < 4; ++s) S[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v6_as_bf8(k0[s]), qf[s], S[0], 0, 0, 0);
-  ds_b128<KOFF + 8192>(k0[0], ka[0]); ds_b128<KOFF + 8192>(k0[1], ka[1]);
-  ds_b128<KOFF + 8192>(k0[2], ka[2]); ds_b128<KOFF + 8192>(k0[3], ka[3]);
-  wait_k4<4>(k1);
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-    S[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v6_as_bf8(k1[s]), qf[4 + s], S[0], 0, 0, 0);
-  ds_b128<KOFF + 8192>(k1[0], ka[4]); ds_b128<KOFF + 8192>(k1[1], ka[5]);
-  ds_b128<KOFF + 8192>(k1[2], ka[6]); ds_b128<KOFF + 8192>(k1[3], ka[7]);
-  wait_k4<4>(k0);
-#pragma unroll
-  for (int s = 0; s < 4; ++s) S[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v6_as_bf8(k0[s]), qf[s], S[1], 0, 0, 0);
-  wait_k4<0>(k1);
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-    S[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v6_as_bf8(k1[s]), qf[4 + s], S[1], 0, 0, 0);
-  // first V^T fragments (16-key step 0, the four d-tiles) under the softmax
-  u32x4 va[4], vc[4];
-  v12_read_v<VOFF, 0>(va, vb);
-  if (kb * KVB + KVB > kv_len) {
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if (kb * KVB + 32 * kt + 8 * (i / 4) + 4 * h + (i % 4) >= kv_len) S[kt][i] = -INFINITY;
-  }
-  float v[32];
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) v[16 * kt + i] = S[kt][i];
-  float r[12];
-#pragma unroll
-  for (int j = 0; j < 10; ++j) r[j] = vmax3(v[3 * j], v[3 * j + 1], v[3 * j + 2]);
-  r[10] = v[30];
-  r[11] = v[31];
-  const float lm = vmax2(vmax3(vmax3(r[0], r[1], r[2]), vmax3(r[3], r[4], r[5]), vmax3(r[6], r[7], r[8])),
-                         vmax3(r[9], r[10], r[11]));
-  if (FIRST || !__all(lm <= RESCALE_THR)) {  // wave-uniform
-    const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(lm), __float_as_uint(lm), false, false);
-    const float mx = vmax2(__uint_as_float(x[0]), __uint_as_float(x[1]));  // the query's max over the block
-    const float delta = FIRST ? mx : fmaxf(mx, 0.f);
-    if (!FIRST) {
-      const float alpha = __builtin_amdgcn_exp2f(-delta);
-      st.lsum *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) st.O[dt][i] *= alpha;
-    }
-    st.negm -= delta;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) S[kt][i] -= delta;
-  }
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) S[kt][i] = __builtin_amdgcn_exp2f(S[kt][i]);
-  bf16x8 pb[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) pb[s][j] = f2bf(S[s / 2][8 * (s % 2) + j]);
-  // row sum of this lane's 32 P values (a pairwise tree)
-  {
-    float t[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) t[j] = S[0][j] + S[1][j];
-#pragma unroll
-    for (int w = 8; w >= 1; w /= 2)
-#pragma unroll
-      for (int j = 0; j < w; ++j) t[j] += t[j + w];
-    st.lsum += t[0];
-  }
-  // O^T += V^T P^T, one 16-key step at a time, the next step's V^T fragments read under the current step's MFMAs
-  v12_read_v<VOFF, 1>(vc, vb);
-  wait_k4<4>(va);
-  v12_mma_v(st.O, va, pb[0]);
-  v12_read_v<VOFF, 2>(va, vb);
-  wait_k4<4>(vc);
-  v12_mma_v(st.O, vc, pb[1]);
-  v12_read_v<VOFF, 3>(vc, vb);
-  wait_k4<4>(va);
-  v12_mma_v(st.O, va, pb[2]);
-  wait_k4<0>(vc);
-  v12_mma_v(st.O, vc, pb[3]);
-}
-
-__device__ __forceinline__ void attn_fwd_v14_body(const AttnArgs& a) {
-  constexpr int NW = 8, QBW = NW * 32, PPW = 16 / NW;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nx = gridDim.x, ny = gridDim.y;
-  const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
-  const int qb = flat % nx, hd = (flat / nx) % ny, seg = flat / (nx * ny);
-  const int* sg = a.segs + seg * 4;
-  const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
-  if (qb * QBW >= q_len) return;
-  const int tid = threadIdx.x, lane = tid & 63;
-  if (kv_len <= 0) {
-    if (!a.accumulate)
-      for (int i = tid; i < QBW * (D / 8); i += NW * 64) {
-        const int qi = qb * QBW + i / (D / 8);
-        if (qi < q_len) {
-          const int orow = a.orows ? a.orows[q_row0 + qi] : q_row0 + qi;
-          *(u32x4*)(a.o + (long)orow * a.os + hd * D + (i % (D / 8)) * 8) = (u32x4){0u, 0u, 0u, 0u};
-        }
-      }
-    return;
-  }
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l32 = lane & 31, h = lane >> 5;
-  // Q^T as the B operand of d-step s (16 d): lane = query l % 32, d 16 s + 8 h .. + 7, prescaled by c
-  bf16x8 qf[8];
-  {
-    const int qc = min(qb * QBW + wave * 32 + l32, q_len - 1);
-    const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + hd * D + 8 * h;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      qf[s] = *(const bf16x8*)(qp + 16 * s);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[s][j] = f2bf(bf2f(qf[s][j]) * a.c);
-    }
-  }
-  const int nkb = (kv_len + KVB - 1) / KVB;
-  const long tail0 = (long)(nkb - 1) * KVB;
-  const bool ragged = kv_len % KVB != 0;
-  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.k + (long)kv_row0 * a.ks + hd * D), (short)0, (int)(((long)kv_len - 1) * a.ks * 2 + 256), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rkt = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.k + (kv_row0 + tail0) * a.ks + hd * D), (short)0, (int)((kv_len - tail0 - 1) * a.ks * 2 + 256),
-      0x00020000);
-  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.v + (long)hd * D * a.vs + kv_row0), (short)0, (int)(((long)(D - 1) * a.vs + (long)nkb * KVB) * 2),
-      0x00020000);
-  const int r16 = lane & 15;
-  int koff[PPW], voff[PPW];
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    const int srow = (wave * PPW + i) * 4 + (lane >> 4);
-    koff[i] = srow * (int)a.ks * 2 + ((r16 ^ (srow & 15)) << 4);
-    const int d = (wave * PPW + i) * 8 + (lane >> 3);
-    voff[i] = d * (int)a.vs * 2 + (((lane & 7) ^ ((d >> 1) & 7)) << 4);
-  }
-  const uint32_t lds_dma = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + wave * PPW * 1024);
-  auto stage = [&](int kb, int buf) {
-    const bool tail = ragged && kb == nkb - 1;
-    const int ks_off = tail ? 0 : kb * KVB * (int)a.ks * 2, vs_off = kb * KVB * 2;
-    const __amdgpu_buffer_rsrc_t bk = tail ? rkt : rk;
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(bk, LDS_PTR((uintptr_t)(lds_dma + buf * STAGE_BYTES + i * 1024)), 16,
-                                               koff[i], ks_off, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rv, LDS_PTR((uintptr_t)(lds_dma + buf * STAGE_BYTES + TILE_BYTES + i * 1024)), 16, voff[i], vs_off, 0, 0);
-    }
-  };
-  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
-  // K rows l % 32 (+32 for key tile 1 by immediate), 16-B chunk 2 s + h of d-step s (K's row swizzle)
-  uint32_t ka[8], vb[4];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) ka[s] = lds0 + l32 * 256 + (((2 * s + h) ^ (l32 & 15)) << 4);
-#pragma unroll
-  for (int s4 = 0; s4 < 4; ++s4) vb[s4] = lds0 + TILE_BYTES + l32 * 128 + (((2 * s4 + h) ^ ((l32 >> 1) & 7)) << 4);
-
-  V14State st;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) st.O[dt][i] = 0.f;
-  st.lsum = 0.f;
-  st.negm = 0.f;
-  using C0 = std::integral_constant<int, 0>;
-  using C1 = std::integral_constant<int, STAGE_BYTES>;
-  stage(0, 0);
-  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (1 < nkb) stage(1, 1);
-  attn_v14_block<0, 0, true>(st, qf, ka, vb, 0, kv_len, h);
-  for (int kb = 1; kb < nkb; kb += 2) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kb + 1 < nkb) stage(kb + 1, 0);
-    attn_v14_block<STAGE_BYTES, STAGE_BYTES, false>(st, qf, ka, vb, kb, kv_len, h);
-    if (kb + 1 >= nkb) break;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kb + 2 < nkb) stage(kb + 2, 1);
-    attn_v14_block<0, 0, false>(st, qf, ka, vb, kb + 1, kv_len, h);
-  }
-  (void)C0{};
-  (void)C1{};
-  // the query's row sum from the two lane halves; O^T rows to 16-byte stores as kernel 4's epilogue
-  const auto xs = __builtin_amdgcn_permlane32_swap(__float_as_uint(st.lsum), __float_as_uint(st.lsum), false, false);
-  const float inv = 1.0f / (__uint_as_float(xs[0]) + __uint_as_float(xs[1]));
-  const int qi = qb * QBW + wave * 32 + l32;
-  const int qrow = q_row0 + min(qi, q_len - 1);
-  const int orow = a.orows ? a.orows[qrow] : qrow;
-  bf16* op = a.o + (long)orow * a.os + hd * D + 8 * h;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const f32x16& O = st.O[dt];
-      const bf16x4 pa = {f2bf(O[8 * m] * inv), f2bf(O[8 * m + 1] * inv), f2bf(O[8 * m + 2] * inv),
-                         f2bf(O[8 * m + 3] * inv)};
-      const bf16x4 pc = {f2bf(O[8 * m + 4] * inv), f2bf(O[8 * m + 5] * inv), f2bf(O[8 * m + 6] * inv),
-                         f2bf(O[8 * m + 7] * inv)};
-      const u32x2 ga = __builtin_bit_cast(u32x2, pa), gc = __builtin_bit_cast(u32x2, pc);
-      const auto rx = __builtin_amdgcn_permlane32_swap(ga[0], gc[0], false, false);
-      const auto ry = __builtin_amdgcn_permlane32_swap(ga[1], gc[1], false, false);
-      u32x4 out = {rx[0], ry[0], rx[1], ry[1]};
-      bf16* p = op + dt * 32 + 16 * m;
-      if (a.accumulate) {
-        const bf16x8 ov = *(const bf16x8*)p;
-        bf16x8 nv = __builtin_bit_cast(bf16x8, out);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) nv[j] = f2bf(bf2f(ov[j]) + bf2f(nv[j]));
-        out = __builtin_bit_cast(u32x4, nv);
-      }
-      if (qi < q_len) *(u32x4*)p = out;
-    }
-}
-
 // ---- v13: the v6t block (V^T in P's order) as a two-phase ping-pong between the two waves of each SIMD.  In v6/v6t
 // the 8 waves pass one barrier per block together, so the two waves of a SIMD run QK^T, softmax and PV in step and
 // the matrix pipe idles through both softmaxes (at 3 140 cycles per block per SIMD against 2 176 of MFMA work,
@@ -1865,371 +1605,6 @@ __device__ __forceinline__ void attn_fwd_pp_body(const AttnArgs& a) {
   }
 }
 
-// ---- v15 (kernel 8): v13's two-phase ping-pong on v14's 32x32x16 block.  With 16x16x32 MFMAs a streaming MFMA
-// wave holds its SIMD's vector issue for 8 of every 16 cycles, so the partner's softmax phase got about half the issue
-// slots and outlasted the MFMA phase (v13 at parity with v6t); a 32x32x16 MFMA holds issue for 8 of 32 cycles, so the
-// softmax phase (32 v_exp, 16 v_maximum3, 16 v_cvt_pk, the row sum) fits beside the other wave's 32 MFMAs (1 024
-// cycles) and each SIMD's matrix pipe stays busy.  Ring, DMA schedule and barriers are v13's; V^T in P16 order.
-struct V15Frags {
-  u32x4 a[4], b[4];
-};
-template <int KOFF>
-__device__ __forceinline__ void v15_read_k(u32x4* f, const uint32_t* ka, int s0) {
-  if (s0 == 0) {
-    ds_b128<KOFF>(f[0], ka[0]); ds_b128<KOFF>(f[1], ka[1]); ds_b128<KOFF>(f[2], ka[2]); ds_b128<KOFF>(f[3], ka[3]);
-  } else {
-    ds_b128<KOFF>(f[0], ka[4]); ds_b128<KOFF>(f[1], ka[5]); ds_b128<KOFF>(f[2], ka[6]); ds_b128<KOFF>(f[3], ka[7]);
-  }
-}
-__device__ __forceinline__ void v15_mma_k(f32x16& S, const u32x4* f, const bf16x8 (&qf)[8], int s0) {
-#pragma unroll
-  for (int s = 0; s < 4; ++s) S = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v6_as_bf8(f[s]), qf[s0 + s], S, 0, 0, 0);
-}
-// QK^T of the block in K stage KOFF (block 0, before the ping-pong starts)
-template <int KOFF>
-__device__ __forceinline__ void v15_qk(f32x16 (&S)[2], float negm, const bf16x8 (&qf)[8], const uint32_t* ka) {
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) S[kt][i] = negm;
-  u32x4 f0[4], f1[4];
-  v15_read_k<KOFF>(f0, ka, 0);
-  v15_read_k<KOFF>(f1, ka, 4);
-  wait_k4<4>(f0);
-  v15_mma_k(S[0], f0, qf, 0);
-  v15_read_k<KOFF + 8192>(f0, ka, 0);
-  wait_k4<4>(f1);
-  v15_mma_k(S[0], f1, qf, 4);
-  v15_read_k<KOFF + 8192>(f1, ka, 4);
-  wait_k4<4>(f0);
-  v15_mma_k(S[1], f0, qf, 0);
-  wait_k4<0>(f1);
-  v15_mma_k(S[1], f1, qf, 4);
-}
-// the softmax phase's operand prefetch: V^T of 16-key steps 0 and 1 (four d-tiles each) of the block in V stage VOFF
-template <int VOFF>
-__device__ __forceinline__ void v15_prefetch(V15Frags& fr, const uint32_t* vb) {
-  v12_read_v<VOFF, 0>(fr.a, vb);
-  v12_read_v<VOFF, 1>(fr.b, vb);
-}
-// the MFMA phase: PV of the softmaxed block (V stage VOFF), then QK^T of the next block (K stage KOFF)
-template <int VOFF, int KOFF>
-__device__ __forceinline__ void v15_mfma_phase(V14State& st, const bf16x8 (&pb)[4], const uint32_t* vb,
-                                               f32x16 (&S)[2], const bf16x8 (&qf)[8], const uint32_t* ka,
-                                               V15Frags& fr) {
-  wait_k4<0>(fr.b);  // (landed before the phase's barrier)
-  v12_mma_v(st.O, fr.a, pb[0]);
-  v12_read_v<VOFF, 2>(fr.a, vb);
-  v12_mma_v(st.O, fr.b, pb[1]);
-  v12_read_v<VOFF, 3>(fr.b, vb);
-  wait_k4<4>(fr.a);
-  v12_mma_v(st.O, fr.a, pb[2]);
-  v15_read_k<KOFF>(fr.a, ka, 0);
-  wait_k4<4>(fr.b);
-  v12_mma_v(st.O, fr.b, pb[3]);
-  v15_read_k<KOFF>(fr.b, ka, 4);
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) S[kt][i] = st.negm;
-  wait_k4<4>(fr.a);
-  v15_mma_k(S[0], fr.a, qf, 0);
-  v15_read_k<KOFF + 8192>(fr.a, ka, 0);
-  wait_k4<4>(fr.b);
-  v15_mma_k(S[0], fr.b, qf, 4);
-  v15_read_k<KOFF + 8192>(fr.b, ka, 4);
-  wait_k4<4>(fr.a);
-  v15_mma_k(S[1], fr.a, qf, 0);
-  wait_k4<0>(fr.b);
-  v15_mma_k(S[1], fr.b, qf, 4);
-}
-// the softmax phase of block kb (v14's): tail mask, rescale test / rescale, exponentials, P^T in bf16, row sums
-template <bool FIRST>
-__device__ __forceinline__ void v15_softmax(V14State& st, f32x16 (&S)[2], bf16x8 (&pb)[4], int kb, int kv_len, int hh) {
-  if (kb * KVB + KVB > kv_len) {
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if (kb * KVB + 32 * kt + 8 * (i / 4) + 4 * hh + (i % 4) >= kv_len) S[kt][i] = -INFINITY;
-  }
-  float r[12];
-#pragma unroll
-  for (int j = 0; j < 10; ++j) {
-    const int a0 = 3 * j, a1 = 3 * j + 1, a2 = 3 * j + 2;
-    r[j] = vmax3(S[a0 / 16][a0 % 16], S[a1 / 16][a1 % 16], S[a2 / 16][a2 % 16]);
-  }
-  r[10] = S[1][14];
-  r[11] = S[1][15];
-  const float lm = vmax2(vmax3(vmax3(r[0], r[1], r[2]), vmax3(r[3], r[4], r[5]), vmax3(r[6], r[7], r[8])),
-                         vmax3(r[9], r[10], r[11]));
-  if (FIRST || !__all(lm <= RESCALE_THR)) {  // wave-uniform
-    const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(lm), __float_as_uint(lm), false, false);
-    const float mx = vmax2(__uint_as_float(x[0]), __uint_as_float(x[1]));
-    const float delta = FIRST ? mx : fmaxf(mx, 0.f);
-    if (!FIRST) {
-      const float alpha = __builtin_amdgcn_exp2f(-delta);
-      st.lsum *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) st.O[dt][i] *= alpha;
-    }
-    st.negm -= delta;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) S[kt][i] -= delta;
-  }
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) S[kt][i] = __builtin_amdgcn_exp2f(S[kt][i]);
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) pb[s][j] = f2bf(S[s / 2][8 * (s % 2) + j]);
-  float t[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) t[j] = S[0][j] + S[1][j];
-#pragma unroll
-  for (int w = 8; w >= 1; w /= 2)
-#pragma unroll
-    for (int j = 0; j < w; ++j) t[j] += t[j + w];
-  st.lsum += t[0];
-}
-
-__device__ __forceinline__ void attn_fwd_pp32_body(const AttnArgs& a) {
-  constexpr int NW = 8, QBW = NW * 32, PPA = 4;  // the K / V DMA is issued by group A only: 4 pieces per wave
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nx = gridDim.x, ny = gridDim.y;
-  const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
-  const int qb = flat % nx, h = (flat / nx) % ny, seg = flat / (nx * ny);
-  const int* sg = a.segs + seg * 4;
-  const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
-  if (qb * QBW >= q_len) return;
-  const int tid = threadIdx.x, lane = tid & 63;
-  if (kv_len <= 0) {
-    if (!a.accumulate)
-      for (int i = tid; i < QBW * (D / 8); i += NW * 64) {
-        const int qi = qb * QBW + i / (D / 8);
-        if (qi < q_len) {
-          const int orow = a.orows ? a.orows[q_row0 + qi] : q_row0 + qi;
-          *(u32x4*)(a.o + (long)orow * a.os + h * D + (i % (D / 8)) * 8) = (u32x4){0u, 0u, 0u, 0u};
-        }
-      }
-    return;
-  }
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool grpB = wave >= 4;  // waves w and w + 4 share a SIMD
-  const int r16 = lane & 15, l32 = lane & 31, hh = lane >> 5;
-  bf16x8 qf[8];  // Q^T B operand of d-step s: lane = query l % 32, d 16 s + 8 hh .. + 7 (v14)
-  {
-    const int qc = min(qb * QBW + wave * 32 + l32, q_len - 1);
-    const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * hh;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      qf[s] = *(const bf16x8*)(qp + 16 * s);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[s][j] = f2bf(bf2f(qf[s][j]) * a.c);
-    }
-  }
-  const int nkb = (kv_len + KVB - 1) / KVB;
-  const long tail0 = (long)(nkb - 1) * KVB;
-  const bool ragged = kv_len % KVB != 0;
-  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.k + (long)kv_row0 * a.ks + h * D), (short)0, (int)(((long)kv_len - 1) * a.ks * 2 + 256), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rkt = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.k + (kv_row0 + tail0) * a.ks + h * D), (short)0, (int)((kv_len - tail0 - 1) * a.ks * 2 + 256),
-      0x00020000);
-  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.v + (long)h * D * a.vs + kv_row0), (short)0, (int)(((long)(D - 1) * a.vs + (long)nkb * KVB) * 2),
-      0x00020000);
-  const uint32_t lds_dma = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + (wave & 3) * PPA * 1024);
-  // the per-lane DMA offsets are recomputed at every staging from the lane id (v_mbcnt), not kept across the loop:
-  // kept, hipcc spills them at this register pressure, and each reload's vmcnt(0) would wait for every DMA piece in
-  // flight (serialising the ring)
-  const int ks2 = (int)a.ks * 2, vs2 = (int)a.vs * 2;
-  auto lane_id = [] {  // volatile: not hoisted out of the loop
-    int l;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-    return l;
-  };
-  // 3-stage ring (V13_LDS): K_j at slot * TILE_BYTES, V_j at V13_VBASE + slot * TILE_BYTES (K and V regions apart,
-  // so every ds_read offset from its region's read base stays below 64 KB)
-  auto stage_k = [&](int kb, int slot) {
-    const bool tail = ragged && kb == nkb - 1;
-    const int ks_off = tail ? 0 : kb * KVB * ks2;
-    const __amdgpu_buffer_rsrc_t bk = tail ? rkt : rk;
-    const int ln = lane_id();
-#pragma unroll
-    for (int i = 0; i < PPA; ++i) {
-      const int srow = ((wave & 3) * PPA + i) * 4 + (ln >> 4);
-      const int koff = srow * ks2 + (((ln & 15) ^ (srow & 15)) << 4);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(bk, LDS_PTR((uintptr_t)(lds_dma + slot * TILE_BYTES + i * 1024)), 16,
-                                               koff, ks_off, 0, 0);
-    }
-  };
-  auto stage_v = [&](int kb, int slot) {
-    const int ln = lane_id();
-#pragma unroll
-    for (int i = 0; i < PPA; ++i) {
-      const int d = ((wave & 3) * PPA + i) * 8 + (ln >> 3);
-      const int voff = d * vs2 + (((ln & 7) ^ ((d >> 1) & 7)) << 4);  // kernel 4's V^T image (32-row reads)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rv, LDS_PTR((uintptr_t)(lds_dma + V13_VBASE + slot * TILE_BYTES + i * 1024)), 16, voff, kb * KVB * 2, 0, 0);
-    }
-  };
-  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
-  uint32_t ka[8], vb[4];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) ka[s] = lds0 + l32 * 256 + (((2 * s + hh) ^ (l32 & 15)) << 4);
-#pragma unroll
-  for (int s4 = 0; s4 < 4; ++s4) vb[s4] = lds0 + V13_VBASE + l32 * 128 + (((2 * s4 + hh) ^ ((l32 >> 1) & 7)) << 4);
-
-  V14State st;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) st.O[dt][i] = 0.f;
-  st.lsum = 0.f;
-  st.negm = 0.f;
-  f32x16 S[2];
-  bf16x8 pb[4];
-
-  V15Frags fr;
-  // ring prologue: K_0, K_1, K_2, V_0 (K_j, V_j in slot j % 3)
-  if (!grpB) {
-    stage_k(0, 0);
-    stage_v(0, 0);
-    if (1 < nkb) stage_k(1, 1);
-  } else {
-    if (2 < nkb) stage_k(2, 2);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // Both groups run the same cyclic body [softmax_j + operand prefetch, PV_j + QK_{j+1}], group B one phase later:
-  // A's body opens with barrier X_j, B's with Y_j (B's QK_0 precedes it in phase X_0), so each SIMD pairs one wave's
-  // softmax with the other's MFMAs.  The K / V DMA rides in the softmax phases, after the softmax (that wave then
-  // waits at the barrier for its partner's MFMAs anyway; issued at the top of an MFMA phase by all eight waves the
-  // 32 pieces held each wave ~700 cycles): A issues V_{j+1} in X_j (into V_{j-2}'s slot, whose readers are done by
-  // X_j), landed before X_{j+1}, where A starts reading it; B issues K_{j+3} in Y_j (into K_j's slot, done by Y_j),
-  // landed before Y_{j+2}, ahead of its first reader (A's QK^T in Y_{j+2}).  4 pieces per wave per block each.
-  // Block 0 is peeled (its softmax sets the running max), so the loop bodies carry no first-block branch.
-#ifdef SA_V13_STAMPS
-  uint64_t acc[6] = {0, 0, 0, 0, 0, 0};
-#endif
-  auto body = [&](auto firstc, auto slotc, auto grpc, int j) {
-    constexpr bool FIRST = decltype(firstc)::value, GB = decltype(grpc)::value;
-    constexpr int SL = decltype(slotc)::value;
-    constexpr int KN = ((SL + 1) % 3) * TILE_BYTES, VO = SL * TILE_BYTES;
-    if constexpr (!GB) {
-      V13_STAMP(tw);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of V_j (issued in X_{j-1})
-      V13_STAMP(t0);
-      V13_ACC(4, t0 - tw);
-      v13_sync();  // X_j
-      V13_STAMP(t1);
-      v15_softmax<FIRST>(st, S, pb, j, kv_len, hh);
-      v15_prefetch<VO>(fr, vb);
-      V13_STAMP(t2s);
-      if (j + 1 < nkb) stage_v(j + 1, (SL + 1) % 3);
-      V13_STAMP(t2);
-      V13_ACC(5, t2 - t2s);
-      v13_sync();  // Y_j
-      V13_STAMP(t3);
-      V13_ACC(0, t1 - t0); V13_ACC(1, t2 - t1); V13_ACC(2, t3 - t2);
-    } else {
-      // this wave's pieces of K_{j+1} (issued in Y_{j-2}) landed; those of K_{j+2} (Y_{j-1}) may fly
-      V13_STAMP(tw);
-      if (j + 2 < nkb)
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      V13_STAMP(t0);
-      V13_ACC(4, t0 - tw);
-      v13_sync();  // Y_j
-      V13_STAMP(t1);
-      v15_softmax<FIRST>(st, S, pb, j, kv_len, hh);
-      v15_prefetch<VO>(fr, vb);
-      if (j + 3 < nkb) stage_k(j + 3, SL);
-      V13_STAMP(t2);
-      if (j + 1 < nkb) v13_sync();  // X_{j+1}
-      V13_STAMP(t3);
-      V13_ACC(0, t1 - t0); V13_ACC(1, t2 - t1); V13_ACC(2, t3 - t2);
-    }
-    // V_j, K_{j+1} (after the last block a QK^T of a stale slot, unused: no branch in the body)
-#ifdef SA_V13_STAMPS
-    const uint64_t t4 = v13_now();
-#endif
-    // the MFMA phase's wave first at the issue arbiter, the softmax wave in its gaps (6.31 / 6.29 vs 6.41 / 6.44 ms
-    // with B's static priority alone, profiles/r05/attn_ab_v13_variants_r5u_r5v.jsonl)
-    __builtin_amdgcn_s_setprio(2);
-    v15_mfma_phase<VO, KN>(st, pb, vb, S, qf, ka, fr);
-    __builtin_amdgcn_s_setprio(GB ? 1 : 0);
-#ifdef SA_V13_STAMPS
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    acc[3] += v13_now() - t4;
-#endif
-  };
-  const auto S0 = std::integral_constant<int, 0>{};
-  const auto S1 = std::integral_constant<int, 1>{};
-  const auto S2 = std::integral_constant<int, 2>{};
-  auto run = [&](auto grpc) {
-    body(std::true_type{}, S0, grpc, 0);
-    for (int j = 1; j < nkb; j += 3) {
-      body(std::false_type{}, S1, grpc, j);
-      if (j + 1 >= nkb) break;
-      body(std::false_type{}, S2, grpc, j + 1);
-      if (j + 2 >= nkb) break;
-      body(std::false_type{}, S0, grpc, j + 2);
-    }
-  };
-  if (!grpB) {
-    v15_qk<0>(S, st.negm, qf, ka);  // QK^T of block 0 before X_0
-    run(std::false_type{});
-  } else {
-    __builtin_amdgcn_s_setprio(1);
-    v13_sync();  // X_0
-    v15_qk<0>(S, st.negm, qf, ka);
-    run(std::true_type{});
-  }
-#ifdef SA_V13_STAMPS
-  if (lane == 0)
-    for (int k = 0; k < 6; ++k) atomicAdd(&g_v13_stamps[(grpB ? 6 : 0) + k], (unsigned long long)acc[k]);
-#endif
-
-  const auto xs = __builtin_amdgcn_permlane32_swap(__float_as_uint(st.lsum), __float_as_uint(st.lsum), false, false);
-  const float inv = 1.0f / (__uint_as_float(xs[0]) + __uint_as_float(xs[1]));
-  const int qi = qb * QBW + wave * 32 + l32;
-  const int qrow = q_row0 + min(qi, q_len - 1);
-  const int orow = a.orows ? a.orows[qrow] : qrow;
-  bf16* op = a.o + (long)orow * a.os + h * D + 8 * hh;
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const f32x16& O = st.O[dt];
-      const bf16x4 pa = {f2bf(O[8 * m] * inv), f2bf(O[8 * m + 1] * inv), f2bf(O[8 * m + 2] * inv),
-                         f2bf(O[8 * m + 3] * inv)};
-      const bf16x4 pc = {f2bf(O[8 * m + 4] * inv), f2bf(O[8 * m + 5] * inv), f2bf(O[8 * m + 6] * inv),
-                         f2bf(O[8 * m + 7] * inv)};
-      const u32x2 ga = __builtin_bit_cast(u32x2, pa), gc = __builtin_bit_cast(u32x2, pc);
-      const auto rx = __builtin_amdgcn_permlane32_swap(ga[0], gc[0], false, false);
-      const auto ry = __builtin_amdgcn_permlane32_swap(ga[1], gc[1], false, false);
-      u32x4 out = {rx[0], ry[0], rx[1], ry[1]};
-      bf16* p = op + dt * 32 + 16 * m;
-      if (a.accumulate) {
-        const bf16x8 ov = *(const bf16x8*)p;
-        bf16x8 nv = __builtin_bit_cast(bf16x8, out);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) nv[j] = f2bf(bf2f(ov[j]) + bf2f(nv[j]));
-        out = __builtin_bit_cast(u32x4, nv);
-      }
-      if (qi < q_len) *(u32x4*)p = out;
-    }
-}
-
 // the fused cross-attention on the self-attention block body: 8 waves x 32 queries of one query block,
 // the text, image and per-frame vocal K/V streams one after the other through 3-stage K / V regions (each
 // block's DMA two blocks ahead), a separate online softmax per source (its first block sets the max), the
@@ -2470,8 +1845,6 @@ __global__ __launch_bounds__(512) void attn_fwd_v6t_kernel(AttnArgs a) { attn_fw
 __global__ __launch_bounds__(512) void attn_fwd_v12_kernel(AttnArgs a) { attn_fwd_vt_body<2>(a); }
 __global__ __launch_bounds__(512) void attn_fwd_v13_kernel(AttnArgs a) { attn_fwd_pp_body(a); }
 __global__ __launch_bounds__(512) void attn_fwd_v6t3_kernel(AttnArgs a) { attn_fwd_vt_body<1, 3>(a); }
-__global__ __launch_bounds__(512) void attn_fwd_v14_kernel(AttnArgs a) { attn_fwd_v14_body(a); }
-__global__ __launch_bounds__(512) void attn_fwd_v15_kernel(AttnArgs a) { attn_fwd_pp32_body(a); }
 
 }  // namespace
 
@@ -2491,7 +1864,7 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
   if (head_dim != D) return SA_ERR_ARG;
   if ((q_stride | k_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
   if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)o)) & 15) return SA_ERR_ARG;
-  if (kernel < 0 || kernel > 8) return SA_ERR_ARG;
+  if (kernel < 0 || kernel > 6) return SA_ERR_ARG;
   if (kernel >= 3 && (v_stride % 64 || (((uintptr_t)v) & 127))) return SA_ERR_ARG;  // V^T rows: whole 64-key blocks
   static const bool attr = [] {  // one-time, thread-safe
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
@@ -2502,8 +1875,6 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
     (void)hipFuncSetAttribute((const void*)attn_fwd_v13_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, V13_LDS);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6t3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               3 * STAGE_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_v14_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_v15_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, V13_LDS);
     return true;
   }();
   (void)attr;
@@ -2533,10 +1904,6 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
       hipLaunchKernelGGL(attn_fwd_v12_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
     else if (kernel == 6)
       hipLaunchKernelGGL(attn_fwd_v6t3_kernel, grid, dim3(512), 3 * STAGE_BYTES, (hipStream_t)stream, a);
-    else if (kernel == 7)
-      hipLaunchKernelGGL(attn_fwd_v14_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
-    else if (kernel == 8)
-      hipLaunchKernelGGL(attn_fwd_v15_kernel, grid, dim3(512), V13_LDS, (hipStream_t)stream, a);
     else
       hipLaunchKernelGGL(attn_fwd_v13_kernel, grid, dim3(512), V13_LDS, (hipStream_t)stream, a);
   } else {

@@ -37,10 +37,6 @@ def vt_layout(v, mode, rows_pad=64):
         perm = torch.where(p % 8 < 4, 4 * (p // 8) + p % 8, 16 + 4 * (p // 8) + p % 8 - 4)
         idx = (torch.arange(Rv, device=v.device) // 32) * 32 + perm[torch.arange(Rv, device=v.device) % 32]
         vt = vt[:, idx].contiguous()
-    elif mode == 7:  # kernels 7/8's P16 order: per 16 keys, positions 4-7 <- keys 8-11 and 8-11 <- keys 4-7
-        perm = torch.tensor([0, 1, 2, 3, 8, 9, 10, 11, 4, 5, 6, 7, 12, 13, 14, 15], device=v.device)
-        idx = (torch.arange(Rv, device=v.device) // 16) * 16 + perm[torch.arange(Rv, device=v.device) % 16]
-        vt = vt[:, idx].contiguous()
     return vt
 
 
@@ -116,7 +112,7 @@ def main(which=("gemm", "attn")):
         q, k, v_ = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
         outs = {}
         variants = tuple(int(v) for v in os.environ.get("SA_KB_AVARS", "1").split(","))
-        vts = {m: vt_layout(v_, {5: 3, 6: 3, 8: 7}.get(m, m)) for m in (3, 4, 5, 6, 7, 8) if m in variants}  # kernels 3-8: V^T
+        vts = {m: vt_layout(v_, 3 if m in (5, 6) else m) for m in (3, 4, 5, 6) if m in variants}  # kernels 3-6 read V^T
         times = {v: [] for v in variants}
         for rnd in range(3):
             for v in variants:
