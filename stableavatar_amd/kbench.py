@@ -138,6 +138,8 @@ def main(which=("gemm", "attn")):
             r[f"v{v}_tflops"] = round(fl / ms / 1e9, 1)
         res.append(r)
         print(json.dumps(r), flush=True)
+    if "attnclip" in which:
+        res.extend(attn_clip_inputs())
     if "cross3" in which:  # the fused text + image + per-frame vocal cross-attention at config 2
         L, H, D, B, nper, nfr = 21504, 12, 128, 3, 32, 21
         q = torch.randn(B * L, H * D, device=dev).bfloat16()
@@ -323,7 +325,56 @@ def bench_dit14(layer_counts=(1, 2)):
             "tflops_forward_projected": round(fl_fwd / fwd40 / 1e9, 1)}
 
 
-def bench_dit(iters=3, attn_variants=None, env_variants=None):
+def attn_clip_inputs(layers=(0, 15, 29)):
+    """The self-attention launches' operands of one config-2 DiT forward (random-init weights, bench_dit's
+    inputs) against random operands of the same shapes: per captured layer, the launch time with q/k and V^T each
+    from the forward or from randn (2 x 2), so a difference splits into the scores' side (rescale frequency) and
+    the data's side (switching power)."""
+    from . import ops as _ops
+    captured, calls = [], [0]
+    real = _ops.attention
+
+    def spy(q, k, v, o, segs, B, L, H, **kw):
+        if kw.get("kernel") == _ops.ATTN_VT_P32:
+            if calls[0] in layers:
+                captured.append((calls[0], q.clone(), k.clone(), v.clone(), segs.clone(), B, L, H))
+            calls[0] += 1
+        return real(q, k, v, o, segs, B, L, H, **kw)
+    fwd = bench_dit(fwd_only=True)
+    _ops.attention = spy
+    try:
+        with torch.no_grad():
+            fwd()
+    finally:
+        _ops.attention = real
+    torch.cuda.synchronize()
+    out = []
+    for (li, q, k, vt, segs, B, L, H) in captured:
+        qr, kr = torch.randn_like(q.float()).bfloat16(), torch.randn_like(k.float()).bfloat16()
+        vr = torch.randn_like(vt.float()).bfloat16()
+        o = torch.empty(B * L, H * 128, device=q.device, dtype=torch.bfloat16)
+        combos = {"qk_clip_v_clip": (q, k, vt), "qk_rand_v_clip": (qr, kr, vt), "qk_clip_v_rand": (q, k, vr),
+                  "qk_rand_v_rand": (qr, kr, vr)}
+        times = {c: [] for c in combos}
+        for _ in range(3):
+            for c, (a, b_, v) in combos.items():
+                times[c].append(_time(lambda: real(a, b_, v, o, segs, B, L, H, kernel=_ops.ATTN_VT_P32), iters=3,
+                                      warmup=1))
+        # scaled score statistics on a sample of rows (head 0, batch row 0): spread of the row max, log2 units
+        qs = q[:L:997, :128].float()
+        sc = qs @ k[:L, :128].float().t() * (128 ** -0.5) * 1.4426950408889634
+        r = {"kernel": "attn_clip_inputs", "layer": li, "q_rms": round(q.float().pow(2).mean().sqrt().item(), 3),
+             "k_rms": round(k.float().pow(2).mean().sqrt().item(), 3),
+             "row_max_log2_mean": round(sc.max(1).values.mean().item(), 2),
+             "score_std_log2": round(sc.std().item(), 2)}
+        for c in combos:
+            r[f"{c}_ms"] = round(sorted(times[c])[1], 3)
+        out.append(r)
+        print(json.dumps(r), flush=True)
+    return out
+
+
+def bench_dit(iters=3, attn_variants=None, env_variants=None, fwd_only=False):
     """One full 30-layer DiT forward at config 2 (B=3 CFG, 21 latent frames at 64x64, L=21504).
     attn_variants: time the forward under each self-attention schedule, interleaved rounds."""
     from . import synthetic
@@ -345,6 +396,8 @@ def bench_dit(iters=3, attn_variants=None, env_variants=None):
     def fwd():
         return m.forward_window(lat, 0, True, 3, t, ctx, 21504, clip, y, voc, 81)
 
+    if fwd_only:
+        return fwd
     from .flops import dit_forward_flops
     fl = dit_forward_flops()
     if env_variants:  # "K=V" settings of one environment switch read per call by the library, interleaved
