@@ -77,6 +77,17 @@ __device__ __forceinline__ int swz128(int r, int c) { return r * 128 + ((c ^ ((r
 // buffer-store cache-policy bits, gfx950: 1 sc0, 2 nt, 16 sc1).  -1 (default): bf16 rows non-temporal, fp32 plain.
 // sc1 stores leave no copy in the XCD's L2 (MI355X_MICROARCH.md store table), so a tile's output burst does not
 // evict the K-slices the XCD's other tiles are still reading.
+// measurement builds only (scripts/build_variant.sh): 1 = the bf16 row epilogue forms its 16-byte values but does
+// not store them (the LDS-strip round trip and the conversion kept; outputs incomplete)
+#ifndef SA_EPI_EXP
+#define SA_EPI_EXP 0
+#endif
+// bf16 row epilogue of the persistent kernels: 1 = straight from the accumulators, two column groups' 4-column pieces
+// joined into 16-byte row pieces by v_permlane16_swap (s7_bf16_perm_epilogue), the tile's bias loaded at the top of
+// its K loop; 0 = the round-4 LDS-strip transposition (also the fallback for a partial last column tile)
+#ifndef SA_EPI_V2
+#define SA_EPI_V2 1
+#endif
 #ifndef SA_STORE_POLICY
 #define SA_STORE_POLICY -1
 #endif
@@ -137,7 +148,9 @@ __device__ __forceinline__ void epi_row(const GemmArgs& g, float* v, long bz, in
           // non-temporal 16-byte stores (global_store ... nt): the epilogue's store burst drains faster
           // (isolated: cross-Q 0.238 vs 0.286 ms, QKV 0.833 vs 0.873, FFN-up 1.535 vs 1.632; in the
           // 30-layer forward 0.4-0.8 % -- the consumers then read more of it from HBM; profiles/r03 r3n)
-          if constexpr (SA_STORE_POLICY < 0)
+          if constexpr (SA_EPI_EXP == 1)  // measurement build: the value is formed, not stored
+            asm volatile("" ::"v"(__builtin_bit_cast(u32x4, o)));
+          else if constexpr (SA_STORE_POLICY < 0)
             __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), (u32x4*)(C + 8 * h));
           else
             store16((bf16*)g.C + bz * g.sC, (long)grow * g.ldc + gcol + 8 * h, __builtin_bit_cast(u32x4, o));
@@ -820,6 +833,97 @@ __device__ __forceinline__ void s7_tile(const GemmArgs& g, int u, int total, int
                                          (int)(rows_w * g.ldw * 2), 0x00020000);
 }
 
+// The bf16 row epilogue's bias for tile column n0 (lane (fr, fc) of wave column wn: columns n0 + wn*128 + J*16 +
+// 4 fc + 0..3 for J = 0..7), issued at the top of the tile's K loop by inline-asm buffer loads.  The compiler does
+// not track these loads, so it places no wait for them: the first K step's counted vmcnt (which retires every VMEM
+// op older than that step's own DMA) does, and the caller marks the registers defined after it.  A compiler-visible
+// load here or in the epilogue gets a vmcnt(0), i.e. waits behind the next tile's DMA in flight.  Returns false
+// (nothing loaded: the LDS-strip epilogue runs, with its own loads) for a wave whose 128 columns pass N.
+__device__ __forceinline__ bool s8_bias_preload(const GemmArgs& g, f32x4 (&b)[8], int n0, int wn, int lane) {
+  if (n0 + wn * 128 + 128 > g.N) return false;  // wave-uniform
+  if (!g.bias) {                                 // wave-uniform
+#pragma unroll
+    for (int J = 0; J < 8; ++J) b[J] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    return true;
+  }
+  const uintptr_t base = (uintptr_t)g.bias;
+  const u32x4 rs = {(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)base),
+                    (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(base >> 32)),
+                    (unsigned)__builtin_amdgcn_readfirstlane(g.N * 4), 0x00020000u};
+  const int c0 = n0 + wn * 128 + 4 * ((lane >> 4) & 3);
+#pragma unroll
+  for (int J = 0; J < 8; ++J)
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(b[J]) : "v"((c0 + J * 16) * 4), "s"(rs));
+  return true;
+}
+
+// 4 outputs of a bf16 row epilogue (bias already added), packed: the Linear's bf16 rounding, then the activation
+// (epi_row's order and arithmetic, so the outputs are bit-identical to the strip path's)
+template <int EPI>
+__device__ __forceinline__ u32x2 s7_pack4(f32x4 v) {
+  if constexpr (EPI == EPI_GELU_BF16) {
+    const f32x2 y0 = gelu_tanh2(__builtin_convertvector(__builtin_convertvector((f32x2){v[0], v[1]}, bf16x2), f32x2));
+    const f32x2 y1 = gelu_tanh2(__builtin_convertvector(__builtin_convertvector((f32x2){v[2], v[3]}, bf16x2), f32x2));
+    v = (f32x4){y0[0], y0[1], y1[0], y1[1]};
+  } else if constexpr (EPI == EPI_GELU_ERF_BF16) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = gelu_erf(bf2f(f2bf(v[e])));
+  }
+  return __builtin_bit_cast(u32x2, (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])});
+}
+
+// bf16 row epilogue straight from the accumulators (interior columns; rows past M not stored).  Lane (fr, fc) holds in
+// acc[i][J] row m0 + wm*16*MI + i*16 + fr, columns n0 + wn*128 + J*16 + 4 fc + 0..3.  For a column-group pair (J, J+1)
+// two v_permlane16_swap (lanes l <-> l ^ 16, i.e. fc ^ 1) give lane fc = 0 / 2 columns J*16 + 0..7 / 8..15 and lane
+// fc = 1 / 3 columns (J+1)*16 + 0..7 / 8..15: one non-temporal 16-byte store per lane, 64 contiguous bytes per row per
+// instruction, 32 stores per wave per tile (the strip path's count) and no LDS round trip.  The strip path moved
+// 512 KB of fp32 through the LDS per tile (~11 k cycles at the config-2 QKV shape; profiles/r05 gemm stamps).
+template <int EPI, int MI>
+__device__ __forceinline__ void s7_bf16_perm_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8], const f32x4 (&bj)[8],
+                                                      int wm, int wn, int fr, int fc, int m0, int n0, long bz) {
+  const int row0 = m0 + wm * 16 * MI + fr;
+  bf16* const C = (bf16*)g.C + bz * g.sC + n0 + wn * 128 + (fc & 1) * 16 + (fc >> 1) * 8;
+#pragma unroll
+  for (int J = 0; J < 8; J += 2) {
+    if constexpr (MI == 8)
+      asm volatile("" : "+a"(acc[0][J]), "+a"(acc[1][J]), "+a"(acc[2][J]), "+a"(acc[3][J]), "+a"(acc[4][J]),
+                        "+a"(acc[5][J]), "+a"(acc[6][J]), "+a"(acc[7][J]), "+a"(acc[0][J + 1]), "+a"(acc[1][J + 1]),
+                        "+a"(acc[2][J + 1]), "+a"(acc[3][J + 1]), "+a"(acc[4][J + 1]), "+a"(acc[5][J + 1]),
+                        "+a"(acc[6][J + 1]), "+a"(acc[7][J + 1])::"memory");
+    else
+      asm volatile("" : "+a"(acc[0][J]), "+a"(acc[1][J]), "+a"(acc[2][J]), "+a"(acc[3][J]), "+a"(acc[4][J]),
+                        "+a"(acc[5][J]), "+a"(acc[0][J + 1]), "+a"(acc[1][J + 1]), "+a"(acc[2][J + 1]),
+                        "+a"(acc[3][J + 1]), "+a"(acc[4][J + 1]), "+a"(acc[5][J + 1])::"memory");
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const f32x4 a = acc[i][J], b = acc[i][J + 1];
+      const u32x2 x = s7_pack4<EPI>((f32x4){a[0] + bj[J][0], a[1] + bj[J][1], a[2] + bj[J][2], a[3] + bj[J][3]});
+      const u32x2 y = s7_pack4<EPI>(
+          (f32x4){b[0] + bj[J + 1][0], b[1] + bj[J + 1][1], b[2] + bj[J + 1][2], b[3] + bj[J + 1][3]});
+      const auto r0 = __builtin_amdgcn_permlane16_swap(x[0], y[0], false, false);
+      const auto r1 = __builtin_amdgcn_permlane16_swap(x[1], y[1], false, false);
+      const u32x4 out = {r0[0], r1[0], r0[1], r1[1]};
+      const int row = row0 + i * 16;
+      if (row < g.M) __builtin_nontemporal_store(out, (u32x4*)(C + (long)row * g.ldc + J * 16));
+    }
+  }
+}
+
+#ifdef SA_GEMM_STAMPS
+// measurement builds only (scripts/build_variant.sh NAME -DSA_GEMM_STAMPS): summed s_memtime cycles over every wave
+// of the persistent kernel's launches: [0] first K-step pair of each tile, [1] the rest of the K loop, [2] the
+// epilogue, [3] tiles (per wave), [4] the epilogue's bias / setup part (to the first strip write)
+__device__ unsigned long long g_gemm_stamps[8];
+__device__ __forceinline__ uint64_t gemm_now() {
+  const uint64_t t = __builtin_amdgcn_s_memtime();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  return t;
+}
+#define GEMM_STAMP(x) const uint64_t x = gemm_now()
+#else
+#define GEMM_STAMP(x)
+#endif
+
 // ------------------------------------------------------------------------------------------------
 // s8 kernel: s7's persistence (tile walk u = blockIdx.x + k*gridDim.x, K pipeline running across tile
 // seams, epilogue from a private strip above the ring) on the spread-DMA feed of variant 14: in the
@@ -1011,13 +1115,22 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
   s5_read<0, 0, 12, MI>(c, a0, b0); s5_read<0, 0, 13, MI>(c, a0, b0); s5_read<0, 0, 14, MI>(c, a0, b0);
   s5_read<0, 0, 15, MI>(c, a0, b0);
 
+  // the bf16 row epilogues' bias, loaded at the top of each tile (SA_EPI_V2)
+  constexpr bool BPRE = SA_EPI_V2 && !NOEPI && !TR && (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16);
+  f32x4 bpre[8];
+  bool pre = false;
+#ifdef SA_GEMM_STAMPS
+  uint64_t sacc[4] = {0, 0, 0, 0};
+#endif
   while (true) {
+    GEMM_STAMP(ta);
     const int un = u + G;
     const bool has_next = un < total;
     __amdgpu_buffer_rsrc_t cra = c.ra, crw = c.rw, nra = c.ra, nrw = c.rw;
     int nm0 = m0, nn0 = n0;
     long nbz = bz;
     if (has_next) s7_tile<MI>(g, un, total, G, nm, nn, nm0, nn0, nbz, nra, nrw);
+    if constexpr (BPRE) pre = s8_bias_preload(g, bpre, n0, wn, lane);
     for (int t = 0; t < nk; t += 2) {
       {
         const bool nx = t + 2 >= nk;  // DMA of the next tile's K-tile t+2-nk (or a re-read of the last)
@@ -1028,7 +1141,18 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
           s9_step<0, PANEL, MI, TR>(g, c, acc, a0, b0, a1, b1, ksd);
         else
           s8_step<0, PANEL, MI, TR>(g, c, acc, a0, b0, a1, b1, ksd);
+        if constexpr (BPRE) {  // the bias registers are defined here: the step's counted wait has retired their loads
+          if (t == 0)
+            asm volatile("" : "+v"(bpre[0]), "+v"(bpre[1]), "+v"(bpre[2]), "+v"(bpre[3]), "+v"(bpre[4]), "+v"(bpre[5]),
+                         "+v"(bpre[6]), "+v"(bpre[7]));
+        }
       }
+#ifdef SA_GEMM_STAMPS
+      if (t == 0) {
+        GEMM_STAMP(tf);
+        sacc[0] += tf - ta;
+      }
+#endif
       {
         const bool nx = t + 3 >= nk;
         c.ra = nx ? nra : cra;
@@ -1041,7 +1165,21 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
       }
     }
     asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // MFMA -> v_accvgpr_read
-    if constexpr (!NOEPI) s7_epilogue<EPI, MI>(g, acc, smem, wave, lane, m0, n0, bz);
+    GEMM_STAMP(tb);
+    if constexpr (BPRE) {
+      if (pre)  // two paths: a join would merge the strip path's load waits into this one
+        s7_bf16_perm_epilogue<EPI, MI>(g, acc, bpre, wm, wn, lane & 15, lane >> 4, m0, n0, bz);
+      else
+        s7_epilogue<EPI, MI>(g, acc, smem, wave, lane, m0, n0, bz);
+    } else if constexpr (!NOEPI) {
+      s7_epilogue<EPI, MI>(g, acc, smem, wave, lane, m0, n0, bz);
+    }
+#ifdef SA_GEMM_STAMPS
+    GEMM_STAMP(tc);
+    sacc[1] += tb - ta;
+    sacc[2] += tc - tb;
+    sacc[3] += 1;
+#endif
     if (!has_next) break;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -1055,6 +1193,14 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
     c.rw = nrw;
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#ifdef SA_GEMM_STAMPS
+  if (lane == 0) {
+    atomicAdd(&g_gemm_stamps[0], (unsigned long long)sacc[0]);
+    atomicAdd(&g_gemm_stamps[1], (unsigned long long)(sacc[1] - sacc[0]));
+    atomicAdd(&g_gemm_stamps[2], (unsigned long long)sacc[2]);
+    atomicAdd(&g_gemm_stamps[3], (unsigned long long)sacc[3]);
+  }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1640,3 +1786,14 @@ extern "C" int sa_gemm_bf16(const void* A, int64_t lda, int64_t strideA, const v
   return sa_gemm_bf16_ex(A, lda, strideA, W, ldw, strideW, bias, C, ldc, strideC, M, N, K, batch, epilogue, residual,
                          ldr, strideR, gate, gate_bstride, rows_per_batch, KERNEL_AUTO, 0, stream);
 }
+
+#ifdef SA_GEMM_STAMPS
+extern "C" int sa_debug_gemm_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gemm_stamps), sizeof(unsigned long long) * 8) != hipSuccess) return SA_ERR_ARG;
+  if (reset) {
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_stamps), z, sizeof(z)) != hipSuccess) return SA_ERR_ARG;
+  }
+  return SA_OK;
+}
+#endif

@@ -86,7 +86,7 @@ def main(which=("gemm", "attn")):
                     o = out.float()
                     if ref is None:
                         ref = o.clone()
-                    if int(vv) >= 8:  # the no-epilogue measurement kernels write nothing
+                    if int(vv) >= 8 or os.environ.get("SA_KB_NOCHECK"):  # measurement kernels / builds
                         continue
                     err = ((o - ref).norm() / ref.norm()).item()
                     assert err < 1e-2, (name, v, err)
