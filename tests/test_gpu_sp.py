@@ -9,7 +9,6 @@ per-row Q/K/V exchanges with one batched attention; every CFG row through the wh
 (two RCCL ranks cannot share a device), so the RCCL tests run at degree 1 with loopback transfers (each rank's own
 chunk sent to itself): every send / receive, stream wait and all-gather of the exchange executes on RCCL."""
 import os
-import socket
 import sys
 
 import numpy as np
@@ -27,11 +26,10 @@ pytestmark = pytest.mark.gpu
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+    """a fresh rendezvous file for the process group (file:// init: no TCP port to race for -- a port picked free and
+    released can be taken before the store listens on it, EADDRINUSE)"""
+    import tempfile
+    return os.path.join(tempfile.mkdtemp(prefix="sa_rdv_"), "store")
 
 
 def _stats(out, ref):
@@ -41,10 +39,9 @@ def _stats(out, ref):
 
 def _worker(rank, world, port, model, qret):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
     sys.path.insert(0, HERE)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         res = []
         if model == "1.3B":
@@ -125,7 +122,7 @@ def _rccl_worker(port, overlap, qret):
     from test_gpu_dit import make_model, run
     from golden_cases import DIT_SMALL, dit_inputs
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+    dist.init_process_group("nccl", init_method="file://" + port, rank=0, world_size=1,
                             device_id=torch.device("cuda:0"))
     try:
         m = make_model(DIT_SMALL)
@@ -174,7 +171,7 @@ def _rccl_fullsize_worker(port, overlap, qret):
     from stableavatar_amd import synthetic
     from stableavatar_amd.transformer import WanTransformer3DFantasyModel, param_shapes
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+    dist.init_process_group("nccl", init_method="file://" + port, rank=0, world_size=1,
                             device_id=torch.device("cuda:0"))
     try:
         dev = "cuda"
@@ -235,7 +232,7 @@ def _rccl_dp_vae_worker(port, qret):
     import torch.distributed as dist
     sys.path.insert(0, HERE)
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+    dist.init_process_group("nccl", init_method="file://" + port, rank=0, world_size=1,
                             device_id=torch.device("cuda:0"))
     try:
         from golden_cases import PIPE

@@ -4,7 +4,6 @@ latent frames, receiving every causal conv's 2-frame cache from rank r-1 and pas
 (gloo, host-staged P2P) must reproduce the single-GPU decode BIT-EXACTLY, including per-rank runs split
 into sub-chunks (chunk 2) and a first run of a single latent frame (3 ranks over 4 frames)."""
 import os
-import socket
 import sys
 
 import pytest
@@ -21,20 +20,18 @@ pytestmark = pytest.mark.gpu
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+    """a fresh rendezvous file for the process group (file:// init: no TCP port to race for -- a port picked free and
+    released can be taken before the store listens on it, EADDRINUSE)"""
+    import tempfile
+    return os.path.join(tempfile.mkdtemp(prefix="sa_rdv_"), "store")
 
 
 def _worker(rank, world, port, T, chunk, qret):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
     from stableavatar_amd import synthetic
     from stableavatar_amd.vae import AutoencoderKLWan, encoder_param_shapes, param_shapes
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         v = AutoencoderKLWan(dim=32)
         v.load_state_dict(synthetic.fill_state_dict(dict(param_shapes(dim=32), **encoder_param_shapes(dim=32)), 24))

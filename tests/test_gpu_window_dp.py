@@ -7,7 +7,6 @@ reference's __call__ goldens) at the pipeline tolerance (latents rel-L2 <= 3e-2)
 (53 latent frames) is config 5's rank count, also against the oracle loop."""
 import math
 import os
-import socket
 import sys
 
 import pytest
@@ -26,11 +25,10 @@ STEPS = 3
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+    """a fresh rendezvous file for the process group (file:// init: no TCP port to race for -- a port picked free and
+    released can be taken before the store listens on it, EADDRINUSE)"""
+    import tempfile
+    return os.path.join(tempfile.mkdtemp(prefix="sa_rdv_"), "store")
 
 
 def _inputs(T):
@@ -74,13 +72,12 @@ def _run(pipe, T, window_parallel):
 
 def _worker(rank, world, port, T, qret):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
     from golden_cases import PIPE
     from stableavatar_amd import synthetic
     from stableavatar_amd.pipeline import WanI2VTalkingInferenceLongPipeline
     from stableavatar_amd.transformer import WanTransformer3DFantasyModel, param_shapes
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         dcfg = PIPE["dit"]
         dit = WanTransformer3DFantasyModel(**{k: v for k, v in dcfg.items() if k != "seed"})

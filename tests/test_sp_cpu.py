@@ -5,7 +5,6 @@ over the token-sharded, head-exchanged layout equals single-device full attentio
 plus the single-GPU frame grouping of the per-frame vocal attention and the head all-gather.
 """
 import os
-import socket
 
 import pytest
 import torch
@@ -16,11 +15,10 @@ from stableavatar_amd import sp
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+    """a fresh rendezvous file for the process group (file:// init: no TCP port to race for -- a port picked free and
+    released can be taken before the store listens on it, EADDRINUSE)"""
+    import tempfile
+    return os.path.join(tempfile.mkdtemp(prefix="sa_rdv_"), "store")
 
 
 def _sdpa(q, k, v):
@@ -48,8 +46,7 @@ def _pack(ex, mine, plan):
 
 def _worker(rank, world, port, B, Lp, H, D, q_ret, loopback=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         g = torch.Generator().manual_seed(7)
         qkv = torch.randn(B, Lp, 3, H, D, generator=g)
@@ -165,8 +162,7 @@ def test_vocal_segments_with_sp_pads(world, S, n_fr):
 
 def _slots_worker(rank, world, port, q_ret):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         n_win, S = 5, 33
         rounds = -(-n_win // world)
