@@ -50,6 +50,25 @@ def test_gemm_epilogues(M, N, K):
     assert rel(out, res + ref.bfloat16().float() * g_rows) < 2e-3
 
 
+@pytest.mark.parametrize("kernel", [0, 2, 3], ids=["auto", "persistent", "persistent192"])
+@pytest.mark.parametrize("M,N", [(1000, 1536), (777, 640), (513, 520), (64512 // 8, 1536)])
+def test_gemm_bf16_epilogue_exact(kernel, M, N):
+    """The bf16 row epilogue's element placement and bias, bit-exact: small-integer operands make every product and
+    sum exact in fp32, so the only rounding is the final bf16 one (RNE on both sides).  N = 640 puts a 128-column
+    partial tile in the last column (one wave on the accumulator path, the other on the LDS-strip path), N = 520 a
+    ragged one; M leaves partial row tiles."""
+    from stableavatar_amd import ops
+    K = 256
+    x = torch.randint(-3, 4, (M, K), device=dev).bfloat16()
+    w = torch.randint(-3, 4, (N, K), device=dev).bfloat16()
+    b = torch.randint(-50, 51, (N,), device=dev).float()
+    ref = (x.float() @ w.float().t() + b).bfloat16()
+    y = ops.linear(x, w, b, ops.EPI_BF16, kernel=kernel)
+    assert torch.equal(y, ref)
+    y = ops.linear(x, w, None, ops.EPI_BF16, kernel=kernel)
+    assert torch.equal(y, (x.float() @ w.float().t()).bfloat16())
+
+
 @pytest.mark.parametrize("kernel", [0, 1, 2, 3], ids=["auto", "pingpong", "persistent", "persistent192"])
 @pytest.mark.parametrize("M,N,K", [(300, 520, 256), (257, 130, 128), (1000, 1536, 1536), (600, 300, 2304)])
 def test_gemm_kernels(kernel, M, N, K):
