@@ -88,13 +88,11 @@ def parse(argv=None):
 
 def launch_workers(args, argv) -> int:
     """--gpus N > 1 without a launcher: start torch.distributed.run as a CHILD process (this process
-    has not touched the GPU and stays the parent) and return its exit code."""
-    import socket
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    has not touched the GPU and stays the parent) and return its exit code.  --standalone: the launcher's
+    c10d rendezvous binds its TCPStore on port 0 itself and the workers share that store (MASTER_PORT = the
+    store's port), so no port is picked free and released before use (a race with any other listener)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", os.path.abspath(__file__), *argv]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.call(cmd, env=env)
@@ -568,50 +566,55 @@ class ClockSampler:
 def timed(work, steps, warmup, world, dev, events=False, before_timed=None):
     """W untimed warmup steps, then EXACTLY K steps between barriers; the max over ranks.
     before_timed(warmup_seconds) runs after the warmup, before the opening barrier.  events=True: the
-    self-attention events (roofline), the per-kernel-class HIP events (ktimer) and the SCLK samples of the timed
-    clips are recorded (work.kernels)."""
+    self-attention events (roofline) and the SCLK samples of the timed clips are recorded, and the per-kernel-class
+    HIP events (ktimer: one event after every library launch) on the LAST WARMUP clip, so that the timed region
+    carries no per-launch event but the self-attention's (work.kernels)."""
+    kt = clk = None
+    if events:
+        from stableavatar_amd.ktimer import KernelTimer
+        kt = KernelTimer() if dev.type == "cuda" and os.environ.get("SA_BENCH_KTIMER", "1") != "0" else None
+        clk = ClockSampler(dev) if dev.type == "cuda" and int(os.environ.get("RANK", "0")) == 0 else None
+    kt_ms = None
     with torch.no_grad():
         tw = time.perf_counter()
         for i in range(warmup):
-            work.step()
-            sync(dev)
+            ti = time.perf_counter()
+            if kt is not None and i == warmup - 1:
+                with kt:
+                    work.step()
+                    sync(dev)
+                kt_ms = (time.perf_counter() - ti) * 1e3
+            else:
+                work.step()
+                sync(dev)
             progress(f"warmup {i + 1}/{warmup} {time.perf_counter() - tw:.1f}s")
         tw = time.perf_counter() - tw
         if before_timed is not None:
             before_timed(tw)
-        kt = clk = None
-        if events:
-            from stableavatar_amd.ktimer import KernelTimer
-            kt = KernelTimer() if dev.type == "cuda" and os.environ.get("SA_BENCH_KTIMER", "1") != "0" else None
-            clk = ClockSampler(dev) if dev.type == "cuda" and int(os.environ.get("RANK", "0")) == 0 else None
         barrier(world, dev)
         if events:
             work.start_events()
-            if kt is not None:
-                kt.__enter__()
             if clk is not None:
                 clk.start()
         t0 = time.perf_counter()
         out = None
-        try:
-            for i in range(steps):
-                out = work.step()
-                if steps > 1 and i + 1 < steps:  # no sync: the clips stay queued back to back
-                    progress(f"timed {i + 1}/{steps} queued {time.perf_counter() - t0:.1f}s")
-            barrier(world, dev)
-        finally:
-            if kt is not None:
-                kt.__exit__(None, None, None)
+        for i in range(steps):
+            out = work.step()
+            if steps > 1 and i + 1 < steps:  # no sync: the clips stay queued back to back
+                progress(f"timed {i + 1}/{steps} queued {time.perf_counter() - t0:.1f}s")
+        barrier(world, dev)
         dt = time.perf_counter() - t0
         progress(f"timed {steps} steps {dt:.1f}s")
         if events:
-            rec = kt.summary(steps) if kt is not None else {}
+            rec = kt.summary(1) if (kt is not None and kt_ms is not None) else {}
             if rec:
-                rec["frac_of_ms_per_step"] = round(rec["sum_ms_per_clip"] / (dt / steps * 1e3), 4)
+                rec["frac_of_clip_ms"] = round(rec["sum_ms_per_clip"] / kt_ms, 4)
+                rec["clip_ms"] = round(kt_ms, 1)
             rec["sclk"] = clk.stop() if clk is not None else None
-            rec["note"] = ("per-kernel-class device time of the timed clips from one HIP event after every library "
-                           "launch on its stream (the interval since the stream's previous event, so each class "
-                           "includes the kernel boundary in front of it); ms per clip = mean over the timed clips")
+            rec["note"] = ("per-kernel-class device time of the last (untimed) warmup clip from one HIP event after "
+                           "every library launch on its stream (the interval since the stream's previous event, so "
+                           "each class includes the kernel boundary in front of it); sclk: sampled over the timed "
+                           "clips, which carry no per-launch events besides the self-attention's (roofline)")
             work.kernels = rec
     if world > 1:
         import torch.distributed as dist
@@ -805,10 +808,14 @@ def main(argv=None, work_factory=ClipWorkload, device=None):
         if world > 1:
             import torch.distributed as dist
             if not dist.is_initialized():
+                # env:// from the launcher by default; SA_DIST_INIT_METHOD (e.g. file://...) binds atomically for
+                # launches without one (the CPU tests)
+                init = os.environ.get("SA_DIST_INIT_METHOD")
+                kw = dict(init_method=init, rank=rank, world_size=world) if init else {}
                 if dev.type == "cuda":
-                    dist.init_process_group("nccl", device_id=dev)
+                    dist.init_process_group("nccl", device_id=dev, **kw)
                 else:
-                    dist.init_process_group("gloo")
+                    dist.init_process_group("gloo", **kw)
         out = run(args, world, rank, dev, work_factory, cpu=cpu)
         if out is not None:
             print(json.dumps(out), flush=True)

@@ -7,11 +7,11 @@ import torch
 import torch.multiprocessing as mp
 
 
-def _w(rank, port):
+def _w(rank, store):
     import torch.distributed as dist
     torch.cuda.set_device(0)
     try:
-        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2,
+        dist.init_process_group("nccl", init_method="file://" + store, rank=rank, world_size=2,
                                 device_id=torch.device("cuda:0"))
         x = torch.full((4,), float(rank + 1), device="cuda")
         dist.all_reduce(x)
@@ -23,10 +23,7 @@ def _w(rank, port):
 
 
 if __name__ == "__main__":
-    import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    mp.start_processes(_w, args=(port,), nprocs=2, join=True, start_method="spawn")
+    import tempfile
+    store = os.path.join(tempfile.mkdtemp(prefix="sa_rccl_probe_"), "store")  # file:// rendezvous: nothing to bind
+    mp.start_processes(_w, args=(store,), nprocs=2, join=True, start_method="spawn")
     sys.exit(0)

@@ -4,8 +4,8 @@ DiT forwards of the small golden model, for a rocprofv3 kernel trace of each mod
 kernels (the exchange is pack / row-mapped attention / column-panel O-projection only).
 usage: rocprofv3 --kernel-trace --stats -d <dir> -o run -- python scripts/sp_trace.py sp|single|loop"""
 import os
-import socket
 import sys
+import tempfile
 
 import torch
 import torch.distributed as dist
@@ -17,12 +17,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
 from test_gpu_dit import make_model, run  # noqa: E402
 from golden_cases import DIT_SMALL, dit_inputs  # noqa: E402
 
-s = socket.socket()
-s.bind(("127.0.0.1", 0))
-port = s.getsockname()[1]
-s.close()
 torch.cuda.set_device(0)
-dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+store = os.path.join(tempfile.mkdtemp(prefix="sa_sp_trace_"), "store")  # file:// rendezvous: nothing to bind
+dist.init_process_group("nccl", init_method="file://" + store, rank=0, world_size=1,
                         device_id=torch.device("cuda:0"))
 try:
     m = make_model(DIT_SMALL)

@@ -40,8 +40,6 @@ constexpr int KVB = 64;
 constexpr int TILE_BYTES = KVB * D * 2;      // 16 KB
 constexpr int STAGE_BYTES = 2 * TILE_BYTES;  // K + V
 constexpr int LDS_BYTES = 2 * STAGE_BYTES;   // 64 KB
-constexpr int V13_LDS = 3 * STAGE_BYTES;     // 96 KB: the ping-pong kernel's 3-stage ring
-constexpr int V13_VBASE = 3 * TILE_BYTES;    // its V region
 
 // 16-byte chunk swizzle for 256-B rows: conflict-free for both row (ds_read_b128) and
 // transposed (ds_read_b64_tr_b16) reads (cdna_hip_programming.md T10 form (b))
@@ -508,15 +506,10 @@ __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2]
 
 // ---- V^T forms of the block (V read as V^T from a d-major producer layout, [H*128][Rv] bf16: row h*128 + d holds
 // d of head h for every key row), so each PV operand is ds_read_b128 instead of two ds_read_b64_tr_b16.
-// VMODE 1 (v6t): the v6 block with V^T staged 128 d-rows x 64 keys (128 B per d-row, 16-B chunk c of row d at
-//   position c ^ (d & 7)); the producer stores the keys of each 32-key chunk in P's permuted order (position 8g + j
-//   <-> key 4g + j, j < 4; 16 + 4g + j - 4, j >= 4), so a lane's 16x16x32 PV operand is one b128 read.
-// VMODE 2 (v12): the PV product on v_mfma_f32_32x32x16_bf16 (16 instead of 32 PV MFMAs per block: half the MFMA
-//   issue slots for the same pipe time), V^T in natural key order (chunk c of row d at position c ^ ((d >> 1) & 7):
-//   conflict-free for the 32-row operand reads).  P reaches the 32x32 B layout (lane = query l % 32, keys 8 (l/32) ..
-//   +7 of a 16-key step) from the 16x16 QK^T accumulators by one permlane16_swap per packed dword pair: lane row 0
-//   keeps its query-tile-0 keys 0-3 and takes row 1's tile-0 keys 4-7, row 1 takes row 0's tile-1 keys 0-3 (rows 2 /
-//   3 likewise with keys 8-15).  The row sums stay on the 16x16x32 ones-MFMA of v6 (same bf16 P, same sums).
+// v6t: the v6 block with V^T staged 128 d-rows x 64 keys (128 B per d-row, 16-B chunk c of row d at position
+//   c ^ (d & 7)); the producer stores the keys of each 32-key chunk in P's permuted order (position 8g + j <-> key
+//   4g + j, j < 4; 16 + 4g + j - 4, j >= 4), so a lane's 16x16x32 PV operand is one b128 read.  (Measured and
+//   removed, records under profiles/r05/: the PV product on 32x32x16 MFMAs, a two-wave ping-pong, a 3-stage ring.)
 template <int VOFF, int C, int T0>
 __device__ __forceinline__ void v6t_read_v(u32x4* f, const uint32_t* vb) {
   ds_b128<VOFF + (T0 + 0) * 2048>(f[0], vb[C]);
@@ -644,85 +637,6 @@ __device__ __forceinline__ void attn_v6t_block(V6State& st, const bf16x8 (&qf)[2
       v6t_mma_v(st.O, 4, v1, pb);
     }
   }
-}
-
-struct V12State {
-  f32x16 O[4];    // O^T d-tile dt (32 d x 32 queries): lane = query l % 32, d = 32 dt + 8 (i/4) + 4 (l/32) + i % 4
-  f32x4 L[2];     // row sums as in V6State (query tile qt = lanes' query qt*16 + l%16)
-  float negm[2];
-  f32x4 negm4[2];
-};
-
-// V^T fragments of 16-key step S for the 4 d-tiles (d-tile t at +4096: 32 d-rows x 128 B)
-template <int VOFF, int S>
-__device__ __forceinline__ void v12_read_v(u32x4* f, const uint32_t* vb) {
-  ds_b128<VOFF + 0 * 4096>(f[0], vb[S]);
-  ds_b128<VOFF + 1 * 4096>(f[1], vb[S]);
-  ds_b128<VOFF + 2 * 4096>(f[2], vb[S]);
-  ds_b128<VOFF + 3 * 4096>(f[3], vb[S]);
-}
-
-__device__ __forceinline__ void v12_mma_v(f32x16 (&O)[4], const u32x4* f, const bf16x8& pb) {
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) O[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v6_as_bf8(f[dt]), pb, O[dt], 0, 0, 0);
-}
-
-template <int KOFF, int VOFF, bool FIRST>
-__device__ __forceinline__ void attn_v12_block(V12State& st, const bf16x8 (&qf)[2][4], const uint32_t* ka,
-                                               const uint32_t* vb, int kb, int kv_len, int g, bool hi16) {
-  f32x4 S[4][2];
-  v6_qk<KOFF>(S, st.negm4, qf, ka);
-  u32x4 va[4], vc[4];
-  v12_read_v<VOFF, 0>(va, vb);
-  v6_tail_mask(S, kb, kv_len, g);
-  v6_softmax_rescale<FIRST>(S, st.L, st.negm, st.negm4, [&](const float (&al)[2]) {
-    const float a = hi16 ? al[1] : al[0];  // this lane's query in the 32x32 layout
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) st.O[dt][i] *= a;
-  });
-  // P in bf16, packed per (16-key tile, query tile): the v6 packing, so the row-sum MFMAs are v6's
-  u32x2 pk[4][2];
-#pragma unroll
-  for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const bf16x4 x = {f2bf(S[kt][qt][0]), f2bf(S[kt][qt][1]), f2bf(S[kt][qt][2]), f2bf(S[kt][qt][3])};
-      pk[kt][qt] = __builtin_bit_cast(u32x2, x);
-    }
-  {
-    bf16x8 ones;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
-        st.L[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, v6_as_bf8(pk[2 * c][qt], pk[2 * c + 1][qt]), st.L[qt],
-                                                           0, 0, 0);
-  }
-  // P^T B operands of the four 16-key steps (32x32 layout)
-  bf16x8 pb[4];
-#pragma unroll
-  for (int kt = 0; kt < 4; ++kt) {
-    const auto x = __builtin_amdgcn_permlane16_swap(pk[kt][0][0], pk[kt][1][0], false, false);
-    const auto y = __builtin_amdgcn_permlane16_swap(pk[kt][0][1], pk[kt][1][1], false, false);
-    pb[kt] = __builtin_bit_cast(bf16x8, (u32x4){x[0], y[0], x[1], y[1]});
-  }
-  // O^T += V^T P^T, one 16-key step at a time: step s+1's V^T fragments are read (into the other buffer) before
-  // the wait for step s's, so they land under step s's MFMAs
-  v12_read_v<VOFF, 1>(vc, vb);
-  wait_k4<4>(va);
-  v12_mma_v(st.O, va, pb[0]);
-  v12_read_v<VOFF, 2>(va, vb);
-  wait_k4<4>(vc);
-  v12_mma_v(st.O, vc, pb[1]);
-  v12_read_v<VOFF, 3>(vc, vb);
-  wait_k4<4>(va);
-  v12_mma_v(st.O, va, pb[2]);
-  wait_k4<0>(vc);
-  v12_mma_v(st.O, vc, pb[3]);
 }
 
 // the fused cross-attention's last block of a source with at most 32 keys left (the image's 257th key, the 32
@@ -979,27 +893,12 @@ __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
   }
 }
 
-// self-attention reading V as V^T (attn_v6t_block / attn_v12_block above): 8 waves x 32 queries, the v6 ring and
-// K staging.  a.v = V^T [heads * 128][Rv] bf16 (row h*128 + d, a.vs = Rv >= the rows any segment reaches, rounded
-// up to 64; segments start on 32-key boundaries; every element of a row readable and finite through Rv: the
-// partial last block reads the keys past kv_len, masked to P = 0).  VMODE 1: keys permuted per 32 as P; VMODE 2:
-// natural key order.
-#if defined(SA_V13_STAMPS) || defined(SA_V6T_STAMPS)
-// measurement builds only (scripts/build_variant.sh ... -DSA_V13_STAMPS / -DSA_V6T_STAMPS): summed s_memtime cycles
-// per wave group over every wave of the launch (v13: barrier 1, work 1, barrier 2, MFMA phase; v6t: the DMA wait,
-// the barrier, the block loop, the blocks)
-__device__ unsigned long long g_v13_stamps[12];
-__device__ __forceinline__ uint64_t v13_now() {
-  const uint64_t t = __builtin_amdgcn_s_memtime();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  return t;
-}
-#endif
-
-// NST: K/V ring stages.  2: block kb+1's DMA issued at block kb (one block of lead, vmcnt(0) + __syncthreads()
-// per block); 3 (kernel 6): block kb+2's DMA at block kb, a counted vmcnt that leaves block kb+1's pieces in flight
-// and a bare s_barrier (no release fence, which would wait for them)
-template <int VMODE, int NST = 2>
+// self-attention reading V as V^T (attn_v6t_block above): 8 waves x 32 queries, the v6 ring and K staging.
+// a.v = V^T [heads * 128][Rv] bf16 (row h*128 + d, keys permuted per 32 as P; a.vs = Rv >= the columns any
+// segment's last 64-key block reaches, i.e. kv_row0 + ceil64(kv_len); segments start on 32-key boundaries; every
+// element of a row readable and finite through that block: the partial last block reads the keys past kv_len,
+// masked to P = 0).  2-stage K/V ring: block kb+1's DMA issued at block kb (one block of lead, vmcnt(0) +
+// __syncthreads() per block).
 __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
   constexpr int NW = 8, QBW = NW * 32, PPW = 16 / NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1054,18 +953,14 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
     const int srow = (dw * PPW + i) * 4 + (lane >> 4);
     koff[i] = srow * (int)a.ks * 2 + ((r16 ^ (srow & 15)) << 4);
     const int d = (dw * PPW + i) * 8 + (lane >> 3);  // a 1-KB piece = 8 d-rows x 128 B
-    const int sw = VMODE == 1 ? (d & 7) : ((d >> 1) & 7);
-    voff[i] = d * (int)a.vs * 2 + (((lane & 7) ^ sw) << 4);
+    voff[i] = d * (int)a.vs * 2 + (((lane & 7) ^ (d & 7)) << 4);
   }
   const uint32_t lds_dma = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + dw * PPW * 1024);
-  // LDS: 2 stages as K | V pairs; 3 stages as a K region and a V region (V13_VBASE), so every ds_read immediate
-  // offset from its region's read base stays below 64 KB
-  auto stage = [&](int kb, int buf) {
+  auto stage = [&](int kb, int buf) {  // LDS: 2 stages as K | V pairs
     const bool tail = ragged && kb == nkb - 1;
     const int ks_off = tail ? 0 : kb * KVB * (int)a.ks * 2, vs_off = kb * KVB * 2;
     const __amdgpu_buffer_rsrc_t bk = tail ? rkt : rk;
-    const int kdst = NST >= 3 ? buf * TILE_BYTES : buf * STAGE_BYTES;
-    const int vdst = NST >= 3 ? NST * TILE_BYTES + buf * TILE_BYTES : buf * STAGE_BYTES + TILE_BYTES;
+    const int kdst = buf * STAGE_BYTES, vdst = buf * STAGE_BYTES + TILE_BYTES;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(bk, LDS_PTR((uintptr_t)(lds_dma + kdst + i * 1024)), 16, koff[i],
@@ -1075,392 +970,11 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
     }
   };
   const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
-  uint32_t ka[4], vb[4];
-#pragma unroll
-  for (int dc = 0; dc < 4; ++dc) ka[dc] = lds0 + r16 * 256 + (((dc * 4 + g) ^ r16) << 4);
-  if constexpr (VMODE == 1) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-      vb[c] = lds0 + (NST >= 3 ? NST * TILE_BYTES : 0) + r16 * 128 + (((4 * c + g) ^ (r16 & 7)) << 4);
-    vb[2] = vb[3] = 0;
-  } else {
-    const int d32 = lane & 31, hh = lane >> 5;
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) vb[s4] = lds0 + d32 * 128 + (((2 * s4 + hh) ^ ((d32 >> 1) & 7)) << 4);
-  }
-  const bool hi16 = (lane >> 4) & 1;
-
-  using State = std::conditional_t<VMODE == 2, V12State, V6State>;
-  State st;
-  if constexpr (VMODE == 2) {
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) st.O[dt][i] = 0.f;
-  } else {
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) st.O[dt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  }
-  st.L[0] = st.L[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  st.negm[0] = st.negm[1] = 0.f;
-  st.negm4[0] = st.negm4[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  auto block = [&](auto koffc, auto firstc, int kb) {
-    constexpr int KO = decltype(koffc)::value;  // 2 stages: the stage's byte offset; 3 stages: the slot's
-    constexpr int VO = NST >= 3 ? KO : KO + TILE_BYTES;
-    constexpr bool FI = decltype(firstc)::value;
-    if constexpr (VMODE == 2)
-      attn_v12_block<KO, VO, FI>(st, qf, ka, vb, kb, kv_len, g, hi16);
-    else
-      attn_v6t_block<KO, VO, FI>(st, qf, ka, vb, kb, kv_len, g);
-  };
-  using C0 = std::integral_constant<int, 0>;
-  using C1 = std::integral_constant<int, STAGE_BYTES>;
-  if constexpr (NST == 2) {
-    stage(0, 0);
-    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (1 < nkb) stage(1, 1);
-    block(C0{}, std::true_type{}, 0);
-#ifdef SA_V6T_STAMPS
-    uint64_t sacc[3] = {0, 0, 0};  // DMA wait, barrier, loop
-    const uint64_t tl0 = v13_now();
-#define V6T_SYNC()                                    \
-  {                                                   \
-    const uint64_t ta = v13_now();                    \
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
-    const uint64_t tb = v13_now();                    \
-    __syncthreads();                                  \
-    const uint64_t tc = v13_now();                    \
-    sacc[0] += tb - ta;                               \
-    sacc[1] += tc - tb;                               \
-  }
-#else
-#define V6T_SYNC()                                    \
-  {                                                   \
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
-    __syncthreads();                                  \
-  }
-#endif
-    for (int kb = 1; kb < nkb; kb += 2) {
-      V6T_SYNC();
-      if (kb + 1 < nkb) stage(kb + 1, 0);
-      block(C1{}, std::false_type{}, kb);
-      if (kb + 1 >= nkb) break;
-      V6T_SYNC();
-      if (kb + 2 < nkb) stage(kb + 2, 1);
-      block(C0{}, std::false_type{}, kb + 1);
-    }
-#undef V6T_SYNC
-#ifdef SA_V6T_STAMPS
-    sacc[2] = v13_now() - tl0;
-    if (lane == 0) {
-      const int gi = __builtin_amdgcn_readfirstlane(tid >> 6) >= 4 ? 6 : 0;
-      for (int k = 0; k < 3; ++k) atomicAdd(&g_v13_stamps[gi + k], (unsigned long long)sacc[k]);
-      atomicAdd(&g_v13_stamps[gi + 3], (unsigned long long)(nkb - 1));
-    }
-#endif
-  } else {
-    using S1 = std::integral_constant<int, TILE_BYTES>;
-    using S2 = std::integral_constant<int, 2 * TILE_BYTES>;
-    // block kb in slot kb % 3; its DMA issued two blocks ahead.  The barrier follows this wave's LDS reads of the
-    // slot restaged after it (lgkmcnt(0)); other waves' pieces of block kb are covered by their own vmcnt before it
-    auto sync = [] {
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    auto wait_block = [&](int kb) {  // block kb landed (this wave's pieces); kb+1's may still fly
-      if (kb + 1 < nkb)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    };
-    stage(0, 0);
-    if (1 < nkb) stage(1, 1);
-    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-    wait_block(0);
-    sync();
-    if (2 < nkb) stage(2, 2);
-    block(C0{}, std::true_type{}, 0);
-    for (int kb = 1; kb < nkb; kb += 3) {
-      wait_block(kb);
-      sync();
-      if (kb + 2 < nkb) stage(kb + 2, 0);
-      block(S1{}, std::false_type{}, kb);
-      if (kb + 1 >= nkb) break;
-      wait_block(kb + 1);
-      sync();
-      if (kb + 3 < nkb) stage(kb + 3, 1);
-      block(S2{}, std::false_type{}, kb + 1);
-      if (kb + 2 >= nkb) break;
-      wait_block(kb + 2);
-      sync();
-      if (kb + 4 < nkb) stage(kb + 4, 2);
-      block(C0{}, std::false_type{}, kb + 2);
-    }
-  }
-
-  if constexpr (VMODE == 2) {
-    // lane l: query (l % 32), d = 32 dt + 8 (i / 4) + 4 (l / 32) + i % 4; a permlane32 swap per dword pair gives
-    // each lane 8 consecutive d (one 16-byte store): lanes < 32 d 16m + 0..7, lanes >= 32 d 16m + 8..15
-    const float inv = 1.0f / (hi16 ? st.L[1][0] : st.L[0][0]);  // a select: a dynamic index would put st in scratch
-    const int hh = lane >> 5;
-    const int qi = qb * QBW + wave * 32 + (lane & 31);
-    const int qrow = q_row0 + min(qi, q_len - 1);
-    const int orow = a.orows ? a.orows[qrow] : qrow;
-    bf16* op = a.o + (long)orow * a.os + h * D + 8 * hh;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int m = 0; m < 2; ++m) {
-        const f32x16& O = st.O[dt];
-        const bf16x4 pa = {f2bf(O[8 * m] * inv), f2bf(O[8 * m + 1] * inv), f2bf(O[8 * m + 2] * inv),
-                           f2bf(O[8 * m + 3] * inv)};
-        const bf16x4 pc = {f2bf(O[8 * m + 4] * inv), f2bf(O[8 * m + 5] * inv), f2bf(O[8 * m + 6] * inv),
-                           f2bf(O[8 * m + 7] * inv)};
-        const u32x2 ga = __builtin_bit_cast(u32x2, pa), gc = __builtin_bit_cast(u32x2, pc);
-        const auto rx = __builtin_amdgcn_permlane32_swap(ga[0], gc[0], false, false);
-        const auto ry = __builtin_amdgcn_permlane32_swap(ga[1], gc[1], false, false);
-        u32x4 out = {rx[0], ry[0], rx[1], ry[1]};
-        bf16* p = op + dt * 32 + 16 * m;
-        if (a.accumulate) {
-          const bf16x8 ov = *(const bf16x8*)p;
-          bf16x8 nv = __builtin_bit_cast(bf16x8, out);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) nv[j] = f2bf(bf2f(ov[j]) + bf2f(nv[j]));
-          out = __builtin_bit_cast(u32x4, nv);
-        }
-        if (qi < q_len) *(u32x4*)p = out;
-      }
-  } else {
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const float inv = 1.0f / st.L[qt][0];
-      const int qi = qb * QBW + wave * 32 + qt * 16 + r16;
-      const int qrow = q_row0 + min(qi, q_len - 1);
-      const int orow = a.orows ? a.orows[qrow] : qrow;
-      bf16* op = a.o + (long)orow * a.os + h * D + 4 * (g & ~1) + 16 * (g & 1);
-#pragma unroll
-      for (int dt = 0; dt < 8; dt += 2) {
-        const f32x4& A = st.O[dt][qt];
-        const f32x4& B = st.O[dt + 1][qt];
-        const bf16x4 pa = {f2bf(A[0] * inv), f2bf(A[1] * inv), f2bf(A[2] * inv), f2bf(A[3] * inv)};
-        const bf16x4 pb = {f2bf(B[0] * inv), f2bf(B[1] * inv), f2bf(B[2] * inv), f2bf(B[3] * inv)};
-        const u32x2 ga = __builtin_bit_cast(u32x2, pa), gb = __builtin_bit_cast(u32x2, pb);
-        const auto rx = __builtin_amdgcn_permlane16_swap(ga[0], gb[0], false, false);
-        const auto ry = __builtin_amdgcn_permlane16_swap(ga[1], gb[1], false, false);
-        u32x4 out = {rx[0], ry[0], rx[1], ry[1]};
-        bf16* p = op + dt * 16;
-        if (a.accumulate) {
-          const bf16x8 ov = *(const bf16x8*)p;
-          bf16x8 nv = __builtin_bit_cast(bf16x8, out);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) nv[j] = f2bf(bf2f(ov[j]) + bf2f(nv[j]));
-          out = __builtin_bit_cast(u32x4, nv);
-        }
-        if (qi < q_len) *(u32x4*)p = out;
-      }
-    }
-  }
-}
-
-// ---- v13: the v6t block (V^T in P's order) as a two-phase ping-pong between the two waves of each SIMD.  In v6/v6t
-// the 8 waves pass one barrier per block together, so the two waves of a SIMD run QK^T, softmax and PV in step and
-// the matrix pipe idles through both softmaxes (at 3 140 cycles per block per SIMD against 2 176 of MFMA work,
-// the idle time is about both waves' softmax).  Here every block has two barrier-separated phases, and the wave
-// groups A (waves 0-3) and B (4-7, each SIMD's partners) alternate roles:
-//   phase X_j:  A  softmax of block j (rescale test, exponentials, P in bf16)  |  B  PV of block j-1, QK^T of block j
-//   phase Y_j:  A  PV of block j, QK^T of block j+1                           |  B  softmax of block j
-// so on each SIMD one wave's MFMAs (68 per phase) run beside the other's exponentials.  The MFMA phase has one
-// wave per SIMD issuing, so its LDS operand latency is not covered by a partner: the softmax phase ends by reading
-// the first three operand sets of the wave's next MFMA phase (V13Frags), and the K / V ring has three stages so that
-// K_{j+1} and V_j are visible from barrier X_j on.  K_j and V_j sit in slot j % 3; after barrier Y_j every reader of
-// K_j and V_{j-1} is done, and their slots take the DMA of K_{j+3} and V_{j+2}, which each wave waits for (counted
-// vmcnt: the pieces issued after Y_{j+1} stay in flight) before barrier X_{j+2}.  Same per-wave arithmetic and order
-// as v6t: bit-identical output.
-// v13's operand fragments: three 16-register sets carry, in order, V chunk 0 d 0-63 / 64-127, V chunk 1 d 0-63 /
-// 64-127 of block j and K tiles 0-3 of block j + 1.  The first three are read at the end of the wave's softmax phase
-// (their data landed a phase earlier, 3-stage ring), so its MFMA phase opens with operands in registers; every later
-// set is read two sets (16 MFMAs) ahead of its use.
-struct V13Frags {
-  u32x4 f0[4], f1[4], f2[4];
-};
-template <int VOFF>
-__device__ __forceinline__ void v13_prefetch(V13Frags& fr, const uint32_t* vb) {
-  v6t_read_v<VOFF, 0, 0>(fr.f0, vb);
-  v6t_read_v<VOFF, 0, 4>(fr.f1, vb);
-  v6t_read_v<VOFF, 1, 0>(fr.f2, vb);
-}
-// the MFMA phase: PV of the softmaxed block j (V stage VOFF), then QK^T of block j + 1 (K stage KOFF; after the last
-// block a QK^T of a stale slot whose S is never used).  Same MFMA order per accumulator as v6t: bit-identical.
-template <int VOFF, int KOFF>
-__device__ __forceinline__ void v13_mfma_phase(V6State& st, const bf16x8 (&pb)[2][2], const uint32_t* vb,
-                                               f32x4 (&S)[4][2], const bf16x8 (&qf)[2][4], const uint32_t* ka,
-                                               V13Frags& fr) {
-  bf16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
-  st.L[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[0][0], st.L[0], 0, 0, 0);
-  st.L[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[0][1], st.L[1], 0, 0, 0);
-  wait_k4<0>(fr.f0);  // (landed before the phase's barrier)
-  v6t_mma_v(st.O, 0, fr.f0, pb[0]);
-  v6t_read_v<VOFF, 1, 4>(fr.f0, vb);  // V chunk 1, d 64-127
-  v6t_mma_v(st.O, 4, fr.f1, pb[0]);
-  v6_read_k<KOFF, 0>(fr.f1, ka);
-  st.L[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[1][0], st.L[0], 0, 0, 0);
-  st.L[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[1][1], st.L[1], 0, 0, 0);
-  v6t_mma_v(st.O, 0, fr.f2, pb[1]);
-  v6_read_k<KOFF, 1>(fr.f2, ka);
-  wait_k4<8>(fr.f0);
-  v6t_mma_v(st.O, 4, fr.f0, pb[1]);
-  v6_read_k<KOFF, 2>(fr.f0, ka);
-#pragma unroll
-  for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) S[kt][qt] = st.negm4[qt];
-  wait_k4<8>(fr.f1);
-  v6_mma_k(S, 0, fr.f1, qf);
-  v6_read_k<KOFF, 3>(fr.f1, ka);
-  wait_k4<8>(fr.f2);
-  v6_mma_k(S, 1, fr.f2, qf);
-  wait_k4<4>(fr.f0);
-  v6_mma_k(S, 2, fr.f0, qf);
-  wait_k4<0>(fr.f1);
-  v6_mma_k(S, 3, fr.f1, qf);
-}
-
-template <bool FIRST>
-__device__ __forceinline__ void v13_softmax(V6State& st, f32x4 (&S)[4][2], bf16x8 (&pb)[2][2], int kb, int kv_len,
-                                            int g) {
-  v6_tail_mask(S, kb, kv_len, g);
-  v6_softmax_rescale<FIRST>(S, st.L, st.negm, st.negm4, [&](const float (&al)[2]) {
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) st.O[dt][qt][i] *= al[qt];
-  });
-#pragma unroll
-  for (int c = 0; c < 2; ++c)
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        pb[c][qt][j] = f2bf(S[2 * c][qt][j]);
-        pb[c][qt][4 + j] = f2bf(S[2 * c + 1][qt][j]);
-      }
-}
-
-// a phase boundary: the workgroup barrier without __syncthreads()'s release fence (which waits vmcnt(0), i.e. for
-// the K/V DMA issued half a block earlier), MFMAs kept on their side of it
-__device__ __forceinline__ void v13_sync() {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS reads of the slots restaged after it
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-#ifdef SA_V13_STAMPS
-#define V13_STAMP(x) const uint64_t x = v13_now()
-#define V13_ACC(k, v) acc[k] += (v)
-#else
-#define V13_STAMP(x)
-#define V13_ACC(k, v)
-#endif
-
-__device__ __forceinline__ void attn_fwd_pp_body(const AttnArgs& a) {
-  constexpr int NW = 8, QBW = NW * 32, PPA = 4;  // the K / V DMA is issued by group A only: 4 pieces per wave
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nx = gridDim.x, ny = gridDim.y;
-  const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
-  const int qb = flat % nx, h = (flat / nx) % ny, seg = flat / (nx * ny);
-  const int* sg = a.segs + seg * 4;
-  const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
-  if (qb * QBW >= q_len) return;
-  const int tid = threadIdx.x, lane = tid & 63;
-  if (kv_len <= 0) {
-    if (!a.accumulate)
-      for (int i = tid; i < QBW * (D / 8); i += NW * 64) {
-        const int qi = qb * QBW + i / (D / 8);
-        if (qi < q_len) {
-          const int orow = a.orows ? a.orows[q_row0 + qi] : q_row0 + qi;
-          *(u32x4*)(a.o + (long)orow * a.os + h * D + (i % (D / 8)) * 8) = (u32x4){0u, 0u, 0u, 0u};
-        }
-      }
-    return;
-  }
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool grpB = wave >= 4;  // waves w and w + 4 share a SIMD
-  const int g = lane >> 4, r16 = lane & 15;
-  bf16x8 qf[2][4];
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int qc = min(qb * QBW + wave * 32 + qt * 16 + r16, q_len - 1);
-    const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * g;
-#pragma unroll
-    for (int dc = 0; dc < 4; ++dc) {
-      qf[qt][dc] = *(const bf16x8*)(qp + 32 * dc);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[qt][dc][j] = f2bf(bf2f(qf[qt][dc][j]) * a.c);
-    }
-  }
-  const int nkb = (kv_len + KVB - 1) / KVB;
-  const long tail0 = (long)(nkb - 1) * KVB;
-  const bool ragged = kv_len % KVB != 0;
-  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.k + (long)kv_row0 * a.ks + h * D), (short)0, (int)(((long)kv_len - 1) * a.ks * 2 + 256), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rkt = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.k + (kv_row0 + tail0) * a.ks + h * D), (short)0, (int)((kv_len - tail0 - 1) * a.ks * 2 + 256),
-      0x00020000);
-  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.v + (long)h * D * a.vs + kv_row0), (short)0, (int)(((long)(D - 1) * a.vs + (long)nkb * KVB) * 2),
-      0x00020000);
-  const uint32_t lds_dma = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + (wave & 3) * PPA * 1024);
-  // the per-lane DMA offsets are recomputed at every staging from the lane id (v_mbcnt), not kept across the loop:
-  // kept, hipcc spills them at this register pressure, and each reload's vmcnt(0) would wait for every DMA piece in
-  // flight (serialising the ring)
-  const int ks2 = (int)a.ks * 2, vs2 = (int)a.vs * 2;
-  auto lane_id = [] {  // volatile: not hoisted out of the loop
-    int l;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-    return l;
-  };
-  // 3-stage ring (V13_LDS): K_j at slot * TILE_BYTES, V_j at V13_VBASE + slot * TILE_BYTES (K and V regions apart,
-  // so every ds_read offset from its region's read base stays below 64 KB)
-  auto stage_k = [&](int kb, int slot) {
-    const bool tail = ragged && kb == nkb - 1;
-    const int ks_off = tail ? 0 : kb * KVB * ks2;
-    const __amdgpu_buffer_rsrc_t bk = tail ? rkt : rk;
-    const int ln = lane_id();
-#pragma unroll
-    for (int i = 0; i < PPA; ++i) {
-      const int srow = ((wave & 3) * PPA + i) * 4 + (ln >> 4);
-      const int koff = srow * ks2 + (((ln & 15) ^ (srow & 15)) << 4);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(bk, LDS_PTR((uintptr_t)(lds_dma + slot * TILE_BYTES + i * 1024)), 16,
-                                               koff, ks_off, 0, 0);
-    }
-  };
-  auto stage_v = [&](int kb, int slot) {
-    const int ln = lane_id();
-#pragma unroll
-    for (int i = 0; i < PPA; ++i) {
-      const int d = ((wave & 3) * PPA + i) * 8 + (ln >> 3);
-      const int voff = d * vs2 + (((ln & 7) ^ (d & 7)) << 4);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rv, LDS_PTR((uintptr_t)(lds_dma + V13_VBASE + slot * TILE_BYTES + i * 1024)), 16, voff, kb * KVB * 2, 0, 0);
-    }
-  };
-  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
   uint32_t ka[4], vb[2];
 #pragma unroll
   for (int dc = 0; dc < 4; ++dc) ka[dc] = lds0 + r16 * 256 + (((dc * 4 + g) ^ r16) << 4);
 #pragma unroll
-  for (int c = 0; c < 2; ++c) vb[c] = lds0 + V13_VBASE + r16 * 128 + (((4 * c + g) ^ (r16 & 7)) << 4);
+  for (int c = 0; c < 2; ++c) vb[c] = lds0 + r16 * 128 + (((4 * c + g) ^ (r16 & 7)) << 4);
 
   V6State st;
 #pragma unroll
@@ -1470,110 +984,24 @@ __device__ __forceinline__ void attn_fwd_pp_body(const AttnArgs& a) {
   st.L[0] = st.L[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
   st.negm[0] = st.negm[1] = 0.f;
   st.negm4[0] = st.negm4[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  f32x4 S[4][2];
-  bf16x8 pb[2][2];
-
-  V13Frags fr;
-  // ring prologue: K_0, K_1, K_2, V_0 (K_j, V_j in slot j % 3)
-  if (!grpB) {
-    stage_k(0, 0);
-    stage_v(0, 0);
-    if (1 < nkb) stage_k(1, 1);
-  } else {
-    if (2 < nkb) stage_k(2, 2);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // Both groups run the same cyclic body [softmax_j + operand prefetch, PV_j + QK_{j+1}], group B one phase later:
-  // A's body opens with barrier X_j, B's with Y_j (B's QK_0 precedes it in phase X_0), so each SIMD pairs one wave's
-  // softmax with the other's MFMAs.  The K / V DMA rides in the softmax phases, after the softmax (that wave then
-  // waits at the barrier for its partner's MFMAs anyway; issued at the top of an MFMA phase by all eight waves the
-  // 32 pieces held each wave ~700 cycles): A issues V_{j+1} in X_j (into V_{j-2}'s slot, whose readers are done by
-  // X_j), landed before X_{j+1}, where A starts reading it; B issues K_{j+3} in Y_j (into K_j's slot, done by Y_j),
-  // landed before Y_{j+2}, ahead of its first reader (A's QK^T in Y_{j+2}).  4 pieces per wave per block each.
-  // Block 0 is peeled (its softmax sets the running max), so the loop bodies carry no first-block branch.
-#ifdef SA_V13_STAMPS
-  uint64_t acc[6] = {0, 0, 0, 0, 0, 0};
-#endif
-  auto body = [&](auto firstc, auto slotc, auto grpc, int j) {
-    constexpr bool FIRST = decltype(firstc)::value, GB = decltype(grpc)::value;
-    constexpr int SL = decltype(slotc)::value;
-    constexpr int KN = ((SL + 1) % 3) * TILE_BYTES, VO = SL * TILE_BYTES;
-    if constexpr (!GB) {
-      V13_STAMP(tw);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of V_j (issued in X_{j-1})
-      V13_STAMP(t0);
-      V13_ACC(4, t0 - tw);
-      v13_sync();  // X_j
-      V13_STAMP(t1);
-      v13_softmax<FIRST>(st, S, pb, j, kv_len, g);
-      v13_prefetch<VO>(fr, vb);
-      V13_STAMP(t2s);
-      if (j + 1 < nkb) stage_v(j + 1, (SL + 1) % 3);
-      V13_STAMP(t2);
-      V13_ACC(5, t2 - t2s);
-      v13_sync();  // Y_j
-      V13_STAMP(t3);
-      V13_ACC(0, t1 - t0); V13_ACC(1, t2 - t1); V13_ACC(2, t3 - t2);
-    } else {
-      // this wave's pieces of K_{j+1} (issued in Y_{j-2}) landed; those of K_{j+2} (Y_{j-1}) may fly
-      V13_STAMP(tw);
-      if (j + 2 < nkb)
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      V13_STAMP(t0);
-      V13_ACC(4, t0 - tw);
-      v13_sync();  // Y_j
-      V13_STAMP(t1);
-      v13_softmax<FIRST>(st, S, pb, j, kv_len, g);
-      v13_prefetch<VO>(fr, vb);
-      if (j + 3 < nkb) stage_k(j + 3, SL);
-      V13_STAMP(t2);
-      if (j + 1 < nkb) v13_sync();  // X_{j+1}
-      V13_STAMP(t3);
-      V13_ACC(0, t1 - t0); V13_ACC(1, t2 - t1); V13_ACC(2, t3 - t2);
-    }
-    // V_j, K_{j+1} (after the last block a QK^T of a stale slot, unused: no branch in the body)
-#ifdef SA_V13_STAMPS
-    const uint64_t t4 = v13_now();
-#endif
-    // the MFMA phase's wave first at the issue arbiter, the softmax wave in its gaps (6.31 / 6.29 vs 6.41 / 6.44 ms
-    // with B's static priority alone, profiles/r05/attn_ab_v13_variants_r5u_r5v.jsonl)
-    __builtin_amdgcn_s_setprio(2);
-    v13_mfma_phase<VO, KN>(st, pb, vb, S, qf, ka, fr);
-    __builtin_amdgcn_s_setprio(GB ? 1 : 0);
-#ifdef SA_V13_STAMPS
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    acc[3] += v13_now() - t4;
-#endif
+  auto sync = [] {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   };
-  const auto S0 = std::integral_constant<int, 0>{};
-  const auto S1 = std::integral_constant<int, 1>{};
-  const auto S2 = std::integral_constant<int, 2>{};
-  auto run = [&](auto grpc) {
-    body(std::true_type{}, S0, grpc, 0);
-    for (int j = 1; j < nkb; j += 3) {
-      body(std::false_type{}, S1, grpc, j);
-      if (j + 1 >= nkb) break;
-      body(std::false_type{}, S2, grpc, j + 1);
-      if (j + 2 >= nkb) break;
-      body(std::false_type{}, S0, grpc, j + 2);
-    }
-  };
-  if (!grpB) {
-    v6_qk<0>(S, st.negm4, qf, ka);  // QK^T of block 0 before X_0
-    run(std::false_type{});
-  } else {
-    __builtin_amdgcn_s_setprio(1);
-    v13_sync();  // X_0
-    v6_qk<0>(S, st.negm4, qf, ka);
-    run(std::true_type{});
+  stage(0, 0);
+  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  sync();
+  if (1 < nkb) stage(1, 1);
+  attn_v6t_block<0, TILE_BYTES, true>(st, qf, ka, vb, 0, kv_len, g);
+  for (int kb = 1; kb < nkb; kb += 2) {
+    sync();
+    if (kb + 1 < nkb) stage(kb + 1, 0);
+    attn_v6t_block<STAGE_BYTES, STAGE_BYTES + TILE_BYTES, false>(st, qf, ka, vb, kb, kv_len, g);
+    if (kb + 1 >= nkb) break;
+    sync();
+    if (kb + 2 < nkb) stage(kb + 2, 1);
+    attn_v6t_block<0, TILE_BYTES, false>(st, qf, ka, vb, kb + 1, kv_len, g);
   }
-#ifdef SA_V13_STAMPS
-  if (lane == 0)
-    for (int k = 0; k < 6; ++k) atomicAdd(&g_v13_stamps[(grpB ? 6 : 0) + k], (unsigned long long)acc[k]);
-#endif
 
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
@@ -1587,17 +1015,17 @@ __device__ __forceinline__ void attn_fwd_pp_body(const AttnArgs& a) {
       const f32x4& A = st.O[dt][qt];
       const f32x4& B = st.O[dt + 1][qt];
       const bf16x4 pa = {f2bf(A[0] * inv), f2bf(A[1] * inv), f2bf(A[2] * inv), f2bf(A[3] * inv)};
-      const bf16x4 pc = {f2bf(B[0] * inv), f2bf(B[1] * inv), f2bf(B[2] * inv), f2bf(B[3] * inv)};
-      const u32x2 ga = __builtin_bit_cast(u32x2, pa), gc = __builtin_bit_cast(u32x2, pc);
-      const auto rx = __builtin_amdgcn_permlane16_swap(ga[0], gc[0], false, false);
-      const auto ry = __builtin_amdgcn_permlane16_swap(ga[1], gc[1], false, false);
+      const bf16x4 pb = {f2bf(B[0] * inv), f2bf(B[1] * inv), f2bf(B[2] * inv), f2bf(B[3] * inv)};
+      const u32x2 ga = __builtin_bit_cast(u32x2, pa), gb = __builtin_bit_cast(u32x2, pb);
+      const auto rx = __builtin_amdgcn_permlane16_swap(ga[0], gb[0], false, false);
+      const auto ry = __builtin_amdgcn_permlane16_swap(ga[1], gb[1], false, false);
       u32x4 out = {rx[0], ry[0], rx[1], ry[1]};
       bf16* p = op + dt * 16;
       if (a.accumulate) {
         const bf16x8 ov = *(const bf16x8*)p;
         bf16x8 nv = __builtin_bit_cast(bf16x8, out);
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) nv[jj] = f2bf(bf2f(ov[jj]) + bf2f(nv[jj]));
+        for (int j = 0; j < 8; ++j) nv[j] = f2bf(bf2f(ov[j]) + bf2f(nv[j]));
         out = __builtin_bit_cast(u32x4, nv);
       }
       if (qi < q_len) *(u32x4*)p = out;
@@ -1841,10 +1269,7 @@ __global__ __launch_bounds__(256, 2) void attn_cross3_w4_kernel(Cross3Args a) { 
 
 __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) { attn_fwd_v6_body<8>(a); }
 __global__ __launch_bounds__(256, 2) void attn_fwd_v6_w4_kernel(AttnArgs a) { attn_fwd_v6_body<4>(a); }
-__global__ __launch_bounds__(512) void attn_fwd_v6t_kernel(AttnArgs a) { attn_fwd_vt_body<1>(a); }
-__global__ __launch_bounds__(512) void attn_fwd_v12_kernel(AttnArgs a) { attn_fwd_vt_body<2>(a); }
-__global__ __launch_bounds__(512) void attn_fwd_v13_kernel(AttnArgs a) { attn_fwd_pp_body(a); }
-__global__ __launch_bounds__(512) void attn_fwd_v6t3_kernel(AttnArgs a) { attn_fwd_vt_body<1, 3>(a); }
+__global__ __launch_bounds__(512) void attn_fwd_v6t_kernel(AttnArgs a) { attn_fwd_vt_body(a); }
 
 }  // namespace
 
@@ -1864,17 +1289,13 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
   if (head_dim != D) return SA_ERR_ARG;
   if ((q_stride | k_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
   if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)o)) & 15) return SA_ERR_ARG;
-  if (kernel < 0 || kernel > 6) return SA_ERR_ARG;
-  if (kernel >= 3 && (v_stride % 64 || (((uintptr_t)v) & 127))) return SA_ERR_ARG;  // V^T rows: whole 64-key blocks
+  if (kernel < 0 || kernel > 3) return SA_ERR_ARG;
+  if (kernel == 3 && (v_stride % 64 || (((uintptr_t)v) & 127))) return SA_ERR_ARG;  // V^T rows: whole 64-key blocks
   static const bool attr = [] {  // one-time, thread-safe
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6_w4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6t_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_v12_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_v13_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, V13_LDS);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_v6t3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              3 * STAGE_BYTES);
     return true;
   }();
   (void)attr;
@@ -1896,16 +1317,9 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
   if (kernel == 2) {
     dim3 grid((max_q_len + 127) / 128, heads, nseg);
     hipLaunchKernelGGL(attn_fwd_v6_w4_kernel, grid, dim3(256), LDS_BYTES, (hipStream_t)stream, a);
-  } else if (kernel >= 3) {  // v = V^T [heads * 128][v_stride] (attn_fwd_vt_body / attn_fwd_pp_body)
+  } else if (kernel == 3) {  // v = V^T [heads * 128][v_stride] (attn_fwd_vt_body)
     dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
-    if (kernel == 3)
-      hipLaunchKernelGGL(attn_fwd_v6t_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
-    else if (kernel == 4)
-      hipLaunchKernelGGL(attn_fwd_v12_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
-    else if (kernel == 6)
-      hipLaunchKernelGGL(attn_fwd_v6t3_kernel, grid, dim3(512), 3 * STAGE_BYTES, (hipStream_t)stream, a);
-    else
-      hipLaunchKernelGGL(attn_fwd_v13_kernel, grid, dim3(512), V13_LDS, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(attn_fwd_v6t_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
   } else {
     dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
     hipLaunchKernelGGL(attn_fwd_v6_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
@@ -1966,14 +1380,3 @@ extern "C" int sa_attn_cross3(const void* q, int64_t q_stride, const void* kt, c
   SA_LAUNCH_CHECK();
   return SA_OK;
 }
-
-#if defined(SA_V13_STAMPS) || defined(SA_V6T_STAMPS)
-extern "C" int sa_debug_v13_stamps(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_v13_stamps), sizeof(unsigned long long) * 12) != hipSuccess) return SA_ERR_ARG;
-  if (reset) {
-    const unsigned long long z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_v13_stamps), z, sizeof(z)) != hipSuccess) return SA_ERR_ARG;
-  }
-  return SA_OK;
-}
-#endif

@@ -691,61 +691,18 @@ __device__ __forceinline__ void s7_t_epilogue(const GemmArgs& g, f32x4 (&acc)[8]
   }
 }
 
-// EPI_BF16_T(P32) through the LDS strip (s10's last tile): the natural-order MFMA's acc[i][j] (rows i*16 + 4 fc + e,
-// column j*16 + fr) written as the strip path writes the swapped layout leaves strip line fr holding, for each of the
-// 4 column groups of half h, 16 consecutive rows of one column; a lane then reads 16 rows of column (4h + (lane & 3))
-// * 16 + (lane >> 2): 4 x 8-byte pieces of row n of C^T (P32: the permuted positions of the half-chunk)
-template <int MI, bool P32>
-__device__ __forceinline__ void s7_t_strip_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8], float* strip, int wm,
-                                                    int wn, int fr, int fc, int lane, int m0, int n0, long bz) {
-  const int er = lane >> 2, jj = lane & 3;
-  bf16* const C = (bf16*)g.C + bz * g.sC;
-#pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const int m = m0 + wm * 16 * MI + i * 16;  // the strip's first row (a multiple of 16)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) *(f32x4*)(strip + fr * 68 + j * 16 + fc * 4) = acc[i][4 * h + j];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-      float v[16];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 t = *(const f32x4*)(strip + er * 68 + jj * 16 + q * 4);
-        v[4 * q] = t[0]; v[4 * q + 1] = t[1]; v[4 * q + 2] = t[2]; v[4 * q + 3] = t[3];
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-      const int n = n0 + wn * 128 + (4 * h + jj) * 16 + er;
-      const float b = (g.bias && n < g.N) ? g.bias[n] : 0.f;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {  // rows m + 4q .. +3
-        const bf16x4 o = {f2bf(v[4 * q] + b), f2bf(v[4 * q + 1] + b), f2bf(v[4 * q + 2] + b), f2bf(v[4 * q + 3] + b)};
-        const int mq = m + 4 * q, qq = (mq >> 2) & 7;
-        const int mc = P32 ? (mq & ~31) + 8 * (qq & 3) + 4 * (qq >> 2) : mq;
-        if (n < g.N && mq < g.M) *(bf16x4*)(C + (long)n * g.ldc + mc) = o;
-      }
-    }
-  }
-}
-
-// STRIP_ONLY: every tile through the LDS strip (no direct-from-AGPR path)
-template <int EPI, int MI = 8, bool STRIP_ONLY = false>
+template <int EPI, int MI = 8>
 __device__ __forceinline__ void s7_epilogue(const GemmArgs& g, f32x4 (&acc)[8][8], char* smem, int wave, int lane,
                                             int m0, int n0, long bz) {
   constexpr int BMT = 32 * MI;  // tile rows
   const int wm = wave >> 1, wn = wave & 1, fr = lane & 15, fc = lane >> 4;
   float* strip = (float*)(smem + S5_LDS + wave * S7_STRIP);
   if constexpr (EPI == EPI_BF16_T || EPI == EPI_BF16_TP32) {
-    if constexpr (STRIP_ONLY)
-      s7_t_strip_epilogue<MI, EPI == EPI_BF16_TP32>(g, acc, strip, wm, wn, fr, fc, lane, m0, n0, bz);
-    else
-      s7_t_epilogue<MI, EPI == EPI_BF16_TP32>(g, acc, wm, wn, fr, fc, m0, n0, bz);
+    s7_t_epilogue<MI, EPI == EPI_BF16_TP32>(g, acc, wm, wn, fr, fc, m0, n0, bz);
     return;
   }
   const int er = lane >> 2, ec = (lane & 3) * 16;
-  if constexpr ((EPI == EPI_RES_F32 || EPI == EPI_F32 || EPI == EPI_SILU_F32) && !STRIP_ONLY) {
+  if constexpr (EPI == EPI_RES_F32 || EPI == EPI_F32 || EPI == EPI_SILU_F32) {
     if (m0 + BMT <= g.M && n0 + BN <= g.N) {  // interior tile (wave-uniform)
       if (EPI != EPI_RES_F32 || !g.gate || m0 / g.rows_per_batch == (m0 + BMT - 1) / g.rows_per_batch)
         s7_f32_epilogue<EPI, true, MI>(g, acc, wm, wn, fr, fc, m0, n0, bz);
@@ -909,20 +866,6 @@ __device__ __forceinline__ void s7_bf16_perm_epilogue(const GemmArgs& g, f32x4 (
   }
 }
 
-#ifdef SA_GEMM_STAMPS
-// measurement builds only (scripts/build_variant.sh NAME -DSA_GEMM_STAMPS): summed s_memtime cycles over every wave
-// of the persistent kernel's launches: [0] first K-step pair of each tile, [1] the rest of the K loop, [2] the
-// epilogue, [3] tiles (per wave), [4] the epilogue's bias / setup part (to the first strip write)
-__device__ unsigned long long g_gemm_stamps[8];
-__device__ __forceinline__ uint64_t gemm_now() {
-  const uint64_t t = __builtin_amdgcn_s_memtime();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  return t;
-}
-#define GEMM_STAMP(x) const uint64_t x = gemm_now()
-#else
-#define GEMM_STAMP(x)
-#endif
 
 // ------------------------------------------------------------------------------------------------
 // s8 kernel: s7's persistence (tile walk u = blockIdx.x + k*gridDim.x, K pipeline running across tile
@@ -983,9 +926,7 @@ struct S9 {
   }
 };
 
-// OWN_WAIT: the caller issues the step's counted vmcnt wait + barrier #3 itself (s10: stores of the deferred epilogue
-// sit among the step's VMEM ops and change the count)
-template <int STAGE_R, int STAGE_D, int MI, int S, bool TR = false, bool OWN_WAIT = false>
+template <int STAGE_R, int STAGE_D, int MI, int S, bool TR = false>
 __device__ __forceinline__ void s9_slot(const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8], u32x4 (&b0)[8],
                                         u32x4 (&a1)[8], u32x4 (&b1)[8], int ks, int ksa) {
   using P = S9<MI>;
@@ -1017,7 +958,7 @@ __device__ __forceinline__ void s9_slot(const S5Ctx& c, f32x4 (&acc)[8][8], u32x
                    "+v"(b1[5]), "+v"(b1[6]), "+v"(b1[7])::"memory");
     __builtin_amdgcn_s_barrier();
   }
-  if constexpr (S == P::T3 - 1 && !OWN_WAIT) {
+  if constexpr (S == P::T3 - 1) {
     if constexpr (MI == 8)
       asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     else
@@ -1119,11 +1060,7 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
   constexpr bool BPRE = SA_EPI_V2 && !NOEPI && !TR && (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_GELU_ERF_BF16);
   f32x4 bpre[8];
   bool pre = false;
-#ifdef SA_GEMM_STAMPS
-  uint64_t sacc[4] = {0, 0, 0, 0};
-#endif
   while (true) {
-    GEMM_STAMP(ta);
     const int un = u + G;
     const bool has_next = un < total;
     __amdgpu_buffer_rsrc_t cra = c.ra, crw = c.rw, nra = c.ra, nrw = c.rw;
@@ -1147,12 +1084,6 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
                          "+v"(bpre[6]), "+v"(bpre[7]));
         }
       }
-#ifdef SA_GEMM_STAMPS
-      if (t == 0) {
-        GEMM_STAMP(tf);
-        sacc[0] += tf - ta;
-      }
-#endif
       {
         const bool nx = t + 3 >= nk;
         c.ra = nx ? nra : cra;
@@ -1165,7 +1096,6 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
       }
     }
     asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // MFMA -> v_accvgpr_read
-    GEMM_STAMP(tb);
     if constexpr (BPRE) {
       if (pre)  // two paths: a join would merge the strip path's load waits into this one
         s7_bf16_perm_epilogue<EPI, MI>(g, acc, bpre, wm, wn, lane & 15, lane >> 4, m0, n0, bz);
@@ -1174,12 +1104,6 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
     } else if constexpr (!NOEPI) {
       s7_epilogue<EPI, MI>(g, acc, smem, wave, lane, m0, n0, bz);
     }
-#ifdef SA_GEMM_STAMPS
-    GEMM_STAMP(tc);
-    sacc[1] += tb - ta;
-    sacc[2] += tc - tb;
-    sacc[3] += 1;
-#endif
     if (!has_next) break;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -1192,354 +1116,6 @@ __global__ __launch_bounds__(256, 1) void gemm_s8_kernel(GemmArgs g, int batch) 
     c.ra = nra;
     c.rw = nrw;
   }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-#ifdef SA_GEMM_STAMPS
-  if (lane == 0) {
-    atomicAdd(&g_gemm_stamps[0], (unsigned long long)sacc[0]);
-    atomicAdd(&g_gemm_stamps[1], (unsigned long long)(sacc[1] - sacc[0]));
-    atomicAdd(&g_gemm_stamps[2], (unsigned long long)sacc[2]);
-    atomicAdd(&g_gemm_stamps[3], (unsigned long long)sacc[3]);
-  }
-#endif
-}
-
-// ------------------------------------------------------------------------------------------------
-// s10: the s9 kernel on 192-row tiles with the epilogue of tile u DEFERRED under tile u+1's K loop.  On the s9 kernel
-// the epilogue runs between two K loops with the matrix pipe idle (kbench, config-2 shapes, epilogue removed vs
-// kept: O-proj 0.206 vs 0.402 ms, FFN-up 1.189 vs 1.498, QKV 0.606 vs 0.742, cross-Q 0.199 vs 0.237;
-// profiles/r05/kb_gemm_noepi_r5e.jsonl).  Here, after a tile's last K step, the accumulators are rounded once to
-// the Linear's bf16 output, bf16(acc + bias) (what every epilogue consumes first: the reference's autocast Linear,
-// 1B:376-379,644-646,677-679,688-691), into a register stash of MI x 8 units (one unit = one lane's 4 outputs: 4
-// columns of one row, or 4 rows of one column when stored transposed), and the next tile's K loop retires two
-// units per K step at one point after the step's counted vmcnt wait: the GELU (FFN-up), the fp32 gated residual
-// r + y * gate (O-projection, cross-O; r / gate of the next step's units loaded there too), or the bf16 store
-// itself.  Those loads and stores are younger than the step's DMA pieces and older than the next step's, whose
-// vmcnt wait retires them: the K pipeline's accounting is s9's.  Registers: the 192-row tile's 192 accumulator
-// AGPRs leave 64 AGPRs, which hold units i = 0..3 of the stash; units i = 4, 5 (32 dwords) sit in VGPRs beside s9's.
-// The unit index is the K step's (runtime) -> one switch per step with compile-time unit indices (no dynamically
-// indexed registers).  The last tile of a workgroup runs the s7 epilogue from the accumulators.  Same MFMA order
-// and the same roundings as s9: bit-identical outputs.  K = 1536 (24 K steps = 48 units = 2 per step).
-#ifndef SA_S10_EXP
-#define SA_S10_EXP 0  // measurement builds only: 1 = no deferred stores, 2 = no stash either (outputs incomplete)
-#endif
-constexpr int S10_NK = 24, S10_MI = 6, S10_AI = 4;  // K steps, tile row fragments, stash rows held in AGPRs
-
-template <int EPI>
-struct S10Stash {
-  u32x2 sa[S10_AI][8];           // bf16x4 of bf16(acc + bias), units i < S10_AI (AGPRs)
-  u32x2 sv[S10_MI - S10_AI][8];  // units i >= S10_AI (VGPRs)
-  f32x4 rin[2], gin[2];          // EPI_RES_F32: residual / gate of the two units of the coming step
-  // this lane's unit-(0, 0) addresses in the stashed tile (units add compile-time row / column steps): the output,
-  // the residual and the gate row; `row` = its first row (a unit's row < M decides its store)
-  // global-address-space pointers: through the opaque asm below a generic pointer would become flat_* stores, which
-  // count in lgkmcnt too and would stall every counted LDS wait of the K loop
-  __attribute__((address_space(1))) char* cp;
-  const __attribute__((address_space(1))) float* rp;
-  const __attribute__((address_space(1))) float* gp;
-  int row;     // the lane's first row of the stashed tile (a unit's rows: row + 16 i ...)
-  int rowlim;  // M - row: unit i stores iff 16 i < rowlim
-};
-
-template <int EPI, int I, int J>
-__device__ __forceinline__ u32x2 s10_get(S10Stash<EPI>& st) {
-  if constexpr (I < S10_AI) {
-    // a use (not a redefinition) in an AGPR: a "+a" here would give every switch case its own copy of the stash
-    // and the case joins dozens of v_accvgpr_mov
-    asm volatile("" ::"a"(st.sa[I][J]));
-    return st.sa[I][J];
-  } else {
-    return st.sv[I - S10_AI][J];
-  }
-}
-
-// unit U = (i = U % MI, j = U / MI): rows / columns of this lane -- swapped layout: row m0 + wm*16*MI + i*16 + fr,
-// columns n0 + wn*128 + j*16 + fc*4 + 0..3; transposed (TR): rows m0 + wm*16*MI + i*16 + 4 fc + 0..3 of column
-// n0 + wn*128 + j*16 + fr (P32: the 32-row chunk's permuted positions -- the tile rows start on 32-row
-// boundaries, so unit i's 4 rows land at +32 (i / 2) + 8 fc + 4 (i & 1) from the lane's chunk base)
-template <int EPI, int U, int SLOT>
-__device__ __forceinline__ void s10_unit_load(const GemmArgs& g, S10Stash<EPI>& st, long ldr) {
-  if constexpr (EPI == EPI_RES_F32) {
-    constexpr int MI = S10_MI, i = U % MI, j = U / MI;
-    if (i * 16 < st.rowlim) {  // a row past M is never stored
-      st.rin[SLOT] = *(const __attribute__((address_space(1))) f32x4*)(st.rp + (i * 16) * ldr + j * 16);
-      st.gin[SLOT] = st.gp ? *(const __attribute__((address_space(1))) f32x4*)(st.gp + j * 16)
-                           : (f32x4){1.f, 1.f, 1.f, 1.f};
-    }
-  }
-}
-
-__device__ __forceinline__ f32x4 s10_unpack(u32x2 p) {
-  return (f32x4){__uint_as_float(p[0] << 16), __uint_as_float(p[0] & 0xffff0000u), __uint_as_float(p[1] << 16),
-                 __uint_as_float(p[1] & 0xffff0000u)};
-}
-
-template <int EPI, int U, int SLOT>
-__device__ __forceinline__ void s10_unit_finish(const GemmArgs& g, S10Stash<EPI>& st, int ncols, long ldc) {
-  constexpr int MI = S10_MI, i = U % MI, j = U / MI;
-  const u32x2 y2 = s10_get<EPI, i, j>(st);
-  if constexpr (EPI == EPI_BF16_T || EPI == EPI_BF16_TP32) {
-    constexpr int off = EPI == EPI_BF16_TP32 ? 32 * (i / 2) + 4 * (i & 1) : 16 * i;  // elements along the row of C^T
-    if (j * 16 < ncols && i * 16 < st.rowlim)
-      *(__attribute__((address_space(1))) u32x2*)(st.cp + ((j * 16) * ldc + off) * 2) = y2;
-  } else {
-    const bool ok = i * 16 < st.rowlim && j * 16 < ncols;
-    if constexpr (EPI == EPI_BF16) {
-      if (ok) *(__attribute__((address_space(1))) u32x2*)(st.cp + ((i * 16) * ldc + j * 16) * 2) = y2;
-    } else if constexpr (EPI == EPI_GELU_BF16) {
-      const f32x4 x = s10_unpack(y2);
-      const f32x2 y0 = gelu_tanh2((f32x2){x[0], x[1]}), y1 = gelu_tanh2((f32x2){x[2], x[3]});
-      const bf16x4 o = {f2bf(y0[0]), f2bf(y0[1]), f2bf(y1[0]), f2bf(y1[1])};
-      if (ok) *(__attribute__((address_space(1))) bf16x4*)(st.cp + ((i * 16) * ldc + j * 16) * 2) = o;
-    } else {  // EPI_RES_F32
-      const f32x4 y = s10_unpack(y2), r = st.rin[SLOT], gt = st.gin[SLOT];
-      const f32x4 o = {r[0] + y[0] * gt[0], r[1] + y[1] * gt[1], r[2] + y[2] * gt[2], r[3] + y[3] * gt[3]};
-      if (ok) *(__attribute__((address_space(1))) f32x4*)(st.cp + ((i * 16) * ldc + j * 16) * 4) = o;
-    }
-  }
-}
-
-// the deferred work of K step T: retire units 2T, 2T+1, then load the residual inputs of step T+1's units
-template <int EPI, int T>
-__device__ __forceinline__ void s10_step_work(const GemmArgs& g, S10Stash<EPI>& st, int ncols, long ldc, long ldr) {
-  s10_unit_finish<EPI, 2 * T, 0>(g, st, ncols, ldc);
-  s10_unit_finish<EPI, 2 * T + 1, 1>(g, st, ncols, ldc);
-  if constexpr (2 * T + 2 < S10_MI * 8) {
-    s10_unit_load<EPI, 2 * T + 2, 0>(g, st, ldr);
-    s10_unit_load<EPI, 2 * T + 3, 1>(g, st, ldr);
-  }
-}
-
-template <int EPI>
-__device__ __forceinline__ void s10_work(const GemmArgs& g, S10Stash<EPI>& st, int step, int ncols) {
-  // the stashed tile's addresses made opaque here, so the units' address arithmetic is formed at the use and not
-  // hoisted out of the K loop (48 units x a 64-bit address would not fit beside the stash)
-  asm volatile("" : "+v"(st.cp), "+v"(st.rp), "+v"(st.gp), "+v"(st.rowlim));
-  // the row strides too (else hipcc hoists all 48 units' scalar offsets out of the loop: ~100 SGPRs, spilled to
-  // VGPR lanes and read back with v_readlane at every use)
-  long ldc = g.ldc, ldr = g.ldr;
-  asm volatile("" : "+s"(ldc), "+s"(ldr));
-  switch (step) {
-#define SA_S10_CASE(T) \
-  case T: s10_step_work<EPI, T>(g, st, ncols, ldc, ldr); break;
-    SA_S10_CASE(0) SA_S10_CASE(1) SA_S10_CASE(2) SA_S10_CASE(3) SA_S10_CASE(4) SA_S10_CASE(5) SA_S10_CASE(6)
-    SA_S10_CASE(7) SA_S10_CASE(8) SA_S10_CASE(9) SA_S10_CASE(10) SA_S10_CASE(11) SA_S10_CASE(12) SA_S10_CASE(13)
-    SA_S10_CASE(14) SA_S10_CASE(15) SA_S10_CASE(16) SA_S10_CASE(17) SA_S10_CASE(18) SA_S10_CASE(19)
-    SA_S10_CASE(20) SA_S10_CASE(21) SA_S10_CASE(22) SA_S10_CASE(23)
-#undef SA_S10_CASE
-    default: break;
-  }
-}
-
-// one s9 slot plus the deferred work of the step (HAVE: a stash is pending, wave-uniform).  The step's two unit stores
-// go right after its last DMA piece (slot T3 - 2), so they are younger than the step's DMA pieces, and the step's
-// wait (slot T3 - 1) counts them out together with the previous step's: vmcnt(14 + stores of this step + stores of
-// the previous one) still retires the previous step's DMA pieces (K-tile t + 1) while every store gets two steps to
-// complete (stores stay counted in vmcnt far longer than a load under load: with one step, 0.34 vs 0.24 ms cross-Q)
-template <int EPI, int STAGE, int S, bool TR>
-__device__ __forceinline__ void s10_slot(const GemmArgs& g, const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8],
-                                         u32x4 (&b0)[8], u32x4 (&a1)[8], u32x4 (&b1)[8], int ks, S10Stash<EPI>& st,
-                                         bool have, int step, int ncols, int nwait) {
-  s9_slot<STAGE, STAGE, S10_MI, S, TR, true>(c, acc, a0, b0, a1, b1, ks, ks);
-  constexpr int T3 = S9<S10_MI>::T3;
-  static_assert(S9<S10_MI>::act(T3 - 2) == 25 + 7, "the step's last W DMA piece sits in slot T3 - 2");
-  if constexpr (S == T3 - 2 && SA_S10_EXP == 0) {
-    if (have) s10_work<EPI>(g, st, step, ncols);
-  }
-  if constexpr (S == T3 - 1) {
-    if (nwait == 18)
-      asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-    else if (nwait == 16)
-      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-}
-
-template <int EPI, int STAGE, bool TR, int... Ss>
-__device__ __forceinline__ void s10_step(const GemmArgs& g, const S5Ctx& c, f32x4 (&acc)[8][8], u32x4 (&a0)[8],
-                                         u32x4 (&b0)[8], u32x4 (&a1)[8], u32x4 (&b1)[8], int ks, S10Stash<EPI>& st,
-                                         bool have, int step, int ncols, int nwait, std::integer_sequence<int, Ss...>) {
-  s4_wait_frags<S10_MI>(a0, b0);
-  (s10_slot<EPI, STAGE, Ss, TR>(g, c, acc, a0, b0, a1, b1, ks, st, have, step, ncols, nwait), ...);
-}
-
-// the stash of this tile: bf16(acc + bias) per unit (bias by column: per lane 32 columns, or 8 when transposed)
-template <int EPI, bool TR>
-__device__ __forceinline__ void s10_stash(const GemmArgs& g, f32x4 (&acc)[8][8], S10Stash<EPI>& st, int m0, int n0,
-                                          long bz, int wm, int wn, int fr, int fc) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    f32x4 b = {0.f, 0.f, 0.f, 0.f};
-    if (g.bias) {
-      if constexpr (TR) {
-        const float bb = g.bias[min(n0 + wn * 128 + j * 16 + fr, g.N - 1)];
-        b = (f32x4){bb, bb, bb, bb};
-      } else {
-        b = *(const f32x4*)(g.bias + min(n0 + wn * 128 + j * 16 + fc * 4, g.N - 4));
-      }
-    }
-    asm volatile("" : "+a"(acc[0][j]), "+a"(acc[1][j]), "+a"(acc[2][j]), "+a"(acc[3][j]), "+a"(acc[4][j]),
-                 "+a"(acc[5][j])::"memory");
-#pragma unroll
-    for (int i = 0; i < S10_MI; ++i) {
-      const f32x4 v = acc[i][j];
-      const bf16x4 o = {f2bf(v[0] + b[0]), f2bf(v[1] + b[1]), f2bf(v[2] + b[2]), f2bf(v[3] + b[3])};
-      const u32x2 w = __builtin_bit_cast(u32x2, o);
-      if (i < S10_AI) {
-        st.sa[i < S10_AI ? i : 0][j] = w;
-        asm volatile("" : "+a"(st.sa[i < S10_AI ? i : 0][j]));
-      } else {
-        st.sv[i >= S10_AI ? i - S10_AI : 0][j] = w;
-      }
-    }
-  }
-  // this lane's unit-(0, 0) addresses (see s10_unit_load)
-  if constexpr (TR) {
-    const int mb = m0 + wm * 16 * S10_MI;  // a multiple of 32
-    const int mcl = EPI == EPI_BF16_TP32 ? mb + 8 * fc : mb + 4 * fc;
-    st.cp = (__attribute__((address_space(1))) char*)((bf16*)g.C + bz * g.sC + (long)(n0 + wn * 128 + fr) * g.ldc + mcl);
-    st.row = mb + 4 * fc;
-    st.rowlim = g.M - st.row;
-  } else {
-    const int row = m0 + wm * 16 * S10_MI + fr, col = n0 + wn * 128 + fc * 4;
-    constexpr int ES = EPI == EPI_RES_F32 ? 4 : 2;
-    st.cp = (__attribute__((address_space(1))) char*)((char*)g.C + (bz * g.sC + (long)row * g.ldc + col) * ES);
-    if constexpr (EPI == EPI_RES_F32) {
-      st.rp = (const __attribute__((address_space(1))) float*)(g.R + bz * g.sR + (long)row * g.ldr + col);
-      st.gp = (const __attribute__((address_space(1))) float*)(
-          g.gate ? g.gate + (long)(m0 / g.rows_per_batch) * g.gate_bstride + col : g.gate);
-    }
-    st.row = row;
-    st.rowlim = g.M - row;
-  }
-}
-
-template <int EPI>
-__global__ __launch_bounds__(256, 1) void gemm_s10_kernel(GemmArgs g, int batch) {
-  constexpr int MI = S10_MI, BMT = 32 * MI;
-  constexpr bool TR = EPI == EPI_BF16_T || EPI == EPI_BF16_TP32;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int fr = lane & 15, fc = lane >> 4;
-  const int nm = (g.M + BMT - 1) / BMT, nn = (g.N + BN - 1) / BN;
-  const int total = nm * nn * batch, G = gridDim.x;
-  int u = blockIdx.x;
-  S5Ctx c;
-  int m0, n0;
-  long bz;
-  s7_tile<MI>(g, u, total, G, nm, nn, m0, n0, bz, c.ra, c.rw);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int row = (i * 4 + wave) * 8 + (lane >> 3);
-    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-    c.aoff[i] = row * (int)g.lda * 2 + chunk * 16;
-    c.woff[i] = row * (int)g.ldw * 2 + chunk * 16;
-  }
-  const uint32_t lds0 = (uint32_t)(uintptr_t)LDS_PTR(smem);
-  c.lds_dma = __builtin_amdgcn_readfirstlane(lds0 + wave * 1024);
-#pragma unroll
-  for (int stg = 0; stg < 2; ++stg)
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      const int sw = ((4 * kh + fc) ^ ((fr >> 1) & 7)) << 4;
-      c.ard[stg][kh] = lds0 + stg * S5_STAGE + (wm * 16 * MI + fr) * 128 + sw;
-      c.wrd[stg][kh] = lds0 + stg * S5_STAGE + 256 * 128 + (wn * 128 + fr) * 128 + sw;
-    }
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  u32x4 a0[8], b0[8], a1[8], b1[8];
-#define SA_S10_DMA(STAGE, P) \
-  if constexpr (P < MI + 8) s5_dma<STAGE, P, MI>(c, ks, ks);
-#define SA_S10_DMA_ALL(STAGE, T)                                                                              \
-  {                                                                                                           \
-    const int ks = (T) * 128;                                                                                 \
-    SA_S10_DMA(STAGE, 0) SA_S10_DMA(STAGE, 1) SA_S10_DMA(STAGE, 2) SA_S10_DMA(STAGE, 3) SA_S10_DMA(STAGE, 4) \
-    SA_S10_DMA(STAGE, 5) SA_S10_DMA(STAGE, 6) SA_S10_DMA(STAGE, 7) SA_S10_DMA(STAGE, 8) SA_S10_DMA(STAGE, 9) \
-    SA_S10_DMA(STAGE, 10) SA_S10_DMA(STAGE, 11) SA_S10_DMA(STAGE, 12) SA_S10_DMA(STAGE, 13)                  \
-  }
-  SA_S10_DMA_ALL(0, 0)
-  SA_S10_DMA_ALL(1, 1)
-#undef SA_S10_DMA_ALL
-#undef SA_S10_DMA
-  asm volatile("s_waitcnt vmcnt(14)" ::: "memory");  // K-tile 0 landed; K-tile 1's 14 pieces may still fly
-  __builtin_amdgcn_s_barrier();
-  s5_read<0, 0, 0, MI>(c, a0, b0); s5_read<0, 0, 1, MI>(c, a0, b0); s5_read<0, 0, 2, MI>(c, a0, b0);
-  s5_read<0, 0, 3, MI>(c, a0, b0); s5_read<0, 0, 4, MI>(c, a0, b0); s5_read<0, 0, 5, MI>(c, a0, b0);
-  s5_read<0, 0, 6, MI>(c, a0, b0); s5_read<0, 0, 7, MI>(c, a0, b0); s5_read<0, 0, 8, MI>(c, a0, b0);
-  s5_read<0, 0, 9, MI>(c, a0, b0); s5_read<0, 0, 10, MI>(c, a0, b0); s5_read<0, 0, 11, MI>(c, a0, b0);
-  s5_read<0, 0, 12, MI>(c, a0, b0); s5_read<0, 0, 13, MI>(c, a0, b0);
-
-  S10Stash<EPI> st;
-  st.cp = nullptr;
-  st.rp = st.gp = nullptr;
-  st.row = st.rowlim = 0;
-  int ncols = 0;  // columns of the stashed tile this lane's units may store (N - the lane's first column)
-  bool have = false;
-  int prev_uv = 0;  // deferred-work VMEM ops in the previous tile's last step
-  const int nk = S10_NK;
-  while (true) {
-    const int un = u + G;
-    const bool has_next = un < total;
-    __amdgpu_buffer_rsrc_t nra = c.ra, nrw = c.rw;
-    const __amdgpu_buffer_rsrc_t cra = c.ra, crw = c.rw;
-    int nm0 = m0, nn0 = n0;
-    long nbz = bz;
-    if (has_next) s7_tile<MI>(g, un, total, G, nm, nn, nm0, nn0, nbz, nra, nrw);
-    // the residual inputs of the stash's first two units (step 0's)
-    if (have) {
-      s10_unit_load<EPI, 0, 0>(g, st, g.ldr);
-      s10_unit_load<EPI, 1, 1>(g, st, g.ldr);
-    }
-    // the steps' vmcnt counts would be 14 DMA pieces + this step's and the previous step's unit stores (UV = 2 per
-    // step with a stash), giving each store two steps to retire.  Measured no faster than vmcnt(14) (cross-Q 0.340 vs
-    // 0.338 ms, profiles/r05/gemm_ab_s9_vs_s10_deferred_r5i_r5j.jsonl), and only exact while no unit's store is
-    // skipped for a whole wave (an all-false exec mask issues nothing) -- so UV = 0: the plain vmcnt(14)
-    constexpr int UV = 0;  // counted VMEM ops per step of the deferred work
-    const int cur = have ? UV : 0;
-    for (int t = 0; t < nk; t += 2) {
-      {
-        const bool nx = t + 2 >= nk;
-        c.ra = nx ? nra : cra;
-        c.rw = nx ? nrw : crw;
-        const int ksd = (nx ? (has_next ? t + 2 - nk : nk - 1) : t + 2) * 128;
-        s10_step<EPI, 0, TR>(g, c, acc, a0, b0, a1, b1, ksd, st, have, t, ncols, 14 + cur + (t == 0 ? prev_uv : cur),
-                             std::make_integer_sequence<int, S9<MI>::TOT>{});
-      }
-      {
-        const bool nx = t + 3 >= nk;
-        c.ra = nx ? nra : cra;
-        c.rw = nx ? nrw : crw;
-        const int ksd = (nx ? (has_next ? t + 3 - nk : nk - 1) : t + 3) * 128;
-        s10_step<EPI, 1, TR>(g, c, acc, a0, b0, a1, b1, ksd, st, have, t + 1, ncols, 14 + 2 * cur,
-                             std::make_integer_sequence<int, S9<MI>::TOT>{});
-      }
-    }
-    prev_uv = cur;
-    asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // MFMA -> v_accvgpr_read
-    if (!has_next) break;
-    if (SA_S10_EXP < 2) s10_stash<EPI, TR>(g, acc, st, m0, n0, bz, wm, wn, fr, fc);
-    ncols = g.N - (n0 + wn * 128 + (TR ? fr : fc * 4));
-    have = true;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    u = un;
-    m0 = nm0;
-    n0 = nn0;
-    bz = nbz;
-    c.ra = nra;
-    c.rw = nrw;
-  }
-  // the workgroup's last tile, from the accumulators through the LDS strip (the direct-from-AGPR epilogues make
-  // hipcc spill the loop's stash)
-  s7_epilogue<EPI, MI, true>(g, acc, smem, wave, lane, m0, n0, bz);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 
@@ -1549,22 +1125,7 @@ constexpr int KERNEL_PERSISTENT_AUTO = 4;  // internal: the persistent kernel wi
 constexpr int KERNEL_S9_AUTO = 5, KERNEL_S9 = 6, KERNEL_S9_192 = 7;
 // measurement only: the s9 kernel with the epilogue removed (256- / 192-row tiles), output not written
 constexpr int KERNEL_S9_NOEPI = 8, KERNEL_S9_192_NOEPI = 9;
-// s10: 192-row tiles, epilogue deferred under the next tile's K loop (K = 1536); auto picks it where it applies
-constexpr int KERNEL_S10 = 10, KERNEL_MAX = 10;
-
-// the deferred-epilogue kernel takes this call (EPI and shape): K = 64 * S10_NK, N % 4 == 0, the fp32 residual only
-// with a per-tile gate row (rows_per_batch a multiple of the 192-row tile) and one A matrix (no column panels)
-template <int EPI>
-bool s10_ok(const GemmArgs& g) {
-  if (EPI != EPI_BF16 && EPI != EPI_GELU_BF16 && EPI != EPI_RES_F32 && EPI != EPI_BF16_T && EPI != EPI_BF16_TP32)
-    return false;
-  if (g.K != 64 * S10_NK || g.N % 4 || g.a_pmul) return false;
-  if ((long)BM * g.lda * 2 >= 0x7fffffffL || (long)BN * g.ldw * 2 >= 0x7fffffffL) return false;
-  if (EPI == EPI_RES_F32 && g.gate && g.rows_per_batch % 192) return false;
-  if ((EPI == EPI_BF16_T || EPI == EPI_BF16_TP32) && g.M % 4) return false;
-  static const bool off = getenv("SA_GEMM_DEFER") && atoi(getenv("SA_GEMM_DEFER")) == 0;  // read once
-  return !off;
-}
+constexpr int KERNEL_MAX = 9;  // (10, the s10 deferred-epilogue kernel, was measured slower and removed: DESIGN.md)
 
 // dynamic-LDS opt-in of one persistent instantiation, once per process
 template <int EPI, bool PANEL, int MI, int SCHED, bool NOEPI = false>
@@ -1641,27 +1202,6 @@ int launch(const GemmArgs& g_in, int batch, int kernel, hipStream_t st) {
       return SA_OK;
     }
     return SA_ERR_ARG;
-  }
-  if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_RES_F32 || EPI == EPI_BF16_T ||
-                EPI == EPI_BF16_TP32) {
-    // kernel 10 forces the deferred epilogue (A/B); auto keeps s9
-    constexpr bool auto_epi = false;  // s10 is selectable (kernel 10) but not picked by auto: see DESIGN.md
-    if (kernel == KERNEL_S10 || (kernel == KERNEL_AUTO && auto_epi && s10_ok<EPI>(g))) {
-      if (!s10_ok<EPI>(g)) return SA_ERR_ARG;
-      if (g.group_m == 0) g.group_m = EPI == EPI_RES_F32 ? 4 : 8;
-      const int tiles = ((g.M + 191) / 192) * ((g.N + BN - 1) / BN) * batch;
-      static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)gemm_s10_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  S7_LDS);
-        return true;
-      }();
-      (void)attr;
-      hipLaunchKernelGGL((gemm_s10_kernel<EPI>), dim3(min(tiles, num_cus())), dim3(256), S7_LDS, st, g, batch);
-      SA_LAUNCH_CHECK();
-      return SA_OK;
-    }
-  } else {
-    if (kernel == KERNEL_S10) return SA_ERR_ARG;
   }
   // auto (measured, profiles/r01/gemm_ab_r4.md): the persistent one-wave-per-SIMD LDS-DMA kernel
   // wherever its K % 128 tiling and 32-bit buffer offsets apply (over the ping-pong: QKV +8-15 %,
@@ -1786,14 +1326,3 @@ extern "C" int sa_gemm_bf16(const void* A, int64_t lda, int64_t strideA, const v
   return sa_gemm_bf16_ex(A, lda, strideA, W, ldw, strideW, bias, C, ldc, strideC, M, N, K, batch, epilogue, residual,
                          ldr, strideR, gate, gate_bstride, rows_per_batch, KERNEL_AUTO, 0, stream);
 }
-
-#ifdef SA_GEMM_STAMPS
-extern "C" int sa_debug_gemm_stamps(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gemm_stamps), sizeof(unsigned long long) * 8) != hipSuccess) return SA_ERR_ARG;
-  if (reset) {
-    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_stamps), z, sizeof(z)) != hipSuccess) return SA_ERR_ARG;
-  }
-  return SA_OK;
-}
-#endif

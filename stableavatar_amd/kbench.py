@@ -29,7 +29,7 @@ def vt_layout(v, mode, rows_pad=64):
     chunk in P's permuted order (position 8g + j <- key 4g + j for j < 4, 16 + 4g + j - 4 for j >= 4); mode 4: natural
     order.  Built by torch (tests / A-B only; the DiT's QKV GEMM writes it itself)."""
     R, HD = v.shape
-    Rv = (R + rows_pad - 1) // rows_pad * rows_pad
+    Rv = (R + rows_pad - 1) // rows_pad * rows_pad + 64  # + one 64-key block: a ragged last block stages all 64
     vt = torch.zeros(HD, Rv, device=v.device, dtype=v.dtype)
     vt[:, :R] = v.t()
     if mode == 3:
@@ -112,7 +112,7 @@ def main(which=("gemm", "attn")):
         q, k, v_ = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
         outs = {}
         variants = tuple(int(v) for v in os.environ.get("SA_KB_AVARS", "1").split(","))
-        vts = {m: vt_layout(v_, 3 if m in (5, 6) else m) for m in (3, 4, 5, 6) if m in variants}  # kernels 3-6 read V^T
+        vts = {m: vt_layout(v_, 3) for m in (3,) if m in variants}  # kernel 3 reads V^T
         times = {v: [] for v in variants}
         for rnd in range(3):
             for v in variants:

@@ -38,8 +38,6 @@ def _check(t, dtype, name):
 GEMM_AUTO, GEMM_PINGPONG, GEMM_PERSISTENT, GEMM_PERSISTENT192 = 0, 1, 2, 3
 # the persistent kernel on the three-barrier (s9) K schedule: tile rows by auto / 256 / 192
 GEMM_S9_AUTO, GEMM_S9, GEMM_S9_192 = 5, 6, 7
-# the persistent kernel with each tile's epilogue deferred under the next tile's K loop (192-row tiles, K = 1536)
-GEMM_S10 = 10
 
 
 def linear(x, weight, bias=None, epilogue=EPI_BF16, out=None, residual=None, gate=None, rows_per_batch=0,
@@ -66,8 +64,9 @@ def linear(x, weight, bias=None, epilogue=EPI_BF16, out=None, residual=None, gat
     assert weight.shape[1] == K and x.stride(1) == 1 and weight.stride(1) == 1
     f32_out = epilogue in (EPI_F32, EPI_RES_F32, EPI_SILU_F32)
     if epilogue in (EPI_BF16_T, EPI_BF16_TP32):  # out = C^T [N, >= M] (row n = column n of the product: V^T)
-        if out is None:
-            out = torch.empty(N, (M + 63) // 64 * 64, device=x.device, dtype=torch.bfloat16)
+        if out is None:  # zeroed: attention kernels 3 / 4 read the pad columns as masked keys (must be finite), and
+            # 64 columns past ceil64(M) cover the whole 64-key block a segment's ragged last block stages
+            out = torch.zeros(N, (M + 63) // 64 * 64 + 64, device=x.device, dtype=torch.bfloat16)
         if out.dtype != torch.bfloat16 or out.stride(1) != 1 or out.shape[0] != N or out.shape[1] < M:
             raise ValueError(f"linear: EPI_BF16_T(P32) needs out bf16 [N, >= M], got {tuple(out.shape)}")
     elif out is None:
@@ -101,9 +100,9 @@ def bmm_nt(a, b, out, epilogue=EPI_F32, kernel=GEMM_AUTO):
 
 
 ATTN_AUTO = 0
-# kernel ids of sa_attn_fwd_ex that read V as V^T [H*128, Rv]: 3 = keys permuted per 32 in P's order (the QKV GEMM's
-# EPI_BF16_TP32 output), 4 = natural order with the PV product on 32x32x16 MFMAs (measured slower, kept for A/B)
-ATTN_VT_P32, ATTN_VT_PV32, ATTN_VT_P32_3STAGE = 3, 4, 6  # 6: kernel 3 on a 3-stage K/V ring (A/B)
+# kernel id of sa_attn_fwd_ex that reads V as V^T [H*128, Rv]: keys permuted per 32 in P's order (the QKV GEMM's
+# EPI_BF16_TP32 output)
+ATTN_VT_P32 = 3
 
 
 def attention(q, k, v, out, segs, nseg, max_q_len, heads, head_dim=128, scale=None, accumulate=False,

@@ -65,8 +65,12 @@ def make_plan(world: int, rank: int, heads: int) -> SPPlan:
     return SPPlan(world, rank, heads, G, world // G)
 
 
-def _panel_slack_rows() -> int:
-    """Rows the column-panel O-projection may read past its last panel (sa_gemm_panel_slack_rows)."""
+def _panel_slack_rows(device) -> int:
+    """Rows the column-panel O-projection may read past its last panel (sa_gemm_panel_slack_rows).  Only a GPU
+    exchange runs that GEMM: on the CPU (the gloo protocol tests) no slack is needed and the HIP library is not
+    loaded."""
+    if torch.device(device).type != "cuda":
+        return 0
     from . import _lib
     return int(_lib.lib().sa_gemm_panel_slack_rows())
 
@@ -174,7 +178,7 @@ class UlyssesExchange:
         # On the per-row-stream path (transformer._sp_layer_rows) row b's O-projection tail tile also reads
         # into row b+1's panel region while another stream may be writing it: benign, those rows' products are
         # discarded (never stored), only their bytes are fetched.
-        self.obuf = torch.empty(2 * G * B * Lc + _panel_slack_rows(), hgd, device=device, dtype=dtype)
+        self.obuf = torch.empty(2 * G * B * Lc + _panel_slack_rows(device), hgd, device=device, dtype=dtype)
         self.pan = self.obuf[G * B * Lc:2 * G * B * Lc]
         self.remote = [d for d in range(N) if d != p.rank or self.loopback]
         self.sq = {d: torch.empty(B, Lc, hgd, device=device, dtype=dtype) for d in self.remote if d // G == p.part}

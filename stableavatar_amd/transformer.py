@@ -825,8 +825,9 @@ class WanTransformer3DFantasyModel(nn.Module):
             x = ws.x
             use_vt = not SP and self._vt_attention(Lp, dev)
             if use_vt and ws.vt is None:
-                # zero-filled once: the pad columns past B * Lp are read (as P = 0 keys) by a partial last block
-                ws.vt = torch.zeros(dim, (ws.x.shape[0] + 63) // 64 * 64, device=dev, dtype=torch.bfloat16)
+                # zero-filled once: the pad columns past B * Lp are read (as P = 0 keys) by a partial last block, which
+                # stages a whole 64-key block: up to (B-1)*Lp + ceil64(Lp) <= ceil64(M) + 64 columns
+                ws.vt = torch.zeros(dim, (ws.x.shape[0] + 63) // 64 * 64 + 64, device=dev, dtype=torch.bfloat16)
             kvv = torch.empty(B * n_fr * nper, 2 * dim, device=dev, dtype=torch.bfloat16)  # per-frame vocal K|V
             grid = (Fw, hp, wp)
             if sp_streams:

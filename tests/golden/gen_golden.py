@@ -230,6 +230,13 @@ def gen_pipeline_log():
     gen_pipeline(PIPE_LOG, "pipeline_log", scheme="log")
 
 
+def gen_pipeline_steps():
+    """the reference __call__ over 5 / 10 / 50 steps (golden_cases.PIPE_STEPS): pipeline_s05/s10/s50.npz"""
+    from golden_cases import PIPE_STEPS
+    for n, P in PIPE_STEPS.items():
+        gen_pipeline(P, f"pipeline_s{n:02d}")
+
+
 def gen_keys():
     """state_dict key -> shape of the reference modules the checkpoint loaders fill: the 1.3B DiT
     (WanTransformer3DFantasyModel at the wan_civitai.yaml / Wan2.1-1.3B dims), the full VAE

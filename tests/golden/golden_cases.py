@@ -80,6 +80,11 @@ PIPE = dict(dit=dict(DIT_SMALL, num_layers=1, seed=31), vae=dict(dim=32, seed=32
 # the "log" overlap blend (pipeline:761-766) needs overlap >= 3 to differ from the uniform ramp
 PIPE_LOG = dict(PIPE, overlap=3)
 
+# SURVEY.md §8(d)'s end-to-end contract at the reference's real step count: the reference __call__
+# (wan_inference_long_pipeline.py:540-806) over 5 / 10 / 50 sampling steps of its own schedule, 2-layer
+# dim-1536 DiT, 2 windows per step, injected noise -> the bf16 drift's growth with the step count
+PIPE_STEPS = {n: dict(PIPE, dit=dict(DIT_SMALL, seed=71), vae=dict(dim=32, seed=72), steps=n) for n in (5, 10, 50)}
+
 
 # BASELINE config 1: the full Wan-1.3B StableAvatar DiT (30 layers, dim 1536, ffn 8960,
 # text_dim 4096) and the full-width VAE (dim 96) at 256x256, clip 17 (5 latent frames), 5 sampling steps,

@@ -3,7 +3,6 @@ the HIP clip: rank/world handling, the barrier-bracketed timing with the max ove
 for N > 1 with the extra `replicas` key, the per-row attention-span accounting and the JSON line."""
 import json
 import os
-import socket
 import sys
 
 import torch
@@ -14,14 +13,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 import bench  # noqa: E402
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
 
 
 class _Ev:
@@ -78,8 +69,9 @@ class FakeClip:
         return self.args.sample_steps * len(self.wins)
 
 
-def _worker(rank, world, port, argv, path):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+def _worker(rank, world, store, argv, path):
+    # a file:// rendezvous: nothing to bind, so no port is picked and released (a race with other listeners)
+    os.environ.update(SA_DIST_INIT_METHOD="file://" + store, RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     out = open(path + f".{rank}", "w")
     sys.stdout = out
@@ -91,7 +83,7 @@ def _worker(rank, world, port, argv, path):
 
 def _run(world, argv, tmp_path):
     path = str(tmp_path / "bench")
-    mp.start_processes(_worker, args=(world, _free_port(), argv, path), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, str(tmp_path / "store"), argv, path), nprocs=world, join=True,
                        start_method="spawn")
     lines = [open(path + f".{r}").read().strip() for r in range(world)]
     assert all(not ln for ln in lines[1:]), "only rank 0 prints"

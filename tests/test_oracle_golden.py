@@ -97,13 +97,15 @@ def test_vae_encode_flops():
     assert abs(ovae.flops_encode(81, 512, 512) / 1e12 - 107.2) < 0.1
 
 
-@pytest.mark.parametrize("case", ["uniform", "log"])
+@pytest.mark.parametrize("case", ["uniform", "log", "s50"])
 def test_pipeline_vs_reference(case):
     """the restated loop vs the reference's __call__; "log" = overlapping_weight_scheme="log" (pipeline:761-766)
-    at overlap 3, where its ramp differs from the uniform one"""
-    from golden_cases import PIPE_LOG
-    P = PIPE if case == "uniform" else PIPE_LOG
-    g = G("pipeline_small.npz" if case == "uniform" else "pipeline_log.npz")
+    at overlap 3, where its ramp differs from the uniform one; "s50" = the reference's full 50-step loop
+    (2-layer DiT, 100 forwards) -- the oracle that the HIP 50-step test is also checked against"""
+    from golden_cases import PIPE_LOG, PIPE_STEPS
+    P = {"uniform": PIPE, "log": PIPE_LOG, "s50": PIPE_STEPS[50]}[case]
+    g = G({"uniform": "pipeline_small.npz", "log": "pipeline_log.npz", "s50": "pipeline_s50.npz"}[case])
+    case = "log" if case == "log" else "uniform"
     Pd = synthetic.fill_state_dict(odit.param_shapes(P["dit"]), P["dit"]["seed"])
     Pv = synthetic.fill_state_dict(ovae.param_shapes(dim=P["vae"]["dim"]), P["vae"]["seed"])
     fx = pipe_fixed_inputs(P)

@@ -2,7 +2,7 @@
 sequence of causal-cache points, takes each cache from rank r-1 and passes its update to rank r+1, in order;
 skipped points forward the previous cache; the frame gather returns every rank's block in rank order."""
 import os
-import socket
+import tempfile
 import sys
 
 import pytest
@@ -15,17 +15,16 @@ sys.path.insert(0, HERE)
 from mp_util import collect  # noqa: E402
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+def _store():
+    """a file:// rendezvous path (nothing to bind: no free port picked and released)"""
+    fd, path = tempfile.mkstemp(prefix="sa_store_")
+    os.close(fd)
+    os.unlink(path)
+    return path
 
 
-def _worker(rank, world, port, qret):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, store, qret):
+    dist.init_process_group("gloo", init_method="file://" + store, rank=rank, world_size=world)
     try:
         from stableavatar_amd.vae import _all_gather, _ChainState, _SeqState
         # 3 "frames" per rank at every cache point; the update keeps the last two; rank r's frames hold r
@@ -56,8 +55,8 @@ def _worker(rank, world, port, qret):
 def test_chain_protocol(world):
     ctx = mp.get_context("spawn")
     qret = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, qret)) for r in range(world)]
+    store = _store()
+    procs = [ctx.Process(target=_worker, args=(r, world, store, qret)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(collect(procs, qret, world))
@@ -75,9 +74,8 @@ def test_chain_protocol(world):
         assert g == [[[float(i)] * 3] * 2 for i in range(world)]
 
 
-def _loop_worker(port, n, qret):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=0, world_size=1)
+def _loop_worker(store, n, qret):
+    dist.init_process_group("gloo", init_method="file://" + store, rank=0, world_size=1)
     try:
         import collections
         from stableavatar_amd.vae import _LoopbackChain
@@ -109,7 +107,7 @@ def test_chain_protocol_loopback():
     hand-off sequence as 3 real ranks, every cache passed through a transfer to the rank itself"""
     ctx = mp.get_context("spawn")
     qret = ctx.Queue()
-    p = ctx.Process(target=_loop_worker, args=(_free_port(), 3, qret))
+    p = ctx.Process(target=_loop_worker, args=(_store(), 3, qret))
     p.start()
     (res, left), = collect([p], qret, 1)
     p.join(timeout=60)
