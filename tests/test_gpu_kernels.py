@@ -99,7 +99,7 @@ def test_gemm_kernels(kernel, M, N, K):
 
 @pytest.mark.parametrize("M,N,K", [(1000, 384, 1536), (64512 // 8, 1536, 1536), (300, 130, 256)])
 def test_gemm_transposed_output(M, N, K):
-    """EPI_BF16_T (the QKV GEMM's V^T output for self-attention kernel 4): C^T[n, m] = bf16(x @ w^T + b)[m, n] vs the
+    """EPI_BF16_T (the QKV GEMM's V^T output in natural key order): C^T[n, m] = bf16(x @ w^T + b)[m, n] vs the
     row-major epilogue, ragged M / N tiles; the pad columns past M are left untouched"""
     from stableavatar_amd import ops
     x = torch.randn(M, K, device=dev).bfloat16()
@@ -115,7 +115,7 @@ def test_gemm_transposed_output(M, N, K):
     assert (out[:, M:] == 7.0).all()
     # P32: the rows of each 32-row chunk in the attention's P order = kbench.vt_layout(y, 3)
     from stableavatar_amd.kbench import vt_layout
-    outp = torch.zeros(N, Rv, device=dev, dtype=torch.bfloat16)
+    outp = torch.zeros(N, Rv + 64, device=dev, dtype=torch.bfloat16)  # vt_layout's width: ceil64(M) + 64
     ops.linear(x, w, b, ops.EPI_BF16_TP32, out=outp)
     assert torch.equal(outp, vt_layout(out[:, :M].t().contiguous(), 3))
 
@@ -172,11 +172,12 @@ def test_attention_segments(Lq, Lk, kernel):
     assert rel(o2, 2 * o.float()) < 1e-2
 
 
-@pytest.mark.parametrize("kernel", [3], ids=["v6t_vt_perm32"])
+@pytest.mark.parametrize("kernel", [3, 4], ids=["v6t_vt_perm32", "v6p_pipelined"])
 @pytest.mark.parametrize("B,Lq,Lk", [(2, 300, 320), (2, 512, 256), (1, 256, 1000), (3, 64, 64), (1, 256, 128)])
 def test_attention_vt_kernels(kernel, B, Lq, Lk):
-    """the self-attention form that reads V as V^T [H*128, Rv] (kernel 3: keys permuted per 32 as P) vs fp32 torch,
-    incl. a ragged last key block and accumulate"""
+    """the self-attention forms that read V as V^T [H*128, Rv] (kernel 3: keys permuted per 32 as P; 4: the same block
+    arithmetic software-pipelined across blocks, bit-identical to 3) vs fp32 torch, incl. a ragged last key block and
+    accumulate"""
     from stableavatar_amd import ops
     from stableavatar_amd.kbench import vt_layout
     H, D = 3, 128
@@ -195,9 +196,13 @@ def test_attention_vt_kernels(kernel, B, Lq, Lk):
     o2 = o.clone()
     ops.attention(q, k, vt, o2, segs, B, Lq, H, accumulate=True, kernel=kernel)
     assert rel(o2, 2 * o.float()) < 1e-2
+    if kernel != 3:
+        o3 = torch.empty_like(o)
+        ops.attention(q, k, vt, o3, segs, B, Lq, H, kernel=3)
+        assert torch.equal(o3, o)
 
 
-@pytest.mark.parametrize("kernel", [3], ids=["v6t_vt_perm32"])
+@pytest.mark.parametrize("kernel", [3, 4], ids=["v6t_vt_perm32", "v6p_pipelined"])
 def test_attention_vt_spike_rescale(kernel):
     """the rescale branch of the V^T form"""
     from stableavatar_amd import ops
@@ -214,6 +219,9 @@ def test_attention_vt_spike_rescale(kernel):
     o = torch.empty_like(q)
     segs = torch.tensor([[0, L, 0, L]], dtype=torch.int32, device=dev)
     ops.attention(q, k, vt_layout(v, 3), o, segs, 1, L, 1, kernel=kernel)
+    o3 = torch.empty_like(q)
+    ops.attention(q, k, vt_layout(v, 3), o3, segs, 1, L, 1, kernel=3)
+    assert torch.equal(o3, o)
     ref = _ref_attn(q, k, v, D ** -0.5)
     assert rel(o, ref) < 1e-2
     for r in (5, 9, 17, 20):
@@ -351,9 +359,9 @@ def test_attention_vt_ragged_batch_stays_inside_allocation():
                             D ** -0.5)
             assert rel(o[b * Lq:(b + 1) * Lq, sl], ref) < 1e-2, (b, h)
     # the default V^T output of ops.linear(EPI_BF16_TP32) has the same width and a zeroed pad
-    x = torch.randn(B * Lk, 64, device=dev).bfloat16()
-    w = torch.randn(H * D, 64, device=dev).bfloat16()
-    vt2 = ops.linear(x, w, None, ops.EPI_BF16_TP32)
+    x = torch.randn(B * Lk, 256, device=dev).bfloat16()
+    w = torch.randn(H * D, 256, device=dev).bfloat16()
+    vt2 = ops.linear(x, w, torch.zeros(H * D, device=dev), ops.EPI_BF16_TP32)
     torch.cuda.synchronize()
     assert vt2.shape == vt0.shape and torch.count_nonzero(vt2[:, B * Lk:]).item() == 0
 

@@ -4,7 +4,9 @@ gather) must reproduce the single-GPU loop BIT-EXACTLY: 2 ranks x 3 windows per 
 second round) and 3 ranks x 8 windows per step (26 latent frames, uneven last round); the 8-window run is also
 checked against the CPU oracle's restatement of the reference loop (oracle/pipeline.py, pinned to the
 reference's __call__ goldens) at the pipeline tolerance (latents rel-L2 <= 3e-2); 8 ranks x 17 windows per step
-(53 latent frames) is config 5's rank count, also against the oracle loop."""
+(53 latent frames) is config 5's rank count, also against the oracle loop; and config 5's LENGTH: T_lat 251 (1 001
+video frames) with the reference's 81-frame windows at overlap 10 = 22 windows per step over 8 ranks (SURVEY.md §8(d)
+config 5), on the small 8x8-latent DiT, bit-exact vs one GPU and against the oracle loop."""
 import math
 import os
 import sys
@@ -31,9 +33,8 @@ def _free_port():
     return os.path.join(tempfile.mkdtemp(prefix="sa_rdv_"), "store")
 
 
-def _inputs(T):
-    from golden_cases import PIPE
-    fpb = (PIPE["clip_length"] - 1) // 4 + 1
+def _inputs(T, clip_length=17):
+    fpb = (clip_length - 1) // 4 + 1
     g = torch.Generator().manual_seed(5)
     lat = torch.randn(1, 16, T, 8, 8, generator=g)
     y = torch.randn(3, 20, fpb, 8, 8, generator=g)
@@ -44,16 +45,14 @@ def _inputs(T):
     return lat, y, ctx, clip, audio
 
 
-def _run(pipe, T, window_parallel):
+def _run(pipe, T, window_parallel, clip_length=17, overlap=2):
     from stableavatar_amd import synthetic
     from stableavatar_amd.pipeline import audio_window, window_schedule
     from stableavatar_amd.scheduler import FlowMatchEulerDiscreteScheduler
-    from golden_cases import PIPE
-    P = PIPE
-    fpb = (P["clip_length"] - 1) // 4 + 1
-    lat, y, ctx, clip, audio = _inputs(T)
+    fpb = (clip_length - 1) // 4 + 1
+    lat, y, ctx, clip, audio = _inputs(T, clip_length)
     feats = {}
-    for (s, e, _) in window_schedule(T, fpb, P["overlap"]):
+    for (s, e, _) in window_schedule(T, fpb, overlap):
         a = synthetic.fake_wav2vec_features(audio[audio_window(s, e, T, 640, audio.shape[0])][None])
         feats[(s, e)] = torch.cat([torch.zeros_like(a), a, a]).cuda()
     sched = FlowMatchEulerDiscreteScheduler(1000, shift=5.0)
@@ -64,13 +63,13 @@ def _run(pipe, T, window_parallel):
     seq_len = math.ceil(8 * 8 / 4 * fpb)
     with torch.no_grad():
         out = pipe.denoise(lat.cuda(), y.cuda(), [c.cuda() for c in ctx], clip.cuda(), feats, sched.timesteps,
-                           sched.sigmas, clip_length=P["clip_length"], seq_len=seq_len, overlap=P["overlap"],
+                           sched.sigmas, clip_length=clip_length, seq_len=seq_len, overlap=overlap,
                            text_guide_scale=3.0, audio_guide_scale=5.0)
     torch.cuda.synchronize()
     return out.cpu()
 
 
-def _worker(rank, world, port, T, qret):
+def _worker(rank, world, port, T, qret, clip_length=17, overlap=2):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     import torch.distributed as dist
     from golden_cases import PIPE
@@ -83,15 +82,15 @@ def _worker(rank, world, port, T, qret):
         dit = WanTransformer3DFantasyModel(**{k: v for k, v in dcfg.items() if k != "seed"})
         dit.load_state_dict(synthetic.fill_state_dict(param_shapes(dcfg), dcfg["seed"]))
         pipe = WanI2VTalkingInferenceLongPipeline(transformer=dit.cuda())
-        single = _run(pipe, T, False)
-        par = _run(pipe, T, True)
+        single = _run(pipe, T, False, clip_length, overlap)
+        par = _run(pipe, T, True, clip_length, overlap)
         qret.put((rank, bool(torch.equal(single, par)), float((single.float() - par.float()).abs().max()),
                   par if rank == 0 else None))
     finally:
         dist.destroy_process_group()
 
 
-def _oracle_loop(T):
+def _oracle_loop(T, clip_length=17, overlap=2):
     """the reference loop (pipeline:703-790) restated on the CPU with the oracle DiT"""
     from oracle import dit as odit
     from oracle import pipeline as opipe
@@ -99,7 +98,7 @@ def _oracle_loop(T):
     from golden_cases import PIPE
     P = PIPE
     Pd = synthetic.fill_state_dict(odit.param_shapes(P["dit"]), P["dit"]["seed"])
-    lat, y, ctx, clip, audio = _inputs(T)
+    lat, y, ctx, clip, audio = _inputs(T, clip_length)
 
     def dit(x, t, context, seq_len, yy, clip_fea, vocal, n):
         return odit.forward(Pd, P["dit"], x.to(torch.bfloat16).float(), t, context, seq_len, clip_fea,
@@ -108,21 +107,24 @@ def _oracle_loop(T):
     enc = lambda s: synthetic.fake_wav2vec_features(torch.as_tensor(s)[None])  # noqa: E731
     with torch.no_grad():
         return opipe.denoise(dit, lat.to(torch.bfloat16).float(), y, ctx, clip, audio, enc,
-                             num_inference_steps=STEPS, clip_length=P["clip_length"], num_frames=P["clip_length"],
-                             height=64, width=64, overlap=P["overlap"], text_guide_scale=3.0, audio_guide_scale=5.0)
+                             num_inference_steps=STEPS, clip_length=clip_length, num_frames=clip_length,
+                             height=64, width=64, overlap=overlap, text_guide_scale=3.0, audio_guide_scale=5.0)
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("world,T", [(2, 9), (3, 26), (8, 53)])
-def test_window_parallel_bit_exact(world, T):
-    """(8, 53): config 5's rank count, 17 windows per step (3 rounds over 8 ranks, 1 window in the last)"""
+@pytest.mark.parametrize("world,T,clip_length,overlap", [(2, 9, 17, 2), (3, 26, 17, 2), (8, 53, 17, 2),
+                                                         (8, 251, 81, 10)])
+def test_window_parallel_bit_exact(world, T, clip_length, overlap):
+    """(8, 53): config 5's rank count, 17 windows per step (3 rounds over 8 ranks, 1 window in the last);
+    (8, 251, 81, 10): config 5's length -- 1 001 frames in 81-frame windows at overlap 10, 22 windows per step
+    (pipeline:714-789), 3 rounds over 8 ranks with 6 windows in the last"""
     from stableavatar_amd.pipeline import window_schedule
-    n_win = len(window_schedule(T, 5, 2))
-    assert n_win == {9: 3, 26: 8, 53: 17}[T]
+    n_win = len(window_schedule(T, (clip_length - 1) // 4 + 1, overlap))
+    assert n_win == {9: 3, 26: 8, 53: 17, 251: 22}[T]
     ctx = mp.get_context("spawn")
     qret = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, T, qret)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, T, qret, clip_length, overlap)) for r in range(world)]
     for p in procs:
         p.start()
     res = collect(procs, qret, world, timeout=540)
@@ -133,7 +135,7 @@ def test_window_parallel_bit_exact(world, T):
         assert same, (rank, mx)
     if T >= 26:
         par = next(r[3] for r in res if r[0] == 0).float()
-        ref = _oracle_loop(T)
+        ref = _oracle_loop(T, clip_length, overlap)
         e = ((par - ref).norm() / ref.norm()).item()
         print(f"window-parallel {world} ranks, {n_win} windows/step: vs oracle loop rel-L2 {e:.2e}")
         assert e <= 3e-2, e
