@@ -893,153 +893,12 @@ __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
   }
 }
 
-// ---- v6p (kernel 4): the v6t block loop software-pipelined across blocks inside each wave (cdna_hip_programming.md
-// T15).  In v6t every block runs QK^T -> softmax -> PV in order and all 8 waves pass one barrier per block, so the
-// two waves of a SIMD reach their softmax together and the matrix pipe idles through both (3 120 cycles per block per
-// SIMD against 2 176 of MFMA work, profiles/r05/attn_v6t_barrier_anatomy_r5.jsonl).  Here iteration j holds two
-// score sets: phase A issues block j+1's QK^T (32 MFMAs) with block j's exponentials and bf16 packing between them,
-// phase B block j's PV and row sums (36 MFMAs) with block j+1's rescale vote between them, so each wave's own MFMAs
-// cover its VALU work.  The rescale of block j (rare) runs at the top of iteration j, before block j+1's QK^T takes
-// the running max as its initial accumulator: every element sees the arithmetic of v6t in the same order
-// (bit-identical).  K ring: block b in K slot b % 2 (0 / 16 KB), V ring: block b in V slot b % 2 (32 / 48 KB); at the
-// barrier of iteration j, K_{j+1} and V_j (issued one iteration earlier) have landed and the slots of K_j (read in
-// iteration j-1's phase A) and V_{j-1} (its phase B) take the DMA of K_{j+2} and V_{j+1}.
-
-// the bf16 P operand of chunk C (key tiles 2C, 2C+1) from the exponentiated scores
-template <int C>
-__device__ __forceinline__ void v6p_pack(const f32x4 (&Sc)[4][2], bf16x8 (&pb)[2][2]) {
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      pb[C][qt][j] = f2bf(Sc[2 * C][qt][j]);
-      pb[C][qt][4 + j] = f2bf(Sc[2 * C + 1][qt][j]);
-    }
-}
-
-// key tile KT of phase A as one hand-placed stream: the tile's 8 QK^T MFMAs (the chains of v6_mma_k in the same order,
-// the first of each chain taking -m as C), each followed by one exponential of the previous block's tile KT.  hipcc
-// schedules an asm statement as one instruction, so the MFMA / exponential alternation is kept (cdna_hip_programming.md
-// §5.7; MI355X_MICROARCH.md: MFMA + v_exp = 8 + 8 issue cycles fill one 16x16x32 gap).  s_nop 1 opens the stream (a
-// VALU-written -m or Q register read as an MFMA operand); LAST ends it with 12 wait states (the MFMA results are read by
-// VALU code hipcc places after it)
-template <bool LAST>
-__device__ __forceinline__ void v6p_tile_asm(f32x4 (&Sn)[2], f32x4 (&Sc)[2], const u32x4* k, const bf16x8 (&qf)[2][4],
-                                             const f32x4 (&negm4)[2]) {
-  asm volatile(
-      "s_nop 1\n\t"
-      "v_mfma_f32_16x16x32_bf16 %[s0], %[k0], %[q00], %[n0]\n\tv_exp_f32 %[e0], %[e0]\n\t"
-      "v_mfma_f32_16x16x32_bf16 %[s1], %[k0], %[q10], %[n1]\n\tv_exp_f32 %[e1], %[e1]\n\t"
-      "v_mfma_f32_16x16x32_bf16 %[s0], %[k1], %[q01], %[s0]\n\tv_exp_f32 %[e2], %[e2]\n\t"
-      "v_mfma_f32_16x16x32_bf16 %[s1], %[k1], %[q11], %[s1]\n\tv_exp_f32 %[e3], %[e3]\n\t"
-      "v_mfma_f32_16x16x32_bf16 %[s0], %[k2], %[q02], %[s0]\n\tv_exp_f32 %[e4], %[e4]\n\t"
-      "v_mfma_f32_16x16x32_bf16 %[s1], %[k2], %[q12], %[s1]\n\tv_exp_f32 %[e5], %[e5]\n\t"
-      "v_mfma_f32_16x16x32_bf16 %[s0], %[k3], %[q03], %[s0]\n\tv_exp_f32 %[e6], %[e6]\n\t"
-      "v_mfma_f32_16x16x32_bf16 %[s1], %[k3], %[q13], %[s1]\n\tv_exp_f32 %[e7], %[e7]"
-      : [s0] "=&v"(Sn[0]), [s1] "=&v"(Sn[1]), [e0] "+v"(Sc[0][0]), [e1] "+v"(Sc[0][1]), [e2] "+v"(Sc[0][2]),
-        [e3] "+v"(Sc[0][3]), [e4] "+v"(Sc[1][0]), [e5] "+v"(Sc[1][1]), [e6] "+v"(Sc[1][2]), [e7] "+v"(Sc[1][3])
-      : [k0] "v"(k[0]), [k1] "v"(k[1]), [k2] "v"(k[2]), [k3] "v"(k[3]), [q00] "v"(qf[0][0]), [q01] "v"(qf[0][1]),
-        [q02] "v"(qf[0][2]), [q03] "v"(qf[0][3]), [q10] "v"(qf[1][0]), [q11] "v"(qf[1][1]), [q12] "v"(qf[1][2]),
-        [q13] "v"(qf[1][3]), [n0] "v"(negm4[0]), [n1] "v"(negm4[1]));
-  if constexpr (LAST) asm volatile("s_nop 7\n\ts_nop 3" ::: "memory");
-}
-
-// phase A: NEXT: block j+1's S'^T = c K Q^T - m into Sn (K stage at KOFF), block j's exponentials between its MFMAs
-// and its bf16 P packed after each key-tile pair; !NEXT (last block): the exponentials and packing only
-template <int KOFF, bool NEXT>
-__device__ __forceinline__ void v6p_phase_a(f32x4 (&Sn)[4][2], f32x4 (&Sc)[4][2], bf16x8 (&pb)[2][2],
-                                            const f32x4 (&negm4)[2], const bf16x8 (&qf)[2][4], const uint32_t* ka) {
-  if constexpr (NEXT) {
-    u32x4 k0[4], k1[4];
-    v6_read_k<KOFF, 0>(k0, ka);
-    v6_read_k<KOFF, 1>(k1, ka);
-    wait_k4<4>(k0);
-    v6p_tile_asm<false>(Sn[0], Sc[0], k0, qf, negm4);
-    v6_read_k<KOFF, 2>(k0, ka);
-    wait_k4<4>(k1);
-    v6p_tile_asm<false>(Sn[1], Sc[1], k1, qf, negm4);
-    v6p_pack<0>(Sc, pb);
-    v6_read_k<KOFF, 3>(k1, ka);
-    wait_k4<4>(k0);
-    v6p_tile_asm<false>(Sn[2], Sc[2], k0, qf, negm4);
-    wait_k4<0>(k1);
-    v6p_tile_asm<true>(Sn[3], Sc[3], k1, qf, negm4);
-    v6p_pack<1>(Sc, pb);
-  } else {
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) Sc[kt][qt][i] = __builtin_amdgcn_exp2f(Sc[kt][qt][i]);
-    v6p_pack<0>(Sc, pb);
-    v6p_pack<1>(Sc, pb);
-  }
-}
-
-// phase B: block j's O^T += V^T P^T and row sums (V stage at VOFF); NEXT: block j+1's rescale vote between them
-template <int VOFF, bool NEXT>
-__device__ __forceinline__ bool v6p_phase_b(V6State& st, const bf16x8 (&pb)[2][2], const f32x4 (&Sn)[4][2],
-                                            const uint32_t* vb) {
-  u32x4 v0[4], v1[4];
-  v6t_read_v<VOFF, 0, 0>(v0, vb);
-  v6t_read_v<VOFF, 0, 4>(v1, vb);
-  bf16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
-  float lm = 0.f;
-  // chunk 0
-  st.L[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[0][0], st.L[0], 0, 0, 0);
-  st.L[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[0][1], st.L[1], 0, 0, 0);
-  wait_k4<4>(v0);
-  v6t_mma_v(st.O, 0, v0, pb[0]);
-  v6t_read_v<VOFF, 1, 0>(v0, vb);
-  if constexpr (NEXT) lm = lanemax32(Sn);
-  wait_k4<4>(v1);
-  v6t_mma_v(st.O, 4, v1, pb[0]);
-  v6t_read_v<VOFF, 1, 4>(v1, vb);
-  // chunk 1
-  st.L[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[1][0], st.L[0], 0, 0, 0);
-  st.L[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[1][1], st.L[1], 0, 0, 0);
-  wait_k4<4>(v0);
-  v6t_mma_v(st.O, 0, v0, pb[1]);
-  wait_k4<0>(v1);
-  v6t_mma_v(st.O, 4, v1, pb[1]);
-  return NEXT && !__all(lm <= RESCALE_THR);  // wave-uniform
-}
-
-// the deferred rescale of a block whose vote failed (v6_softmax_rescale's non-first branch)
-__device__ __forceinline__ void v6p_rescale(V6State& st, f32x4 (&S)[4][2]) {
-  float mx[2], alpha[2];
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) mx[qt] = rowmax64(S, qt);
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const float delta = fmaxf(mx[qt], 0.f);
-    alpha[qt] = __builtin_amdgcn_exp2f(-delta);
-    st.L[qt] *= alpha[qt];
-    st.negm[qt] -= delta;
-    st.negm4[qt] = (f32x4){st.negm[qt], st.negm[qt], st.negm[qt], st.negm[qt]};
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) S[kt][qt][i] -= delta;
-  }
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) st.O[dt][qt][i] *= alpha[qt];
-}
-
 // self-attention reading V as V^T (attn_v6t_block above): 8 waves x 32 queries, the v6 ring and K staging.
 // a.v = V^T [heads * 128][Rv] bf16 (row h*128 + d, keys permuted per 32 as P; a.vs = Rv >= the columns any
 // segment's last 64-key block reaches, i.e. kv_row0 + ceil64(kv_len); segments start on 32-key boundaries; every
 // element of a row readable and finite through that block: the partial last block reads the keys past kv_len,
 // masked to P = 0).  2-stage K/V ring: block kb+1's DMA issued at block kb (one block of lead, vmcnt(0) +
 // __syncthreads() per block).
-template <bool PIPE>
 __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
   constexpr int NW = 8, QBW = NW * 32, PPW = 16 / NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1097,24 +956,7 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
     voff[i] = d * (int)a.vs * 2 + (((lane & 7) ^ (d & 7)) << 4);
   }
   const uint32_t lds_dma = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + dw * PPW * 1024);
-  // K / V tile of block kb into the LDS region at byte kdst / vdst (v6t: 2 stages as K | V pairs; v6p: K slots at
-  // 0 / 16 KB, V slots at 32 / 48 KB)
-  auto stage_k = [&](int kb, int kdst) {
-    const bool tail = ragged && kb == nkb - 1;
-    const int ks_off = tail ? 0 : kb * KVB * (int)a.ks * 2;
-    const __amdgpu_buffer_rsrc_t bk = tail ? rkt : rk;
-#pragma unroll
-    for (int i = 0; i < PPW; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(bk, LDS_PTR((uintptr_t)(lds_dma + kdst + i * 1024)), 16, koff[i],
-                                               ks_off, 0, 0);
-  };
-  auto stage_v = [&](int kb, int vdst) {
-#pragma unroll
-    for (int i = 0; i < PPW; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, LDS_PTR((uintptr_t)(lds_dma + vdst + i * 1024)), 16, voff[i],
-                                               kb * KVB * 2, 0, 0);
-  };
-  auto stage = [&](int kb, int buf) {  // both tiles of block kb, K / V pieces interleaved
+  auto stage = [&](int kb, int buf) {  // LDS: 2 stages as K | V pairs
     const bool tail = ragged && kb == nkb - 1;
     const int ks_off = tail ? 0 : kb * KVB * (int)a.ks * 2, vs_off = kb * KVB * 2;
     const __amdgpu_buffer_rsrc_t bk = tail ? rkt : rk;
@@ -1132,7 +974,7 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
 #pragma unroll
   for (int dc = 0; dc < 4; ++dc) ka[dc] = lds0 + r16 * 256 + (((dc * 4 + g) ^ r16) << 4);
 #pragma unroll
-  for (int c = 0; c < 2; ++c) vb[c] = lds0 + (PIPE ? 2 * TILE_BYTES : 0) + r16 * 128 + (((4 * c + g) ^ (r16 & 7)) << 4);
+  for (int c = 0; c < 2; ++c) vb[c] = lds0 + r16 * 128 + (((4 * c + g) ^ (r16 & 7)) << 4);
 
   V6State st;
 #pragma unroll
@@ -1146,76 +988,19 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   };
-  if constexpr (!PIPE) {
-    stage(0, 0);
-    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  stage(0, 0);
+  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  sync();
+  if (1 < nkb) stage(1, 1);
+  attn_v6t_block<0, TILE_BYTES, true>(st, qf, ka, vb, 0, kv_len, g);
+  for (int kb = 1; kb < nkb; kb += 2) {
     sync();
-    if (1 < nkb) stage(1, 1);
-    attn_v6t_block<0, TILE_BYTES, true>(st, qf, ka, vb, 0, kv_len, g);
-    for (int kb = 1; kb < nkb; kb += 2) {
-      sync();
-      if (kb + 1 < nkb) stage(kb + 1, 0);
-      attn_v6t_block<STAGE_BYTES, STAGE_BYTES + TILE_BYTES, false>(st, qf, ka, vb, kb, kv_len, g);
-      if (kb + 1 >= nkb) break;
-      sync();
-      if (kb + 2 < nkb) stage(kb + 2, 1);
-      attn_v6t_block<0, TILE_BYTES, false>(st, qf, ka, vb, kb + 1, kv_len, g);
-    }
-  } else {
-    constexpr int K0 = 0, K1 = TILE_BYTES, V0 = 2 * TILE_BYTES, V1 = 3 * TILE_BYTES;  // vb: V slot 0 at +32 KB
-    f32x4 SA[4][2], SB[4][2];
-    bf16x8 pb[2][2];
-    stage_k(0, K0);
-    stage_v(0, V0);
-    if (1 < nkb) stage_k(1, K1);
-    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+    if (kb + 1 < nkb) stage(kb + 1, 0);
+    attn_v6t_block<STAGE_BYTES, STAGE_BYTES + TILE_BYTES, false>(st, qf, ka, vb, kb, kv_len, g);
+    if (kb + 1 >= nkb) break;
     sync();
-    // block 0: QK^T, tail mask, the first block's running max (v6_softmax_rescale<true>)
-    v6_qk<K0>(SA, st.negm4, qf, ka);
-    v6_tail_mask(SA, 0, kv_len, g);
-    {
-      float mx[2];
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) mx[qt] = rowmax64(SA, qt);
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        st.negm[qt] -= mx[qt];
-        st.negm4[qt] = (f32x4){st.negm[qt], st.negm[qt], st.negm[qt], st.negm[qt]};
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) SA[kt][qt][i] -= mx[qt];
-      }
-    }
-    bool resc = false;
-    // iteration j: Sc = block j (SA for even j), Sn = block j+1; K_{j+1} in K slot (j+1) % 2, V_j in V slot j % 2.
-    // The last block's iteration (no block j+1) is peeled off the loop, once per parity.
-    auto iter = [&](auto sc_is_a, auto nextc, int j) {
-      constexpr bool EVEN = decltype(sc_is_a)::value, NEXT = decltype(nextc)::value;
-      f32x4(&Sc)[4][2] = EVEN ? SA : SB;
-      f32x4(&Sn)[4][2] = EVEN ? SB : SA;
-      sync();  // K_{j+1}, V_j landed; K_j's and V_{j-1}'s slots free
-      if constexpr (NEXT) {
-        if (j + 2 < nkb) stage_k(j + 2, EVEN ? K0 : K1);
-        stage_v(j + 1, EVEN ? V1 : V0);
-      }
-      if (resc) v6p_rescale(st, Sc);  // wave-uniform
-      constexpr int KN = EVEN ? K1 : K0, VC = (EVEN ? V0 : V1) - V0;
-      v6p_phase_a<KN, NEXT>(Sn, Sc, pb, st.negm4, qf, ka);
-      if constexpr (NEXT) v6_tail_mask(Sn, j + 1, kv_len, g);
-      resc = v6p_phase_b<VC, NEXT>(st, pb, Sn, vb);
-    };
-    int j = 0;
-    for (; j + 2 < nkb; j += 2) {  // blocks j, j+1 both with a successor
-      iter(std::true_type{}, std::true_type{}, j);
-      iter(std::false_type{}, std::true_type{}, j + 1);
-    }
-    if (j + 1 < nkb) {  // blocks nkb-2 (even), nkb-1
-      iter(std::true_type{}, std::true_type{}, j);
-      iter(std::false_type{}, std::false_type{}, j + 1);
-    } else {  // block nkb-1 (even)
-      iter(std::true_type{}, std::false_type{}, j);
-    }
+    if (kb + 2 < nkb) stage(kb + 2, 1);
+    attn_v6t_block<0, TILE_BYTES, false>(st, qf, ka, vb, kb + 1, kv_len, g);
   }
 
 #pragma unroll
@@ -1484,8 +1269,7 @@ __global__ __launch_bounds__(256, 2) void attn_cross3_w4_kernel(Cross3Args a) { 
 
 __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) { attn_fwd_v6_body<8>(a); }
 __global__ __launch_bounds__(256, 2) void attn_fwd_v6_w4_kernel(AttnArgs a) { attn_fwd_v6_body<4>(a); }
-__global__ __launch_bounds__(512) void attn_fwd_v6t_kernel(AttnArgs a) { attn_fwd_vt_body<false>(a); }
-__global__ __launch_bounds__(512) void attn_fwd_v6p_kernel(AttnArgs a) { attn_fwd_vt_body<true>(a); }
+__global__ __launch_bounds__(512) void attn_fwd_v6t_kernel(AttnArgs a) { attn_fwd_vt_body(a); }
 
 }  // namespace
 
@@ -1505,14 +1289,13 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
   if (head_dim != D) return SA_ERR_ARG;
   if ((q_stride | k_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
   if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)o)) & 15) return SA_ERR_ARG;
-  if (kernel < 0 || kernel > 4) return SA_ERR_ARG;
-  if (kernel >= 3 && (v_stride % 64 || (((uintptr_t)v) & 127))) return SA_ERR_ARG;  // V^T rows: whole 64-key blocks
+  if (kernel < 0 || kernel > 3) return SA_ERR_ARG;
+  if (kernel == 3 && (v_stride % 64 || (((uintptr_t)v) & 127))) return SA_ERR_ARG;  // V^T rows: whole 64-key blocks
   static const bool attr = [] {  // one-time, thread-safe
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6_w4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6t_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_v6p_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     return true;
   }();
   (void)attr;
@@ -1534,12 +1317,9 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
   if (kernel == 2) {
     dim3 grid((max_q_len + 127) / 128, heads, nseg);
     hipLaunchKernelGGL(attn_fwd_v6_w4_kernel, grid, dim3(256), LDS_BYTES, (hipStream_t)stream, a);
-  } else if (kernel >= 3) {  // v = V^T [heads * 128][v_stride] (attn_fwd_vt_body; 4: software-pipelined blocks)
+  } else if (kernel == 3) {  // v = V^T [heads * 128][v_stride] (attn_fwd_vt_body)
     dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
-    if (kernel == 3)
-      hipLaunchKernelGGL(attn_fwd_v6t_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
-    else
-      hipLaunchKernelGGL(attn_fwd_v6p_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(attn_fwd_v6t_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
   } else {
     dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
     hipLaunchKernelGGL(attn_fwd_v6_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);

@@ -112,7 +112,7 @@ def main(which=("gemm", "attn")):
         q, k, v_ = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
         outs = {}
         variants = tuple(int(v) for v in os.environ.get("SA_KB_AVARS", "1").split(","))
-        vts = {m: vt_layout(v_, 3) for m in (3, 4) if m in variants}  # kernels 3, 4 read V^T
+        vts = {m: vt_layout(v_, 3) for m in (3,) if m in variants}  # kernel 3 reads V^T
         times = {v: [] for v in variants}
         for rnd in range(3):
             for v in variants:

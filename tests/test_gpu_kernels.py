@@ -172,12 +172,11 @@ def test_attention_segments(Lq, Lk, kernel):
     assert rel(o2, 2 * o.float()) < 1e-2
 
 
-@pytest.mark.parametrize("kernel", [3, 4], ids=["v6t_vt_perm32", "v6p_pipelined"])
+@pytest.mark.parametrize("kernel", [3], ids=["v6t_vt_perm32"])
 @pytest.mark.parametrize("B,Lq,Lk", [(2, 300, 320), (2, 512, 256), (1, 256, 1000), (3, 64, 64), (1, 256, 128)])
 def test_attention_vt_kernels(kernel, B, Lq, Lk):
-    """the self-attention forms that read V as V^T [H*128, Rv] (kernel 3: keys permuted per 32 as P; 4: the same block
-    arithmetic software-pipelined across blocks, bit-identical to 3) vs fp32 torch, incl. a ragged last key block and
-    accumulate"""
+    """the self-attention form that reads V as V^T [H*128, Rv] (kernel 3: keys permuted per 32 as P) vs fp32 torch,
+    incl. a ragged last key block and accumulate"""
     from stableavatar_amd import ops
     from stableavatar_amd.kbench import vt_layout
     H, D = 3, 128
@@ -196,13 +195,9 @@ def test_attention_vt_kernels(kernel, B, Lq, Lk):
     o2 = o.clone()
     ops.attention(q, k, vt, o2, segs, B, Lq, H, accumulate=True, kernel=kernel)
     assert rel(o2, 2 * o.float()) < 1e-2
-    if kernel != 3:
-        o3 = torch.empty_like(o)
-        ops.attention(q, k, vt, o3, segs, B, Lq, H, kernel=3)
-        assert torch.equal(o3, o)
 
 
-@pytest.mark.parametrize("kernel", [3, 4], ids=["v6t_vt_perm32", "v6p_pipelined"])
+@pytest.mark.parametrize("kernel", [3], ids=["v6t_vt_perm32"])
 def test_attention_vt_spike_rescale(kernel):
     """the rescale branch of the V^T form"""
     from stableavatar_amd import ops
@@ -219,9 +214,6 @@ def test_attention_vt_spike_rescale(kernel):
     o = torch.empty_like(q)
     segs = torch.tensor([[0, L, 0, L]], dtype=torch.int32, device=dev)
     ops.attention(q, k, vt_layout(v, 3), o, segs, 1, L, 1, kernel=kernel)
-    o3 = torch.empty_like(q)
-    ops.attention(q, k, vt_layout(v, 3), o3, segs, 1, L, 1, kernel=3)
-    assert torch.equal(o3, o)
     ref = _ref_attn(q, k, v, D ** -0.5)
     assert rel(o, ref) < 1e-2
     for r in (5, 9, 17, 20):
