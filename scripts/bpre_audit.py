@@ -3,7 +3,8 @@ as inline-asm buffer_load_dwordx4 into bpre[0..7], which hipcc does not count (c
 first K step's counted vmcnt wait retires them.  Correctness needs that NO compiler instruction between the loads and
 that wait reads, writes, copies or spills a bpre register.  This compiles gemm.hip for gfx950 (--save-temps), finds
 every preload group in every kernel, and scans to the first s_waitcnt vmcnt: any instruction outside an asm statement
-naming a bpre VGPR there, or any scratch access, is a violation.
+naming a bpre VGPR there (a copy, a spill or a use) is a violation, except on the K loop's zero-trip path, which the ABI
+makes dead (K <= 0 is rejected).
 usage: python scripts/bpre_audit.py  -> one line per kernel with a preload; exit 1 on a violation or if none found"""
 import re
 import subprocess
@@ -27,16 +28,17 @@ def regs_of(line):
     return out
 
 
-def _scan(asm_lines, start, regs, labels, seen):
-    """violations on every control-flow path from line `start` to the first s_waitcnt vmcnt (s_branch followed,
-    s_cbranch both ways)"""
-    viol, work = [], [start]
+def _scan(asm_lines, start, regs, labels):
+    """(violations, zero-trip reads) on every control-flow path from line `start` to the first s_waitcnt vmcnt
+    (s_branch followed, s_cbranch both ways).  A read of a bpre register reached without any MFMA on the path is the
+    K loop's zero-trip path (nk == 0), dead at run time: the ABI rejects K <= 0 (sa_gemm_bf16_panels / _ex)."""
+    viol, zero_trip, work, seen = [], [], [(start, False)], set()
     n = len(asm_lines)
     while work:
-        k = work.pop()
+        k, mfma = work.pop()
         in_asm = False
-        while k < n and k not in seen:
-            seen.add(k)
+        while k < n and (k, mfma) not in seen:
+            seen.add((k, mfma))
             t = asm_lines[k].strip()
             if ";;#ASMSTART" in t:
                 in_asm = True
@@ -47,15 +49,17 @@ def _scan(asm_lines, start, regs, labels, seen):
             elif t and not t.startswith(";") and not t.startswith("."):
                 if t.startswith("s_waitcnt") and "vmcnt" in t:
                     break
+                if t.startswith("v_mfma"):
+                    mfma = True
                 if t.startswith("s_branch "):
                     k = labels[t.split()[1]]
                     continue
                 if t.startswith("s_cbranch"):
-                    work.append(labels[t.split()[1]])
-                elif t.startswith("scratch_") or (not in_asm and regs & regs_of(t)):
-                    viol.append(t)
+                    work.append((labels[t.split()[1]], mfma))
+                elif not in_asm and regs & regs_of(t):
+                    (viol if mfma else zero_trip).append(t)
             k += 1
-    return viol
+    return viol, zero_trip
 
 
 def audit(asm_lines):
@@ -97,8 +101,8 @@ def audit(asm_lines):
                     viol.append(t)
             k += 1
         if cnt == 8:
-            viol += _scan(asm_lines, k, regs, labels, set())
-            res.append((kern, sorted(regs), viol, cnt))
+            v2, zt = _scan(asm_lines, k, regs, labels)
+            res.append((kern, sorted(regs), viol + v2, cnt, len(zt)))
         i = k
     return res
 
@@ -114,8 +118,8 @@ if __name__ == "__main__":
         s = next(Path(td).glob("gemm-hip-amdgcn-amd-amdhsa-gfx950.s")).read_text().split("\n")
     res = audit(s)
     bad = 0
-    for kern, regs, viol, cnt in res:
-        print(f"{kern[:70]:70s} {cnt} loads, bpre {len(regs)} VGPRs: "
+    for kern, regs, viol, cnt, zt in res:
+        print(f"{kern[:70]:70s} {cnt} loads, bpre {len(regs)} VGPRs, {zt} reads on the zero-trip path: "
               f"{'OK' if not viol else 'VIOLATION ' + '; '.join(viol[:3])}")
         bad += bool(viol) or cnt != 8
     if not res:

@@ -74,3 +74,30 @@ def test_encoder_entry_points_reject_bad_arguments():
     assert L.sa_conv3d_cl_down(one, 1, 8, 8, 3, 1, one, one, 32, 96, one, None) == 1        # Cin % 32
     assert L.sa_vae_latent_out(None, 32, 16, 64, one, one, one, None) == 1
     assert L.sa_vae_latent_out(one, 16, 16, 64, one, one, one, None) == 1                   # 2*Cz > C_stride
+
+
+def test_gemm_rejects_empty_k_without_gpu_work():
+    """K <= 0 is refused at the ABI: the persistent GEMM's bias preload (inline-asm loads retired by the first K step's
+    counted wait) relies on every tile running at least one K step (scripts/bpre_audit.py)"""
+    if not _lib.LIB_PATH.exists():
+        pytest.skip("library not built")
+    import ctypes
+    L = _lib.lib()
+    buf = ctypes.create_string_buffer(4096)
+    p = ctypes.addressof(buf) + (-ctypes.addressof(buf)) % 16  # 16-byte aligned, never dereferenced on this path
+    for K in (0, -128):
+        assert L.sa_gemm_bf16(p, 128, 0, p, 128, 0, None, p, 64, 0, 64, 64, K, 1, 0, None, 0, 0, None, 0, 0,
+                              None) == 1
+
+
+@pytest.mark.timeout(600)
+def test_bias_preload_disassembly_audit():
+    """no compiler instruction copies, spills or reads the inline-asm bias preload registers before the
+    first K step's counted vmcnt wait, in every bf16 / GELU persistent-GEMM instantiation (gfx950 disassembly)"""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "bpre_audit.py")], capture_output=True, text=True)
+    print(r.stdout[-3000:])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert r.stdout.count(": OK") >= 8
