@@ -1061,11 +1061,7 @@ __device__ __forceinline__ void attn_cross3_body(const Cross3Args& a) {
     const bf16* qp = a.q + (long)(q_row0 + qc) * a.qs + h * D + 8 * g;
 #pragma unroll
     for (int dc = 0; dc < 4; ++dc) {
-#ifdef SA_X3_NOQ  // measurement builds only: no Q load (timing only)
-      for (int j = 0; j < 8; ++j) qf[qt][dc][j] = (bf16)(0.01f * (float)(j + qc % 7));
-#else
       qf[qt][dc] = *(const bf16x8*)(qp + 32 * dc);
-#endif
 #pragma unroll
       for (int j = 0; j < 8; ++j) qf[qt][dc][j] = f2bf(bf2f(qf[qt][dc][j]) * a.c);
     }
@@ -1165,87 +1161,56 @@ __device__ __forceinline__ void attn_cross3_body(const Cross3Args& a) {
     reset();
   };
 
-  // block j in stage j % 3, its DMA issued two blocks ahead (with one block of lead the L2 latency of
-  // the next block was exposed at the barriers of these short streams)
-  auto step = [&](int jj, auto bufc) {
-    constexpr int BUF = decltype(bufc)::value;
+  // Block j sits in ring slot j % NST, chosen at run time through the LDS read bases (kas / vas): one copy of the
+  // block body.  With a copy per slot (the slot as the ds_read immediate offset, round 4) hipcc spilled 118 (8 waves)
+  // / 152 (4 waves) VGPRs to scratch: every copy's temporaries live across the unrolled loop.
+  uint32_t kas[4], vas[8];
+  auto at_slot = [&](int slot) {
+    const uint32_t so = (uint32_t)slot * TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) kas[i] = ka[i] + so;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) vas[i] = va[i] + so;
+  };
+  // block j's DMA issued NST - 1 blocks ahead (with one block of lead the L2 latency of the next block was exposed
+  // at the barriers of these short streams)
+  auto step = [&](int jj) {
     if (NST > 2 && jj + 1 < ntot)
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");  // block jj landed; jj+1 may still fly
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (jj + NST - 1 < ntot) stage(jj + NST - 1, (BUF + NST - 1) % NST);
+    if (jj + NST - 1 < ntot) stage(jj + NST - 1, (jj + NST - 1) % NST);
     const int src = jj < nT ? 0 : (jj < nT + nI ? 1 : 2);
     const int kb = src == 0 ? jj : (src == 1 ? jj - nT : jj - nT - nI);
     const int len = src == 0 ? a.t_len : (src == 1 ? a.i_len : a.nper);
-    attn_v6_block<BUF * TILE_BYTES, BUF * TILE_BYTES, false>(st, qf, ka, va, kb, len, g, kb == 0);
+    at_slot(jj % NST);
+    attn_v6_block<0, 0, false>(st, qf, kas, vas, kb, len, g, kb == 0);
     if (jj == nT - 1 || jj == nT + nI - 1 || jj == ntot - 1) finish(src);
   };
-  // the vocal stream's single block when a frame has at most 32 audio tokens (StableAvatar: 32): peeled out of
-  // the loop as a half block (key tiles 0-1: half the MFMAs and exponentials of a 64-key block)
+  // the vocal stream's single block when a frame has at most 32 audio tokens (StableAvatar: 32), and the image
+  // stream's last block when it holds at most 32 keys (CLIP: 257 = 4 x 64 + 1) while the vocal block is peeled too:
+  // peeled out of the loop as half blocks (key tiles 0-1: half the MFMAs and exponentials of a 64-key block)
   const bool vhalf = nV == 1 && a.nper <= KVB / 2;
-  auto last_half = [&](int jj, auto bufc) {
-    constexpr int BUF = decltype(bufc)::value;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    attn_half_block<BUF * TILE_BYTES, BUF * TILE_BYTES>(st, qf, ka, va, 0, a.nper, g, true);
-    finish(2);
-  };
-  // likewise the image stream's last block when it holds at most 32 keys (CLIP: 257 = 4 x 64 + 1), when the vocal
-  // block is peeled too (so the loop still ends on a block boundary of the 3-stage ring)
   const bool ihalf = vhalf && a.i_len % KVB != 0 && a.i_len % KVB <= KVB / 2;
-  auto img_half = [&](int jj, auto bufc) {
-    constexpr int BUF = decltype(bufc)::value;
-    if (NST > 2)
+  auto half = [&](bool voc) {
+    const int jj = voc ? ntot - 1 : ntot - 2;
+    if (!voc && NST > 2)
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");  // this block landed; the vocal block may fly
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (NST == 2) stage(jj + 1, (BUF + 1) % NST);  // the vocal block, one ahead
-    attn_half_block<BUF * TILE_BYTES, BUF * TILE_BYTES>(st, qf, ka, va, nI - 1, a.i_len, g, nI == 1);
-    finish(1);
+    if (!voc && NST == 2) stage(jj + 1, (jj + 1) % NST);  // the vocal block, one ahead
+    at_slot(jj % NST);
+    attn_half_block<0, 0>(st, qf, kas, vas, voc ? 0 : nI - 1, voc ? a.nper : a.i_len, g, voc || nI == 1);
+    finish(voc ? 2 : 1);
   };
   const int nloop = vhalf ? (ihalf ? ntot - 2 : ntot - 1) : ntot;
   if (NW == 8 && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-#ifndef SA_X3_REPS
-#define SA_X3_REPS 1  // measurement builds only: > 1 runs the block stream that many times per tile (timing only)
-#endif
-#if SA_X3_REPS > 1
-  for (int rep = 0; rep < SA_X3_REPS; ++rep) {
-  if (rep) __syncthreads();
-#endif
   stage(0, 0);
   if (NST > 2 && 1 < ntot) stage(1, 1);
-  for (int j = 0; j < nloop; j += NST) {
-    step(j, std::integral_constant<int, 0>{});
-    if (j + 1 >= nloop) break;
-    step(j + 1, std::integral_constant<int, 1 % NST>{});
-    if (NST > 2) {
-      if (j + 2 >= nloop) break;
-      step(j + 2, std::integral_constant<int, 2 % NST>{});
-    }
-  }
-  if (ihalf) {
-    const int ji = ntot - 2;
-    if (ji % NST == 0)
-      img_half(ji, std::integral_constant<int, 0>{});
-    else if (ji % NST == 1)
-      img_half(ji, std::integral_constant<int, 1 % NST>{});
-    else
-      img_half(ji, std::integral_constant<int, 2 % NST>{});
-  }
-  if (vhalf) {
-    const int jl = ntot - 1;
-    if (jl % NST == 0)
-      last_half(jl, std::integral_constant<int, 0>{});
-    else if (jl % NST == 1)
-      last_half(jl, std::integral_constant<int, 1 % NST>{});
-    else
-      last_half(jl, std::integral_constant<int, 2 % NST>{});
-  }
-#if SA_X3_REPS > 1
-  }
-#endif
+  for (int j = 0; j < nloop; ++j) step(j);
+  for (int hb = ihalf ? 0 : 1; hb < (vhalf ? 2 : 0); ++hb) half(hb == 1);
 
   // 16-byte stores from permlane16-swapped column-group pairs, as the self-attention epilogue (T21)
 #pragma unroll
