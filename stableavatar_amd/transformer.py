@@ -518,10 +518,14 @@ class WanTransformer3DFantasyModel(nn.Module):
 
     # ------------------------------------------------------------------ vocal projector
 
-    def _vocal(self, pk, vocal_embeddings, n_frames, lat_bf16, Lq, e0_row, e_row, dev):
+    def _vocal(self, pk, vocal_embeddings, n_frames, lat_bf16, Lq, e0_row, e_row, dev, frames=None):
         """FantasyTalkingVocalCondition{1B,14B}Model.forward (vocal_projector_fantasy_1B.py:433-450,
         _14B.py:431-449) for one audio row; lat_bf16 = patch-embedded tokens of that row [Lq, dim].
-        Returns [F*n, vd] bf16 (vd = 1536 for 1.3B, the DiT width for 14B)."""
+        Returns [F*n, vd] bf16 (vd = 1536 for 1.3B, the DiT width for 14B).
+        frames = (f0, nf): latent frames f0 .. f0+nf-1 only (lat_bf16 then holds just their tokens, and the result is
+        [nf*n, vd]).  Every op of the projector is per row except the attention, whose queries of frame f attend only
+        to frame f's tokens (:259-270), so these rows equal those of the whole projector bit for bit: a
+        sequence-parallel rank computes the frames its token chunk covers."""
         V, vd = pk.vocal, self.vd
         hdv = vd // 8  # 8 heads: D = 192 (1.3B) or 640 (14B)
         feat = vocal_embeddings.to(device=dev, dtype=torch.bfloat16).contiguous()
@@ -538,14 +542,16 @@ class WanTransformer3DFantasyModel(nn.Module):
             rows = (torch.tensor([i for row in r for i in row], dtype=torch.int32, device=dev), len(r), len(r[0]))
             self._split_cache[key] = rows
         idx, Fn, nper = rows
-        x = torch.empty(Fn * nper, vd, device=dev, dtype=torch.float32)
-        ops.gather_rows(feat, idx, x)
+        f0, nf = (0, Fn) if frames is None else frames
+        Mv = nf * nper
+        x = torch.empty(Mv, vd, device=dev, dtype=torch.float32)
+        ops.gather_rows(feat, idx[f0 * nper:(f0 + nf) * nper], x)
         em = torch.empty(2, 1, 6, vd, device=dev, dtype=torch.float32)
         ops.mod_add(V.mod, e0_row, em)
-        Mv = Fn * nper
         hb = torch.empty(Mv, vd, device=dev, dtype=torch.bfloat16)
         G = Lq // Fn
-        segs = self._segs.get(("vp", Fn, nper, G), [[f * nper, nper, f * G, G] for f in range(Fn)], dev)
+        assert lat_bf16.shape[0] == nf * G
+        segs = self._segs.get(("vp", nf, nper, G), [[f * nper, nper, f * G, G] for f in range(nf)], dev)
         for i, B_ in enumerate(V.blocks):
             e = em[i, 0]
             # "self-attention" branch is x + modulate(LN(x))*e2 (vocal_projector_fantasy_1B.py:345-347)
@@ -556,7 +562,7 @@ class WanTransformer3DFantasyModel(nn.Module):
             kv = ops.linear(lat_bf16, B_.w_kv, B_.b_kv, ops.EPI_BF16)
             ops.qk_rmsnorm_rope(kv, 0, -1, B_.nk, None, vd, 1e-6)
             o = torch.empty(Mv, vd, device=dev, dtype=torch.bfloat16)
-            ops.attention_small(q, kv[:, :vd], kv[:, vd:], o, segs, Fn, nper, G, 8, hdv)
+            ops.attention_small(q, kv[:, :vd], kv[:, vd:], o, segs, nf, nper, G, 8, hdv)
             ops.linear(o, B_.w_o, B_.b_o, ops.EPI_RES_F32, out=x, residual=x)
             ops.layernorm_mod(x, hb, 1e-6, shift=e[3:4], scale=e[4:5], rows_per_batch=Mv)
             h = ops.linear(hb, B_.w_f0, B_.b_f0, ops.EPI_GELU_TANH_BF16)
@@ -588,7 +594,7 @@ class WanTransformer3DFantasyModel(nn.Module):
         return out
 
     def _sp_layer_rows(self, pk, L, li, x, ws, em, ex, pack_kw, rank, Lc, Lq, hg, hgd, grid, segs_rows, row_segs,
-                       ctx, vctx, kvv, nper, Gf, n_fr, use_cross3, rstreams):
+                       ctx, vctx, kvv, nper, Gf, n_fr, use_cross3, rstreams, vrows=None):
         """One DiT block (1B:650-695) with Ulysses sequence parallelism, each CFG row on its own stream
         (SA_SP_OVERLAP=4): row b's Q/K/V exchange (wan_xfuser.py:102-107) travels while the other rows compute
         (their QKV GEMMs, attention, O-projection, cross-attention and FFN), and its head-output exchange travels
@@ -603,6 +609,7 @@ class WanTransformer3DFantasyModel(nn.Module):
         tl, ni = ctx.text_len, ctx.img_len
         kvt, kvi = ctx.kv[li]
         nv = n_fr * nper
+        vrows = slice(0, nv) if vrows is None else vrows  # the vocal context rows this rank's queries read
         pend, back = [], []
         for b, st in enumerate(rstreams):  # self-attention inputs (1B:675-676) and the Q/K/V exchange
             rs = slice(b * Lc, (b + 1) * Lc)
@@ -633,7 +640,8 @@ class WanTransformer3DFantasyModel(nn.Module):
                 ops.linear(mod, L.w_cq, L.b_cq, ops.EPI_BF16, out=qc)
                 ops.qk_rmsnorm_rope(qc, 0, -1, L.cnq, None, dim, eps)
                 kv_b = kvv[b * nv:(b + 1) * nv]
-                ops.linear(vctx[b * nv:(b + 1) * nv], L.w_kv_v, L.b_kv_v, ops.EPI_BF16, out=kv_b)
+                ops.linear(vctx[b * nv + vrows.start:b * nv + vrows.stop], L.w_kv_v, L.b_kv_v, ops.EPI_BF16,
+                           out=kv_b[vrows])
                 if use_cross3:
                     kt, ki = kvt[b * tl:(b + 1) * tl], kvi[b * ni:(b + 1) * ni]
                     ops.attention_cross3(qc, kt[:, :dim], kt[:, dim:], tl, ki[:, :dim], ki[:, dim:], ni, kv_b[:, :dim],
@@ -755,7 +763,16 @@ class WanTransformer3DFantasyModel(nn.Module):
             n_fr = (video_sample_n_frames - 1) // 4 + 1
             if S % n_fr:
                 raise ValueError("seq_len must split evenly into latent frames for the per-frame audio attention")
-            lat_row = torch.empty(S, dim, device=dev, dtype=torch.bfloat16)
+            G = S // n_fr
+            # the latent frames this rank's tokens belong to (SP pads past S join the last frame): the only vocal
+            # context rows its cross-attention reads (sp.vocal_segments); without SP every frame
+            if SP:
+                t0, t1 = rank * Lc, min((rank + 1) * Lc, S)
+                vf0 = min(t0 // G, n_fr - 1)
+                vnf = min(max(t1 - 1, t0) // G, n_fr - 1) - vf0 + 1
+            else:
+                vf0, vnf = 0, n_fr
+            lat_row = torch.empty(vnf * G, dim, device=dev, dtype=torch.bfloat16)
             if vocal_embeddings.shape[0] == 1 and B != 1:
                 raise ValueError("a single audio row drives a batch of 1 (1B:1008-1009); CFG batches pass 3 rows")
             # 1.3B: the projector runs on the last (full-condition) row only, the unconditional row gets
@@ -764,22 +781,27 @@ class WanTransformer3DFantasyModel(nn.Module):
             voc_rows = []
             for r in range(rows_v):
                 src = B - 1 if rows_v == 1 else r
-                ops.cast_bf16(xfull[src * Lp:src * Lp + S], lat_row)
+                ops.cast_bf16(xfull[src * Lp + vf0 * G:src * Lp + (vf0 + vnf) * G], lat_row)
                 vv, Fn, nper = self._vocal(pk, vocal_embeddings[src], video_sample_n_frames, lat_row, S,
-                                           e0[src:src + 1], e[src:src + 1], dev)
+                                           e0[src:src + 1], e[src:src + 1], dev, frames=(vf0, vnf))
                 if self.vd != dim:
                     raise ValueError("vocal context width must equal the DiT width")
                 voc_rows.append(vv)
             assert Fn == n_fr
-            if rows_v == 1:
+            vr = slice(vf0 * nper, (vf0 + vnf) * nper)  # the computed frames' rows of each CFG row's context
+            if rows_v == 1 and vnf == n_fr:
                 vctx = torch.zeros(B, Fn * nper, dim, device=dev, dtype=torch.bfloat16)
                 for b in range(1, B):
                     vctx[b].copy_(voc_rows[0])
-            else:
+            elif vnf == n_fr:
                 vctx = torch.stack(voc_rows)
+            else:
+                vctx = torch.zeros(B, Fn * nper, dim, device=dev, dtype=torch.bfloat16)
+                for b in range(B):
+                    if rows_v == B or b >= 1:
+                        vctx[b, vr].copy_(voc_rows[b if rows_v == B else 0])
             vctx = vctx.view(B * Fn * nper, dim)
 
-            G = S // n_fr
             if SP:
                 plan = sp.make_plan(NS, rank, H_)
                 ex = self._sp_exchange(plan, B, Lc, dev)
@@ -840,7 +862,8 @@ class WanTransformer3DFantasyModel(nn.Module):
             for li, L in enumerate(pk.layers):
                 if sp_streams:
                     self._sp_layer_rows(pk, L, li, x, ws, emod[li], ex, pack_kw, rank, Lc, Lq, hg, hgd, grid,
-                                        segs_rows, row_segs, ctx, vctx, kvv, nper, G, n_fr, use_cross3, rstreams)
+                                        segs_rows, row_segs, ctx, vctx, kvv, nper, G, n_fr, use_cross3, rstreams,
+                                        vrows=vr)
                     continue
                 em = emod[li]  # [B, 6, dim]
                 # self-attention (1B:675-679)
@@ -924,7 +947,13 @@ class WanTransformer3DFantasyModel(nn.Module):
                 ops.linear(ws.mod, L.w_cq, L.b_cq, ops.EPI_BF16, out=qc)
                 ops.qk_rmsnorm_rope(qc, 0, -1, L.cnq, None, dim, self.eps)
                 kvt, kvi = ctx.kv[li]
-                ops.linear(vctx, L.w_kv_v, L.b_kv_v, ops.EPI_BF16, out=kvv)
+                if vnf == n_fr:
+                    ops.linear(vctx, L.w_kv_v, L.b_kv_v, ops.EPI_BF16, out=kvv)
+                else:  # SP: the rows of the frames this rank's queries attend to
+                    for b in range(B):
+                        r0 = b * n_fr * nper + vf0 * nper
+                        ops.linear(vctx[r0:r0 + vnf * nper], L.w_kv_v, L.b_kv_v, ops.EPI_BF16,
+                                   out=kvv[r0:r0 + vnf * nper])
                 if use_cross3:  # text + image + vocal in one launch, bf16 sum as 1B:602
                     ops.attention_cross3(qc, kvt[:, :dim], kvt[:, dim:], ctx.text_len, kvi[:, :dim], kvi[:, dim:],
                                          ctx.img_len, kvv[:, :dim], kvv[:, dim:], nper, G, n_fr, ws.att, B, Lc, H_,
