@@ -29,7 +29,7 @@ EXTRA: dict[str, list[str]] = {}
 
 def _compile(src: Path) -> Path:
     obj = BUILD / (src.stem + ".o")
-    deps = [src, CSRC / "common.h", Path(__file__)]
+    deps = [src, *CSRC.glob("*.h"), Path(__file__)]
     if obj.exists() and all(obj.stat().st_mtime >= d.stat().st_mtime for d in deps if d.exists()):
         return obj
     cmd = [HIPCC, *CFLAGS, *EXTRA.get(src.stem, []), "-c", str(src), "-o", str(obj)]
