@@ -112,6 +112,14 @@ int sa_attn_small(const void* q, const void* k, const void* v, void* o, const in
                   int max_kv_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride, int64_t v_stride,
                   int64_t o_stride, float scale, void* stream);
 
+/* sa_attn_small with the keys of each 32-query chunk split over nsplit workgroups (head_dim <= 256 only), merged by
+ * a second launch: for launches with few query chunks (a sequence-parallel rank's vocal projector, 24 workgroups at
+ * N = 8).  work: device scratch of nseg * heads * ceil(max_q_len / 32) * nsplit * 32 * (head_dim + 2) floats. */
+int sa_attn_small_split(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
+                        int max_q_len, int max_kv_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride,
+                        int64_t v_stride, int64_t o_stride, float scale, int nsplit, void* work, int64_t work_bytes,
+                        void* stream);
+
 /* LayerNorm (+affine) (+AdaLN modulate  y*(1+scale[b])+shift[b]) (+gated residual x + y*gate[b]):
  * WanLayerNorm 1B:345-355 and its call sites :675,684,687,721-722; MLPProj LayerNorms :731-734;
  * vocal_projector_fantasy_1B.py:345-347,352,354,386,398.  in/out dtype: 0 = f32, 1 = bf16. */

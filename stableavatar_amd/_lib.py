@@ -31,6 +31,7 @@ SIGNATURES = {
     "sa_small_linear_f32": "pliplppliiiip",
     "sa_mod_add": "ppllpiiiip",
     "sa_attn_small": "pppppiiiiillllfp",
+    "sa_attn_small_split": "pppppiiiiillllfiplp",
     "sa_attn_cross3": "plpplipplippliiiipliiifp",
     "sa_flow_step": "pppiiiilifffiipip",
     "sa_gather_rows": "plpipllp",

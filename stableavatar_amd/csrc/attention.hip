@@ -150,19 +150,31 @@ __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* q, const bf
 // (Q broadcast from LDS, prescaled by scale·log2e), online softmax in fp32, then O with 4 head dims per
 // lane.  The one-wave-per-query kernel above re-read K and V from L2 for every query (0.7 ms per vocal-
 // projector call at config 2); this reads them once per 32 queries.
+// Key split (nsplit > 1): the workgroups of a 32-query chunk each take kper keys and write their unnormalised O,
+// running max and row sum to `work`, and attn_small2_combine_kernel merges them.  A sequence-parallel rank's vocal
+// projector has 17 queries x 8 heads x 3 frames = 24 workgroups, each walking 1024 keys alone (0.28 ms per call at
+// N = 8); split 8 ways, the same keys run on 192 CUs.
 constexpr int SM2_D = 256, SM2_DP = SM2_D + 8, SM2_KC = 64, SM2_QW = 32;
+
+// work block of one (segment, head, query chunk, split): O [32][D], then m [32], then l [32] (fp32)
+__device__ __forceinline__ float* sm2_work_block(float* work, int seg, int h, int qc, int s, int heads, int nqc,
+                                                 int nsplit, int D) {
+  return work + ((((long)seg * heads + h) * nqc + qc) * nsplit + s) * (long)(SM2_QW * (D + 2));
+}
 
 __global__ __launch_bounds__(256) void attn_small2_kernel(const bf16* q, const bf16* k, const bf16* v, bf16* o,
                                                           const int* segs, int D, long qs, long ks, long vs, long os,
-                                                          float c) {
+                                                          float c, int nsplit, int kper, float* work) {
   __shared__ __attribute__((aligned(16))) bf16 Ks[SM2_KC * SM2_DP];
   __shared__ __attribute__((aligned(16))) bf16 Vs[SM2_KC * SM2_DP];
   __shared__ __attribute__((aligned(16))) float Qs[SM2_QW * SM2_D];
   __shared__ __attribute__((aligned(16))) float Ps[4][8][SM2_KC];
   const int* sg = segs + blockIdx.z * 4;
   const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
-  const int q0 = blockIdx.x * SM2_QW;
+  const int qc = blockIdx.x / nsplit, split = blockIdx.x % nsplit;
+  const int q0 = qc * SM2_QW;
   if (q0 >= q_len) return;
+  const int kb0 = split * kper, kb1 = min(kv_len, kb0 + kper);  // this workgroup's keys
   const int h = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int DP = D + 8, nch = D / 8;  // padded row (elements), 16-B chunks per row
@@ -188,12 +200,12 @@ __global__ __launch_bounds__(256) void attn_small2_kernel(const bf16* q, const b
     for (int t = 0; t < 4; ++t) O[qq][t] = 0.f;
   }
   const float* Qw = Qs + w * 8 * SM2_D;
-  for (int kc = 0; kc < kv_len; kc += SM2_KC) {
+  for (int kc = kb0; kc < kb1; kc += SM2_KC) {
     __syncthreads();  // previous chunk's K / V reads done (and Q written, first time)
     for (int i = tid; i < SM2_KC * nch; i += 256) {
       const int r = i / nch, ch = i % nch;
       u32x4 kx = {0u, 0u, 0u, 0u}, vx = {0u, 0u, 0u, 0u};
-      if (kc + r < kv_len) {
+      if (kc + r < kb1) {
         kx = *(const u32x4*)(k + (long)(kv_row0 + kc + r) * ks + h * D + ch * 8);
         vx = *(const u32x4*)(v + (long)(kv_row0 + kc + r) * vs + h * D + ch * 8);
       }
@@ -219,7 +231,7 @@ __global__ __launch_bounds__(256) void attn_small2_kernel(const bf16* q, const b
         sc[qq] = fmaf(kf[6], b[2], sc[qq]); sc[qq] = fmaf(kf[7], b[3], sc[qq]);
       }
     }
-    const bool valid = kc + lane < kv_len;
+    const bool valid = kc + lane < kb1;
 #pragma unroll
     for (int qq = 0; qq < 8; ++qq) {
       const float s = valid ? sc[qq] : -INFINITY;
@@ -255,6 +267,22 @@ __global__ __launch_bounds__(256) void attn_small2_kernel(const bf16* q, const b
     }
     __builtin_amdgcn_wave_barrier();  // P reads done before the next chunk overwrites P
   }
+  if (nsplit > 1) {  // partial result (a split with no keys: m = -inf, l = 0, O = 0)
+    float* blk = sm2_work_block(work, blockIdx.z, h, qc, split, gridDim.y, (gridDim.x + nsplit - 1) / nsplit,
+                                nsplit, D);
+#pragma unroll
+    for (int qq = 0; qq < 8; ++qq) {
+      const int r = w * 8 + qq;
+      if (q0 + r < q_len) {
+        if (4 * lane < D) *(f32x4*)(blk + r * D + 4 * lane) = (f32x4){O[qq][0], O[qq][1], O[qq][2], O[qq][3]};
+        if (lane == 0) {
+          blk[SM2_QW * D + r] = m[qq];
+          blk[SM2_QW * D + SM2_QW + r] = l[qq];
+        }
+      }
+    }
+    return;
+  }
   if (4 * lane < D) {
 #pragma unroll
     for (int qq = 0; qq < 8; ++qq) {
@@ -268,7 +296,73 @@ __global__ __launch_bounds__(256) void attn_small2_kernel(const bf16* q, const b
   }
 }
 
+// merge of the key splits: O = sum_s 2^(m_s - M) O_s / sum_s 2^(m_s - M) l_s, M = max_s m_s (m in log2 units)
+__global__ __launch_bounds__(256) void attn_small2_combine_kernel(bf16* o, const int* segs, int D, long os,
+                                                                  int nsplit, const float* work) {
+  const int* sg = segs + blockIdx.z * 4;
+  const int q_row0 = sg[0], q_len = sg[1];
+  const int qc = blockIdx.x, q0 = qc * SM2_QW, h = blockIdx.y;
+  if (q0 >= q_len) return;
+  const int nq = min(SM2_QW, q_len - q0), n4 = D / 4;
+  const float* blk0 = sm2_work_block(const_cast<float*>(work), blockIdx.z, h, qc, 0, gridDim.y, gridDim.x, nsplit, D);
+  const long bstride = (long)SM2_QW * (D + 2);
+  for (int i = threadIdx.x; i < nq * n4; i += 256) {
+    const int r = i / n4, d = (i % n4) * 4;
+    float M = -INFINITY;
+    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, blk0[s * bstride + SM2_QW * D + r]);
+    float L = 0.f;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (M != -INFINITY) {
+      for (int s = 0; s < nsplit; ++s) {
+        const float* b = blk0 + s * bstride;
+        const float a = __builtin_amdgcn_exp2f(b[SM2_QW * D + r] - M);
+        L += a * b[SM2_QW * D + SM2_QW + r];
+        const f32x4 x = *(const f32x4*)(b + r * D + d);
+        acc[0] += a * x[0]; acc[1] += a * x[1]; acc[2] += a * x[2]; acc[3] += a * x[3];
+      }
+    }
+    const float inv = L > 0.f ? 1.f / L : 0.f;  // no keys at all: zeros, as SDPA
+    *(bf16x4*)(o + (long)(q_row0 + q0 + r) * os + h * D + d) =
+        (bf16x4){f2bf(acc[0] * inv), f2bf(acc[1] * inv), f2bf(acc[2] * inv), f2bf(acc[3] * inv)};
+  }
+}
+
 }  // namespace
+
+static bool sm2_applies(const void* q, const void* v, const void* o, int head_dim, int64_t q_stride, int64_t v_stride,
+                        int64_t o_stride) {
+  return head_dim <= SM2_D && !(q_stride % 8) && !(v_stride % 8) && !(o_stride % 4) &&
+         !(((uintptr_t)q | (uintptr_t)v) & 15) && !(((uintptr_t)o) & 7);
+}
+
+extern "C" int sa_attn_small(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
+                             int max_q_len, int max_kv_len, int heads, int head_dim, int64_t q_stride,
+                             int64_t k_stride, int64_t v_stride, int64_t o_stride, float scale, void* stream);
+
+extern "C" int sa_attn_small_split(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
+                                   int max_q_len, int max_kv_len, int heads, int head_dim, int64_t q_stride,
+                                   int64_t k_stride, int64_t v_stride, int64_t o_stride, float scale, int nsplit,
+                                   void* work, int64_t work_bytes, void* stream) {
+  if (!q || !k || !v || !o || !segs || nseg <= 0 || max_q_len <= 0 || heads <= 0 || nsplit < 2) return SA_ERR_ARG;
+  if (head_dim <= 0 || head_dim % 8 || max_kv_len <= 0 || (k_stride % 8) || (((uintptr_t)k) & 15)) return SA_ERR_ARG;
+  if (!sm2_applies(q, v, o, head_dim, q_stride, v_stride, o_stride)) return SA_ERR_ARG;
+  const int nchunks = (max_kv_len + SM2_KC - 1) / SM2_KC;
+  const int per = (nchunks + nsplit - 1) / nsplit;  // 64-key chunks per split
+  nsplit = (nchunks + per - 1) / per;               // no split without keys at the longest segment
+  const int nqc = (max_q_len + SM2_QW - 1) / SM2_QW;
+  const int64_t need = (int64_t)nseg * heads * nqc * nsplit * SM2_QW * (head_dim + 2) * 4;
+  if (!work || (((uintptr_t)work) & 15) || work_bytes < need) return SA_ERR_ARG;
+  if (nsplit < 2) return sa_attn_small(q, k, v, o, segs, nseg, max_q_len, max_kv_len, heads, head_dim, q_stride,
+                                       k_stride, v_stride, o_stride, scale, stream);
+  hipLaunchKernelGGL(attn_small2_kernel, dim3(nqc * nsplit, heads, nseg), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, segs, head_dim, q_stride, k_stride,
+                     v_stride, o_stride, scale * 1.4426950408889634f, nsplit, per * SM2_KC, (float*)work);
+  SA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(attn_small2_combine_kernel, dim3(nqc, heads, nseg), dim3(256), 0, (hipStream_t)stream, (bf16*)o,
+                     segs, head_dim, o_stride, nsplit, (const float*)work);
+  SA_LAUNCH_CHECK();
+  return SA_OK;
+}
 
 extern "C" int sa_attn_small(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
                              int max_q_len, int max_kv_len, int heads, int head_dim, int64_t q_stride,
@@ -277,12 +371,11 @@ extern "C" int sa_attn_small(const void* q, const void* k, const void* v, void* 
   if (head_dim <= 0 || head_dim > SMALL_MAXD || head_dim % 8 || max_kv_len <= 0) return SA_ERR_ARG;
   if ((k_stride % 8) || (((uintptr_t)k) & 15)) return SA_ERR_ARG;
   // the tiled kernel: 16-byte Q / K / V row chunks, 8-byte O stores (head_dim % 8 == 0 already holds)
-  if (head_dim <= SM2_D && !(q_stride % 8) && !(v_stride % 8) && !(o_stride % 4) &&
-      !(((uintptr_t)q | (uintptr_t)v) & 15) && !(((uintptr_t)o) & 7)) {
+  if (sm2_applies(q, v, o, head_dim, q_stride, v_stride, o_stride)) {
     dim3 grid2((max_q_len + SM2_QW - 1) / SM2_QW, heads, nseg);
     hipLaunchKernelGGL(attn_small2_kernel, grid2, dim3(256), 0, (hipStream_t)stream, (const bf16*)q, (const bf16*)k,
                        (const bf16*)v, (bf16*)o, segs, head_dim, q_stride, k_stride, v_stride, o_stride,
-                       scale * 1.4426950408889634f);
+                       scale * 1.4426950408889634f, 1, max_kv_len, (float*)nullptr);
     SA_LAUNCH_CHECK();
     return SA_OK;
   }

@@ -28,6 +28,17 @@ def _dt(t):
     raise TypeError(f"unsupported dtype {t.dtype}")
 
 
+_N_CU = {}
+
+
+def _n_cu(device) -> int:
+    """compute units of a device (cached)"""
+    i = torch.device(device).index or 0
+    if i not in _N_CU:
+        _N_CU[i] = torch.cuda.get_device_properties(i).multi_processor_count
+    return _N_CU[i]
+
+
 def _check(t, dtype, name):
     if not t.is_cuda:
         raise RuntimeError(f"{name}: expected a GPU tensor")
@@ -220,9 +231,22 @@ def mod_add(mod, e, out, e_jstride=None):
     return out
 
 
-def attention_small(q, k, v, out, segs, nseg, max_q_len, max_kv_len, heads, head_dim, scale=None):
+def attention_small(q, k, v, out, segs, nseg, max_q_len, max_kv_len, heads, head_dim, scale=None, nsplit=None):
+    """Attention for head dims sa_attn_fwd does not take.  nsplit = key splits per 32-query chunk (None: auto -- split
+    when the launch has at most half as many workgroups as the device has CUs, so each CU takes one split)."""
     if scale is None:
         scale = head_dim ** -0.5
+    wgs = nseg * heads * -(-max_q_len // 32)
+    if nsplit is None:
+        nsplit = 1
+        if head_dim <= 256 and q.is_cuda and 2 * wgs <= _n_cu(q.device):
+            nsplit = min(-(-max_kv_len // 64), _n_cu(q.device) // wgs)
+    if nsplit > 1:
+        work = torch.empty(wgs * nsplit * 32 * (head_dim + 2), device=q.device, dtype=torch.float32)
+        call("sa_attn_small_split", q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), segs.data_ptr(), nseg,
+             max_q_len, max_kv_len, heads, head_dim, q.stride(0), k.stride(0), v.stride(0), out.stride(0),
+             float(scale), int(nsplit), work.data_ptr(), work.numel() * 4, _stream())
+        return out
     call("sa_attn_small", q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), segs.data_ptr(), nseg, max_q_len,
          max_kv_len, heads, head_dim, q.stride(0), k.stride(0), v.stride(0), out.stride(0), float(scale), _stream())
     return out

@@ -368,6 +368,12 @@ class WanTransformer3DFantasyModel(nn.Module):
         pk.w_tp, pk.b_tp = bf("time_projection.1.weight"), f32("time_projection.1.bias")
         pk.mod = torch.cat([P[f"blocks.{i}.modulation"].detach() for i in range(self.num_layers)], 0).float().contiguous()
         pk.layers = []
+        # per-frame vocal K|V weights of every block stacked [layers * 2 * dim, vd]: the vocal context is the same for
+        # all blocks of a forward, so one GEMM forms every block's vocal keys and values (L.w_kv_v are views)
+        pk.w_kv_v_all = torch.cat([P[f"blocks.{i}.cross_attn.{n}_vocal.weight"].detach() for i in range(self.num_layers)
+                                   for n in ("k", "v")], 0).to(torch.bfloat16).contiguous()
+        pk.b_kv_v_all = torch.cat([P[f"blocks.{i}.cross_attn.{n}_vocal.bias"].detach() for i in range(self.num_layers)
+                                   for n in ("k", "v")], 0).float().contiguous()
         for i in range(self.num_layers):
             p = f"blocks.{i}."
             L = SimpleNamespace()
@@ -384,8 +390,7 @@ class WanTransformer3DFantasyModel(nn.Module):
             L.cnq, L.cnk, L.cnki = f32(c + "norm_q.weight"), f32(c + "norm_k.weight"), f32(c + "norm_k_img.weight")
             L.w_kv_t, L.b_kv_t = cat_bf(c + "k.weight", c + "v.weight"), cat_f(c + "k.bias", c + "v.bias")
             L.w_kv_i, L.b_kv_i = cat_bf(c + "k_img.weight", c + "v_img.weight"), cat_f(c + "k_img.bias", c + "v_img.bias")
-            L.w_kv_v, L.b_kv_v = (cat_bf(c + "k_vocal.weight", c + "v_vocal.weight"),
-                                  cat_f(c + "k_vocal.bias", c + "v_vocal.bias"))
+            L.w_kv_v, L.b_kv_v = pk.w_kv_v_all[2 * dim * i:2 * dim * (i + 1)], pk.b_kv_v_all[2 * dim * i:2 * dim * (i + 1)]
             L.w_co, L.b_co = bf(c + "o.weight"), f32(c + "o.bias")
             L.w_f0, L.b_f0 = bf(p + "ffn.0.weight"), f32(p + "ffn.0.bias")
             L.w_f2, L.b_f2 = bf(p + "ffn.2.weight"), f32(p + "ffn.2.bias")
@@ -594,7 +599,7 @@ class WanTransformer3DFantasyModel(nn.Module):
         return out
 
     def _sp_layer_rows(self, pk, L, li, x, ws, em, ex, pack_kw, rank, Lc, Lq, hg, hgd, grid, segs_rows, row_segs,
-                       ctx, vctx, kvv, nper, Gf, n_fr, use_cross3, rstreams, vrows=None):
+                       ctx, kvv, nper, Gf, n_fr, use_cross3, rstreams):
         """One DiT block (1B:650-695) with Ulysses sequence parallelism, each CFG row on its own stream
         (SA_SP_OVERLAP=4): row b's Q/K/V exchange (wan_xfuser.py:102-107) travels while the other rows compute
         (their QKV GEMMs, attention, O-projection, cross-attention and FFN), and its head-output exchange travels
@@ -609,7 +614,6 @@ class WanTransformer3DFantasyModel(nn.Module):
         tl, ni = ctx.text_len, ctx.img_len
         kvt, kvi = ctx.kv[li]
         nv = n_fr * nper
-        vrows = slice(0, nv) if vrows is None else vrows  # the vocal context rows this rank's queries read
         pend, back = [], []
         for b, st in enumerate(rstreams):  # self-attention inputs (1B:675-676) and the Q/K/V exchange
             rs = slice(b * Lc, (b + 1) * Lc)
@@ -640,8 +644,6 @@ class WanTransformer3DFantasyModel(nn.Module):
                 ops.linear(mod, L.w_cq, L.b_cq, ops.EPI_BF16, out=qc)
                 ops.qk_rmsnorm_rope(qc, 0, -1, L.cnq, None, dim, eps)
                 kv_b = kvv[b * nv:(b + 1) * nv]
-                ops.linear(vctx[b * nv + vrows.start:b * nv + vrows.stop], L.w_kv_v, L.b_kv_v, ops.EPI_BF16,
-                           out=kv_b[vrows])
                 if use_cross3:
                     kt, ki = kvt[b * tl:(b + 1) * tl], kvi[b * ni:(b + 1) * ni]
                     ops.attention_cross3(qc, kt[:, :dim], kt[:, dim:], tl, ki[:, :dim], ki[:, dim:], ni, kv_b[:, :dim],
@@ -850,7 +852,17 @@ class WanTransformer3DFantasyModel(nn.Module):
                 # zero-filled once: the pad columns past B * Lp are read (as P = 0 keys) by a partial last block, which
                 # stages a whole 64-key block: up to (B-1)*Lp + ceil64(Lp) <= ceil64(M) + 64 columns
                 ws.vt = torch.zeros(dim, (ws.x.shape[0] + 63) // 64 * 64 + 64, device=dev, dtype=torch.bfloat16)
-            kvv = torch.empty(B * n_fr * nper, 2 * dim, device=dev, dtype=torch.bfloat16)  # per-frame vocal K|V
+            # per-frame vocal K|V of every block in one GEMM [B * n_fr * nper, layers * 2 * dim] (1B:575-578: the
+            # block's k_vocal / v_vocal of the shared vocal context); under SP only the rows of the frames this rank's
+            # queries read (the others are never read)
+            kvv_all = torch.empty(B * n_fr * nper, pk.w_kv_v_all.shape[0], device=dev, dtype=torch.bfloat16)
+            if vnf == n_fr:
+                ops.linear(vctx, pk.w_kv_v_all, pk.b_kv_v_all, ops.EPI_BF16, out=kvv_all)
+            else:
+                for b in range(B):
+                    r0 = b * n_fr * nper + vf0 * nper
+                    ops.linear(vctx[r0:r0 + vnf * nper], pk.w_kv_v_all, pk.b_kv_v_all, ops.EPI_BF16,
+                               out=kvv_all[r0:r0 + vnf * nper])
             grid = (Fw, hp, wp)
             if sp_streams:
                 # every CFG row through the whole layer on its own HIP stream (_sp_layer_rows); rows are independent
@@ -860,10 +872,10 @@ class WanTransformer3DFantasyModel(nn.Module):
                     rs_.wait_stream(main)
                 row_segs = self._row_cross_segs(B, Lc, ctx, voc_list, dev)
             for li, L in enumerate(pk.layers):
+                kvv = kvv_all[:, 2 * dim * li:2 * dim * (li + 1)]
                 if sp_streams:
                     self._sp_layer_rows(pk, L, li, x, ws, emod[li], ex, pack_kw, rank, Lc, Lq, hg, hgd, grid,
-                                        segs_rows, row_segs, ctx, vctx, kvv, nper, G, n_fr, use_cross3, rstreams,
-                                        vrows=vr)
+                                        segs_rows, row_segs, ctx, kvv, nper, G, n_fr, use_cross3, rstreams)
                     continue
                 em = emod[li]  # [B, 6, dim]
                 # self-attention (1B:675-679)
@@ -947,13 +959,6 @@ class WanTransformer3DFantasyModel(nn.Module):
                 ops.linear(ws.mod, L.w_cq, L.b_cq, ops.EPI_BF16, out=qc)
                 ops.qk_rmsnorm_rope(qc, 0, -1, L.cnq, None, dim, self.eps)
                 kvt, kvi = ctx.kv[li]
-                if vnf == n_fr:
-                    ops.linear(vctx, L.w_kv_v, L.b_kv_v, ops.EPI_BF16, out=kvv)
-                else:  # SP: the rows of the frames this rank's queries attend to
-                    for b in range(B):
-                        r0 = b * n_fr * nper + vf0 * nper
-                        ops.linear(vctx[r0:r0 + vnf * nper], L.w_kv_v, L.b_kv_v, ops.EPI_BF16,
-                                   out=kvv[r0:r0 + vnf * nper])
                 if use_cross3:  # text + image + vocal in one launch, bf16 sum as 1B:602
                     ops.attention_cross3(qc, kvt[:, :dim], kvt[:, dim:], ctx.text_len, kvi[:, :dim], kvi[:, dim:],
                                          ctx.img_len, kvv[:, :dim], kvv[:, dim:], nper, G, n_fr, ws.att, B, Lc, H_,

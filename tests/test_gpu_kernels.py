@@ -398,10 +398,14 @@ def test_attention_cross3_tail_blocks_stay_inside_sources(x3k, monkeypatch):
     (64, 2, [(0, 70, 0, 5000)]),                                               # > 4096 keys (tiled kernel)
     (640, 8, [(0, 17, 0, 300)]),                                               # vocal projector (14B)
 ])
-def test_attention_small(D, H, segs):
+@pytest.mark.parametrize("nsplit", [1, None, 3, 16], ids=["unsplit", "auto", "split3", "split16"])
+def test_attention_small(D, H, segs, nsplit):
     """sa_attn_small (the head dims sa_attn_fwd does not take) vs torch fp32 per segment and head,
-    ragged query / key counts (tiled kernel for D <= 256, one wave per query above)."""
+    ragged query / key counts (tiled kernel for D <= 256, one wave per query above); split: sa_attn_small_split
+    (keys of each query chunk over several workgroups + merge; splits past a short segment's keys are empty)."""
     from stableavatar_amd import ops
+    if D > 256 and nsplit not in (1, None):
+        pytest.skip("key split: tiled kernel (D <= 256) only")
     nq = max(a + b for a, b, _, _ in segs)
     nk = max(c + d for _, _, c, d in segs)
     q = torch.randn(nq, H * D, device=dev).bfloat16()
@@ -409,7 +413,8 @@ def test_attention_small(D, H, segs):
     k, v = kv[:, :H * D], kv[:, H * D:]
     o = torch.full((nq, H * D), float("nan"), device=dev, dtype=torch.bfloat16)
     st = torch.tensor(segs, dtype=torch.int32, device=dev)
-    ops.attention_small(q, k, v, o, st, len(segs), max(b for _, b, _, _ in segs), max(d for *_, d in segs), H, D)
+    ops.attention_small(q, k, v, o, st, len(segs), max(b for _, b, _, _ in segs), max(d for *_, d in segs), H, D,
+                        nsplit=nsplit)
     for q0, ql, k0, kl in segs:
         for h in range(H):
             sl = slice(h * D, (h + 1) * D)
