@@ -19,7 +19,7 @@ from mp_util import collect  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def _free_port():
+def _rendezvous_file():
     """a fresh rendezvous file for the process group (file:// init: no TCP port to race for -- a port picked free and
     released can be taken before the store listens on it, EADDRINUSE)"""
     import tempfile
@@ -51,7 +51,7 @@ def _worker(rank, world, port, T, chunk, qret):
 def test_vae_decode_multi_rank_bit_exact(world, T, chunk):
     ctx = mp.get_context("spawn")
     qret = ctx.Queue()
-    port = _free_port()
+    port = _rendezvous_file()
     procs = [ctx.Process(target=_worker, args=(r, world, port, T, chunk, qret)) for r in range(world)]
     for p in procs:
         p.start()

@@ -26,7 +26,7 @@ pytestmark = pytest.mark.gpu
 STEPS = 3
 
 
-def _free_port():
+def _rendezvous_file():
     """a fresh rendezvous file for the process group (file:// init: no TCP port to race for -- a port picked free and
     released can be taken before the store listens on it, EADDRINUSE)"""
     import tempfile
@@ -123,7 +123,7 @@ def test_window_parallel_bit_exact(world, T, clip_length, overlap):
     assert n_win == {9: 3, 26: 8, 53: 17, 251: 22}[T]
     ctx = mp.get_context("spawn")
     qret = ctx.Queue()
-    port = _free_port()
+    port = _rendezvous_file()
     procs = [ctx.Process(target=_worker, args=(r, world, port, T, qret, clip_length, overlap)) for r in range(world)]
     for p in procs:
         p.start()
