@@ -26,7 +26,7 @@ enum {
   SA_EPI_GELU_ERF_BF16 = 4, /* C(bf16) = gelu_erf(A·W^T + bias)    (nn.GELU())           */
   SA_EPI_SILU_F32 = 5,      /* C(f32)  = silu(A·W^T + bias)                              */
   SA_EPI_BF16_T = 6,        /* C^T(bf16): C[n * ldc + m] = A·W^T + bias (persistent kernel, K % 128 == 0,
-                               M % 4 == 0, ldc >= M) */
+                               M % 4 == 0, ldc >= M): the V^T operand of sa_attn_fwd_ex kernel 4 */
   SA_EPI_BF16_TP32 = 7      /* SA_EPI_BF16_T with row 32c + 4q + r at column 32c + 8(q & 3) + 4(q >> 2) + r
                                (ldc >= M rounded up to 32, ldc and strideC % 8 == 0, C 16-B aligned:
                                16-byte stores): the V^T of sa_attn_fwd_ex kernel 3, the
@@ -80,10 +80,7 @@ int sa_attn_fwd(const void* q, const void* k, const void* v, void* o, const int3
 
 /* sa_attn_fwd with the kernel chosen per call (A/B without process-wide state): 0 = auto,
  * 1 = 8 waves x 32 queries on mfma_f32_16x16x32_bf16 (one 256-row workgroup per CU), 2 = the same body
- * with 4 waves x 32 queries (two 128-row workgroups per CU; bit-identical output).  V given as V^T
- * [heads * 128][v_stride] (SA_EPI_BF16_TP32's layout, keys permuted per 32; v_stride % 64 == 0, v 128-B aligned,
- * segments starting on 32-key boundaries, the columns of a ragged last 64-key block readable and finite): 3 = auto
- * between the 8- and 4-wave forms, 4 = the 4-wave form (bit-identical to 1 / 2). */
+ * with 4 waves x 32 queries (two 128-row workgroups per CU; bit-identical output). */
 int sa_attn_fwd_ex(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
                    int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride, int64_t v_stride,
                    int64_t o_stride, float scale, int accumulate, int kernel, void* stream);
@@ -95,18 +92,6 @@ int sa_attn_fwd_ex(const void* q, const void* k, const void* v, void* o, const i
 int sa_attn_fwd_map(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
                     int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride, int64_t v_stride,
                     int64_t o_stride, float scale, int accumulate, int kernel, const int32_t* o_rows, void* stream);
-
-/* sa_attn_fwd_map (kernel 3 / 4) with V^T in chunks of chunk_keys keys (a multiple of 64): key j of the flat key
- * axis is column j % chunk_keys of chunk j / chunk_keys, a [heads * 128][vt_stride] matrix at chunk_stride elements
- * per chunk from vt (the P order per 32 keys within each chunk; segments start on 64-key boundaries).  The Ulysses
- * exchange receives V^T of one (CFG row, source rank) per chunk (wan_xfuser.py:72-115 all-to-all).  vt_own (may be
- * NULL): chunk own_chunk of each group of chunks_per_row chunks (a CFG row's keys) is read from vt_own + row *
- * own_row_stride instead -- this rank's own tokens, straight from the V^T GEMM's output, never copied. */
-int sa_attn_fwd_vt_chunked(const void* q, const void* k, const void* vt, void* o, const int32_t* segs, int nseg,
-                           int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride,
-                           int64_t vt_stride, int64_t o_stride, float scale, int accumulate, int kernel,
-                           const int32_t* o_rows, int chunk_keys, int64_t chunk_stride, const void* vt_own,
-                           int64_t own_row_stride, int chunks_per_row, int own_chunk, void* stream);
 
 /* The three attentions of WanI2VTalkingCrossAttention.forward (1B:556-603) in one launch: per batch
  * row b, queries q[b*q_len + i] attend to text k/v rows [b*t_len, +t_len), image rows [b*i_len, +i_len)
@@ -159,12 +144,6 @@ int sa_qk_rmsnorm_rope(void* x, int64_t ldx, int q_col, int k_col, const float* 
 int sa_qkv_pack(const void* x, int64_t ldx, const float* wq, const float* wk, int M, int C, int head_dim, float eps,
                 const float* rope, int rows_per_batch, int tok_offset, int F, int H, int W, int n_frame_pairs,
                 int n_height_pairs, const int64_t* table, int G, int R, int my_part, int b_offset, void* stream);
-
-/* sa_qkv_pack without v (x = [M, >= 2C] q|k rows, the kv slabs [.., C/G] k only): the exchange path that moves V
- * as V^T (sa_gemm_bf16 SA_EPI_BF16_TP32 per CFG row, read by sa_attn_fwd_vt_chunked). */
-int sa_qk_pack(const void* x, int64_t ldx, const float* wq, const float* wk, int M, int C, int head_dim, float eps,
-               const float* rope, int rows_per_batch, int tok_offset, int F, int H, int W, int n_frame_pairs,
-               int n_height_pairs, const int64_t* table, int G, int R, int my_part, int b_offset, void* stream);
 
 /* cat(x, y, dim=channels) -> Conv3d(k=s=(1,2,2)) im2col (1B:972-976); out = bf16 [B, Lpad, Kpad]. */
 int sa_patch_im2col(const void* x, int64_t xb, int64_t xc, int64_t xf, int xcn, const void* y, int64_t yb, int64_t yc,

@@ -47,11 +47,9 @@ def fwd():
 
 res = []
 modes = os.environ.get("SA_SPRC_MODES", "1").split(",")  # SA_SP_OVERLAP values to time at each degree > 1
-vts = os.environ.get("SA_SPRC_VT", "0").split(",")  # SA_SP_VT values (V^T exchange on / off) at each degree > 1
 with torch.no_grad():
-    for N, ov, vt in [(n, o, v) for n in degrees for o in (modes if n > 1 else ["1"]) for v in (vts if n > 1 else ["1"])]:
+    for N, ov in [(n, o) for n in degrees for o in (modes if n > 1 else ["1"])]:
         os.environ["SA_SP_OVERLAP"] = ov
-        os.environ["SA_SP_VT"] = vt
         if N == 1:
             m.disable_multi_gpus_inference()
         else:
@@ -59,7 +57,7 @@ with torch.no_grad():
         fwd()  # builds the exchange buffers at this degree
         if N > 1:
             ex = m._sp_ex[1]
-            for buf in (ex.q, ex.kv, ex.obuf) + ((ex.vt, ex.svt) if ex.vt_mode else ()):
+            for buf in (ex.q, ex.kv, ex.obuf):
                 buf.normal_()
         for _ in range(2):
             fwd()
@@ -71,7 +69,7 @@ with torch.no_grad():
             hs.append((time.perf_counter() - t0) * 1e3)  # host enqueue time of the forward (no sync inside)
             torch.cuda.synchronize()
             ts.append((time.perf_counter() - t0) * 1e3)
-        r = {"kernel": "sp_rank_forward", "degree": N, "sp_overlap": ov, "sp_vt": vt, "ms": round(sorted(ts)[1], 2),
+        r = {"kernel": "sp_rank_forward", "degree": N, "sp_overlap": ov, "ms": round(sorted(ts)[1], 2),
              "host_enqueue_ms": round(sorted(hs)[1], 2)}
         res.append(r)
         print(json.dumps(r), flush=True)

@@ -22,11 +22,9 @@ SIGNATURES = {
     "sa_attn_fwd": "pppppiiiillllfip",
     "sa_attn_fwd_ex": "pppppiiiillllfiip",
     "sa_attn_fwd_map": "pppppiiiillllfiipp",
-    "sa_attn_fwd_vt_chunked": "pppppiiiillllfiipilpliip",
     "sa_layernorm_mod": "pliplipppplpiiifp",
     "sa_qk_rmsnorm_rope": "pliippiiifpiiiiiiip",
     "sa_qkv_pack": "plppiiifpiiiiiiipiiiip",
-    "sa_qk_pack": "plppiiifpiiiiiiipiiiip",
     "sa_patch_im2col": "plllipllliiiiipiip",
     "sa_unpatchify": "pliiiiiipip",
     "sa_timestep_embed": "piipp",

@@ -31,16 +31,6 @@ struct AttnArgs {
   float c;  // softmax scale * log2(e)
   int accumulate;
   const int* orows;  // output row of query row r = orows[r] (null: r); the Ulysses exchange's receive layout
-  // V^T forms only: the key columns come in chunks of vchunk keys (a multiple of 64; 0 = one [heads*128][vs] matrix),
-  // chunk c at c * vcstride elements from v, each a [heads*128][vs] matrix -- the Ulysses exchange's V^T, one chunk
-  // per (CFG row, source rank) as received
-  int vchunk;
-  long vcstride;
-  // chunked form: chunk vown_idx of each CFG row's vnper chunks (this rank's own tokens, never sent) is read from
-  // vown + row * vown_bstride instead (null: every chunk from v)
-  const bf16* vown;
-  long vown_bstride;
-  int vnper, vown_idx;
 };
 
 constexpr int D = 128;
@@ -884,10 +874,11 @@ __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
   // K/V pieces: each wave moves 2 x 1-KB pieces (4 rows each) of K and of V per block; lane -> row
   // (lane / 16), stored position lane % 16 holding source chunk (lane % 16) ^ swizzle(row).  By
   // buffer_load...lds from SGPR descriptors, per-lane 32-bit offsets and the block in soffset: no 64-bit
-  // address VALU.  The range check takes voffset + soffset + the instruction offset against the records (the
-  // chunked V^T form read zeros past a records value that left soffset out, r6j); a partial last block is
-  // staged from a descriptor of its own (base = its first row, soffset 0) whose range ends at the segment's
-  // last row, so its rows past kv_len read as zeros (masked in S, and 0 x 0 in PV) instead of whatever follows
+  // address VALU.  The range check takes voffset + soffset + the instruction offset against the records (a V^T
+  // form reading per-source chunks, measured and removed in round 6, read zeros past a records value that left
+  // soffset out); a partial last block is staged from a descriptor of its own (base = its first row, soffset 0)
+  // whose range ends at the segment's last row, so its rows past kv_len read as zeros (masked in S, and 0 x 0 in
+  // PV) instead of whatever follows
   const int nkb = (kv_len + KVB - 1) / KVB;
   const long tail0 = (long)(nkb - 1) * KVB;  // first row of the last block
   const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
@@ -1002,9 +993,8 @@ __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
 // element of a row readable and finite through that block: the partial last block reads the keys past kv_len,
 // masked to P = 0).  2-stage K/V ring: block kb+1's DMA issued at block kb (one block of lead, vmcnt(0) +
 // __syncthreads() per block).
-template <int NW>
 __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
-  constexpr int QBW = NW * 32, PPW = 16 / NW;
+  constexpr int NW = 8, QBW = NW * 32, PPW = 16 / NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nx = gridDim.x, ny = gridDim.y;
   const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
@@ -1046,22 +1036,9 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
   const __amdgpu_buffer_rsrc_t rkt = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.k + (kv_row0 + tail0) * a.ks + h * D), (short)0, (int)((kv_len - tail0 - 1) * a.ks * 2 + 256),
       0x00020000);
-  // V^T: the head's 128 d-rows from key kv_row0, each through the segment's last block (chunked: from chunk 0, the
-  // block's chunk and column in soffset; the range check covers the per-lane offsets, i.e. one chunk's 128 rows)
-  // (the records bound the per-lane offsets plus soffset: one chunk's rows in place, every chunk through the
-  // segment's last block in the chunk array)
-  const long vcol0 = a.vchunk ? 0 : kv_row0;
-  const long vspan = a.vchunk ? ((long)((kv_row0 + nkb * KVB - 1) / a.vchunk) * a.vcstride + a.vchunk)
-                              : (long)nkb * KVB;
-  const int vrec = (int)(((long)(D - 1) * a.vs + vspan) * 2);
-  const int vrec_own = (int)(((long)(D - 1) * a.vs + a.vchunk) * 2);
-  const __amdgpu_buffer_rsrc_t rv =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(a.v + (long)h * D * a.vs + vcol0), (short)0, vrec, 0x00020000);
-  // this rank's own chunk of the segment's CFG row (chunked form with vown)
-  const int vrow_b = a.vchunk && a.vown ? kv_row0 / a.vchunk / a.vnper : 0;
-  const int own_c = a.vchunk && a.vown ? vrow_b * a.vnper + a.vown_idx : -1;
-  const __amdgpu_buffer_rsrc_t rvo = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)((a.vown ? a.vown + vrow_b * a.vown_bstride : a.v) + (long)h * D * a.vs), (short)0, vrec_own,
+  // V^T: the head's 128 d-rows from key kv_row0, each through the segment's last block
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.v + (long)h * D * a.vs + kv_row0), (short)0, (int)(((long)(D - 1) * a.vs + (long)nkb * KVB) * 2),
       0x00020000);
   const int dw = wave;  // this wave's share of the K / V pieces
   int koff[PPW], voff[PPW];
@@ -1075,20 +1052,14 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
   const uint32_t lds_dma = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem) + dw * PPW * 1024);
   auto stage = [&](int kb, int buf) {  // LDS: 2 stages as K | V pairs
     const bool tail = ragged && kb == nkb - 1;
-    const int key0 = kv_row0 + kb * KVB;  // wave-uniform
-    const int ks_off = tail ? 0 : kb * KVB * (int)a.ks * 2;
-    const int vc = a.vchunk ? key0 / a.vchunk : 0;
-    const bool own = vc == own_c;
-    const int vs_off = !a.vchunk ? kb * KVB * 2
-                       : own     ? (key0 % a.vchunk) * 2
-                                 : (int)(((long)vc * a.vcstride + key0 % a.vchunk) * 2);
-    const __amdgpu_buffer_rsrc_t bk = tail ? rkt : rk, bv = own ? rvo : rv;
+    const int ks_off = tail ? 0 : kb * KVB * (int)a.ks * 2, vs_off = kb * KVB * 2;
+    const __amdgpu_buffer_rsrc_t bk = tail ? rkt : rk;
     const int kdst = buf * STAGE_BYTES, vdst = buf * STAGE_BYTES + TILE_BYTES;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(bk, LDS_PTR((uintptr_t)(lds_dma + kdst + i * 1024)), 16, koff[i],
                                                ks_off, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(bv, LDS_PTR((uintptr_t)(lds_dma + vdst + i * 1024)), 16, voff[i],
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, LDS_PTR((uintptr_t)(lds_dma + vdst + i * 1024)), 16, voff[i],
                                                vs_off, 0, 0);
     }
   };
@@ -1112,7 +1083,7 @@ __device__ __forceinline__ void attn_fwd_vt_body(const AttnArgs& a) {
     __syncthreads();
   };
   stage(0, 0);
-  if (NW == 8 && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
   sync();
   if (1 < nkb) stage(1, 1);
   attn_v6t_block<0, TILE_BYTES, true>(st, qf, ka, vb, 0, kv_len, g);
@@ -1357,73 +1328,54 @@ __global__ __launch_bounds__(256, 2) void attn_cross3_w4_kernel(Cross3Args a) { 
 
 __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) { attn_fwd_v6_body<8>(a); }
 __global__ __launch_bounds__(256, 2) void attn_fwd_v6_w4_kernel(AttnArgs a) { attn_fwd_v6_body<4>(a); }
-__global__ __launch_bounds__(512) void attn_fwd_v6t_kernel(AttnArgs a) { attn_fwd_vt_body<8>(a); }
-__global__ __launch_bounds__(256, 2) void attn_fwd_v6t_w4_kernel(AttnArgs a) { attn_fwd_vt_body<4>(a); }
+__global__ __launch_bounds__(512) void attn_fwd_v6t_kernel(AttnArgs a) { attn_fwd_vt_body(a); }
 
 }  // namespace
 
 // kernel: 0 = auto, 1 = attn_fwd_v6_kernel (8 waves x 32 queries, mfma_f32_16x16x32_bf16), 2 = the 4-wave
-// attn_fwd_v6_w4_kernel (two workgroups per CU); V^T operand (attn_fwd_vt_body): 3 = auto between the 8-wave
-// attn_fwd_v6t_kernel and the 4-wave attn_fwd_v6t_w4_kernel, 4 = the 4-wave one.  Auto estimates both launches in
-// rounds of one 8-wave workgroup per CU: a 4-wave round holds two workgroups per CU and runs 3 % slower per FLOP; a
-// last 4-wave round of at most one workgroup per CU (one wave per SIMD) takes 0.75 of a round (measured,
+// attn_fwd_v6_w4_kernel (two workgroups per CU).  Auto estimates both launches in rounds of one 8-wave
+// workgroup per CU: a 4-wave round holds two workgroups per CU and runs 3 % slower per FLOP; a last 4-wave
+// round of at most one workgroup per CU (one wave per SIMD) takes 0.75 of a round (measured,
 // profiles/r02/attn_sp_shapes.json: the Ulysses N = 8 shape, 378 / 756 workgroups, 1.036 vs 0.927 ms).
 // o_rows (optional, device int32 indexed by query row): query row r's output goes to row o_rows[r] of o --
 // the sequence-parallel path writes this rank's own token chunk straight into the O-projection's input
 // panels and the other chunks into their send slabs (stableavatar_amd/sp.py)
-static bool attn_pick_w4(int nseg, int heads, int max_q_len) {
-  static int cus[64] = {0};  // per device, queried once
-  int dev = 0, ncu = 256;
-  if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
-    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus[dev] = 256;
-    ncu = cus[dev] > 0 ? cus[dev] : 256;
-  }
-  const long n8 = (long)nseg * heads * ((max_q_len + 255) / 256), n4 = (long)nseg * heads * ((max_q_len + 127) / 128);
-  const long t8 = (n8 + ncu - 1) / ncu, full = n4 / (2 * ncu), rem = n4 % (2 * ncu);
-  const double t4 = 1.03 * (full + (rem == 0 ? 0.0 : (rem <= ncu ? 0.75 : 1.0)));
-  return t4 < (double)t8;
-}
-
-static int attn_fwd_launch(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
-                           int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride,
-                           int64_t v_stride, int64_t o_stride, float scale, int accumulate, int kernel,
-                           const int32_t* o_rows, int v_chunk, int64_t v_chunk_stride, const void* v_own,
-                           int64_t v_own_bstride, int v_chunks_per_row, int v_own_idx, void* stream) {
+extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
+                               int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride,
+                               int64_t v_stride, int64_t o_stride, float scale, int accumulate, int kernel,
+                               const int32_t* o_rows, void* stream) {
   if (!q || !k || !v || !o || !segs || nseg <= 0 || max_q_len <= 0 || heads <= 0) return SA_ERR_ARG;
   if (head_dim != D) return SA_ERR_ARG;
   if ((q_stride | k_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
   if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)o)) & 15) return SA_ERR_ARG;
-  if (kernel < 0 || kernel > 4) return SA_ERR_ARG;
-  if (kernel >= 3 && (v_stride % 64 || (((uintptr_t)v) & 127))) return SA_ERR_ARG;  // V^T rows: whole 64-key blocks
-  if (v_chunk && (kernel < 3 || v_chunk < 0 || v_chunk % KVB || v_chunk_stride % 64 ||
-                  v_chunk_stride < (int64_t)heads * D * v_stride || v_stride < v_chunk))
-    return SA_ERR_ARG;
-  if (v_own && (!v_chunk || v_chunks_per_row <= 0 || v_own_idx < 0 || v_own_idx >= v_chunks_per_row ||
-                v_own_bstride % 64 || (((uintptr_t)v_own) & 127)))
-    return SA_ERR_ARG;
+  if (kernel < 0 || kernel > 3) return SA_ERR_ARG;
+  if (kernel == 3 && (v_stride % 64 || (((uintptr_t)v) & 127))) return SA_ERR_ARG;  // V^T rows: whole 64-key blocks
   static const bool attr = [] {  // one-time, thread-safe
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6_w4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_v6t_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_v6t_w4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
     return true;
   }();
   (void)attr;
   AttnArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, segs,
-             q_stride, k_stride, v_stride, o_stride, scale * 1.4426950408889634f, accumulate, o_rows,
-             v_chunk, (long)v_chunk_stride, (const bf16*)v_own, (long)v_own_bstride, v_chunks_per_row,
-             v_own_idx};
-  if (kernel == 0) kernel = attn_pick_w4(nseg, heads, max_q_len) ? 2 : 1;
-  if (kernel == 3 && attn_pick_w4(nseg, heads, max_q_len)) kernel = 4;
+             q_stride, k_stride, v_stride, o_stride, scale * 1.4426950408889634f, accumulate, o_rows};
+  if (kernel == 0) {
+    static int cus[64] = {0};  // per device, queried once
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+      if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus[dev] = 256;
+      ncu = cus[dev] > 0 ? cus[dev] : 256;
+    }
+    const long n8 = (long)nseg * heads * ((max_q_len + 255) / 256), n4 = (long)nseg * heads * ((max_q_len + 127) / 128);
+    const long t8 = (n8 + ncu - 1) / ncu, full = n4 / (2 * ncu), rem = n4 % (2 * ncu);
+    const double t4 = 1.03 * (full + (rem == 0 ? 0.0 : (rem <= ncu ? 0.75 : 1.0)));
+    kernel = t4 < (double)t8 ? 2 : 1;
+  }
   if (kernel == 2) {
     dim3 grid((max_q_len + 127) / 128, heads, nseg);
     hipLaunchKernelGGL(attn_fwd_v6_w4_kernel, grid, dim3(256), LDS_BYTES, (hipStream_t)stream, a);
-  } else if (kernel == 4) {
-    dim3 grid((max_q_len + 127) / 128, heads, nseg);
-    hipLaunchKernelGGL(attn_fwd_v6t_w4_kernel, grid, dim3(256), LDS_BYTES, (hipStream_t)stream, a);
   } else if (kernel == 3) {  // v = V^T [heads * 128][v_stride] (attn_fwd_vt_body)
     dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
     hipLaunchKernelGGL(attn_fwd_v6t_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
@@ -1433,27 +1385,6 @@ static int attn_fwd_launch(const void* q, const void* k, const void* v, void* o,
   }
   SA_LAUNCH_CHECK();
   return SA_OK;
-}
-
-extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
-                               int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride,
-                               int64_t v_stride, int64_t o_stride, float scale, int accumulate, int kernel,
-                               const int32_t* o_rows, void* stream) {
-  return attn_fwd_launch(q, k, v, o, segs, nseg, max_q_len, heads, head_dim, q_stride, k_stride, v_stride, o_stride,
-                         scale, accumulate, kernel, o_rows, 0, 0, nullptr, 0, 0, 0, stream);
-}
-
-extern "C" int sa_attn_fwd_vt_chunked(const void* q, const void* k, const void* vt, void* o, const int32_t* segs,
-                                      int nseg, int max_q_len, int heads, int head_dim, int64_t q_stride,
-                                      int64_t k_stride, int64_t vt_stride, int64_t o_stride, float scale,
-                                      int accumulate, int kernel, const int32_t* o_rows, int chunk_keys,
-                                      int64_t chunk_stride, const void* vt_own, int64_t own_row_stride,
-                                      int chunks_per_row, int own_chunk, void* stream) {
-  if (kernel != 3 && kernel != 4) return SA_ERR_ARG;
-  if (chunk_keys <= 0) return SA_ERR_ARG;
-  return attn_fwd_launch(q, k, vt, o, segs, nseg, max_q_len, heads, head_dim, q_stride, k_stride, vt_stride, o_stride,
-                         scale, accumulate, kernel, o_rows, chunk_keys, chunk_stride, vt_own, own_row_stride,
-                         chunks_per_row, own_chunk, stream);
 }
 
 extern "C" int sa_attn_fwd_ex(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,

@@ -297,7 +297,6 @@ struct PackArgs {
   const long* table;     // [G*R][6]
   int G, R, my_part;
   int b_offset;          // CFG row of launch row 0 is b_offset + row / rows_per_batch
-  int with_v;            // 0: q and k only (the exchange moves V as V^T from its own GEMM)
 };
 
 struct PackStore {
@@ -312,12 +311,12 @@ struct PackStore {
       const long* e = table + (long)(my_part * G + g) * 6;
       store8<bf16>((bf16*)e[0] + b * e[2] + t * e[1] + w, y);
     } else {
-      const u32x4 vv = vrow ? *(const u32x4*)(vrow + c0) : (u32x4){0u, 0u, 0u, 0u};
+      const u32x4 vv = *(const u32x4*)(vrow + c0);
       for (int r = 0; r < R; ++r) {
         const long* e = table + (long)(r * G + g) * 6;
         bf16* kd = (bf16*)e[3] + b * e[5] + t * e[4] + w;
         store8<bf16>(kd, y);
-        if (vrow) *(u32x4*)(kd + hgd) = vv;
+        *(u32x4*)(kd + hgd) = vv;
       }
     }
   }
@@ -337,7 +336,7 @@ __global__ __launch_bounds__(256) void qkv_pack_kernel(PackArgs pa) {
   if (row >= a.M) return;
   const bf16* base = a.x + (long)row * a.ldx;
   const PackStore ps{pa.table, pa.G, pa.R, pa.my_part, a.C / pa.G, (long)(pa.b_offset + row / a.rows_per_batch),
-                     (long)(row % a.rows_per_batch), pa.with_v ? base + 2 * a.C : nullptr};
+                     (long)(row % a.rows_per_batch), base + 2 * a.C};
   if (PAIR && a.rope && a.head_dim == 128) {  // the 1.3B shape: the pair path, as the in-place launcher takes
     qk_pair_row(a, row, lane, [&](int i, const float* yq, const float* yk) {
       ps.put<true>(i * 512 + lane * 8, yq);
@@ -507,18 +506,18 @@ extern "C" int sa_qk_rmsnorm_rope(void* x, int64_t ldx, int q_col, int k_col, co
   return SA_OK;
 }
 
-static int qkv_pack_launch(const void* x, int64_t ldx, const float* wq, const float* wk, int M, int C, int head_dim,
+extern "C" int sa_qkv_pack(const void* x, int64_t ldx, const float* wq, const float* wk, int M, int C, int head_dim,
                            float eps, const float* rope, int rows_per_batch, int tok_offset, int F, int H, int W,
                            int n_frame_pairs, int n_height_pairs, const int64_t* table, int G, int R, int my_part,
-                           int b_offset, int with_v, void* stream) {
-  if (!x || !wq || !wk || !table || M <= 0 || C <= 0 || C % 512 || C > 512 * MAXV || ldx % 8 || ldx < (with_v ? 3 : 2) * C)
+                           int b_offset, void* stream) {
+  if (!x || !wq || !wk || !table || M <= 0 || C <= 0 || C % 512 || C > 512 * MAXV || ldx % 8 || ldx < 3 * C)
     return SA_ERR_ARG;
   if (G <= 0 || R <= 0 || my_part < 0 || my_part >= R || b_offset < 0 || rows_per_batch <= 0) return SA_ERR_ARG;
   if (C % G || (C / G) % 8) return SA_ERR_ARG;
   if (rope && (head_dim % 8 || F <= 0 || H <= 0 || W <= 0)) return SA_ERR_ARG;
   PackArgs pa{QkArgs{(bf16*)x, ldx, 0, C, wq, wk, M, C, head_dim, eps, rope, rows_per_batch, tok_offset, F, H, W,
                      n_frame_pairs, n_height_pairs},
-              (const long*)table, G, R, my_part, b_offset, with_v};
+              (const long*)table, G, R, my_part, b_offset};
   static const bool generic = getenv("SA_QK_GENERIC") != nullptr;  // the in-place launcher's A/B switch
   if (C == 1536 && !generic)
     hipLaunchKernelGGL((qkv_pack_kernel<3, true>), dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, pa);
@@ -530,20 +529,4 @@ static int qkv_pack_launch(const void* x, int64_t ldx, const float* wq, const fl
     hipLaunchKernelGGL((qkv_pack_kernel<0, false>), dim3((M + 3) / 4), dim3(256), 0, (hipStream_t)stream, pa);
   SA_LAUNCH_CHECK();
   return SA_OK;
-}
-
-extern "C" int sa_qkv_pack(const void* x, int64_t ldx, const float* wq, const float* wk, int M, int C, int head_dim,
-                           float eps, const float* rope, int rows_per_batch, int tok_offset, int F, int H, int W,
-                           int n_frame_pairs, int n_height_pairs, const int64_t* table, int G, int R, int my_part,
-                           int b_offset, void* stream) {
-  return qkv_pack_launch(x, ldx, wq, wk, M, C, head_dim, eps, rope, rows_per_batch, tok_offset, F, H, W,
-                         n_frame_pairs, n_height_pairs, table, G, R, my_part, b_offset, 1, stream);
-}
-
-extern "C" int sa_qk_pack(const void* x, int64_t ldx, const float* wq, const float* wk, int M, int C, int head_dim,
-                          float eps, const float* rope, int rows_per_batch, int tok_offset, int F, int H, int W,
-                          int n_frame_pairs, int n_height_pairs, const int64_t* table, int G, int R, int my_part,
-                          int b_offset, void* stream) {
-  return qkv_pack_launch(x, ldx, wq, wk, M, C, head_dim, eps, rope, rows_per_batch, tok_offset, F, H, W,
-                         n_frame_pairs, n_height_pairs, table, G, R, my_part, b_offset, 0, stream);
 }

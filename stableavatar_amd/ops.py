@@ -111,18 +111,16 @@ def bmm_nt(a, b, out, epilogue=EPI_F32, kernel=GEMM_AUTO):
 
 
 ATTN_AUTO = 0
-# kernel ids of sa_attn_fwd_ex that read V as V^T [H*128, Rv]: keys permuted per 32 in P's order (the QKV GEMM's
-# EPI_BF16_TP32 output); 3 = auto between the 8-wave and the 4-wave form, 4 = the 4-wave form
-ATTN_VT_P32, ATTN_VT_P32_W4 = 3, 4
+# kernel id of sa_attn_fwd_ex that reads V as V^T [H*128, Rv]: keys permuted per 32 in P's order (the QKV GEMM's
+# EPI_BF16_TP32 output)
+ATTN_VT_P32 = 3
 
 
 def attention(q, k, v, out, segs, nseg, max_q_len, heads, head_dim=128, scale=None, accumulate=False,
-              kernel=ATTN_AUTO, o_rows=None, v_chunks=None, v_own=None):
+              kernel=ATTN_AUTO, o_rows=None):
     """Flash attention over row-segment table `segs` (int32 [nseg,4] on device); kernel = per-call
     schedule selection (sa_attn_fwd_ex; 0 = auto); o_rows = int32 device map query row -> output row of
-    `out` (sa_attn_fwd_map); v_chunks = (chunk_keys, chunk_stride): v is V^T in key chunks (sa_attn_fwd_vt_chunked,
-    kernel ATTN_VT_P32 / ATTN_VT_P32_W4; v = chunk 0 [H*128, row stride]); v_own = (tensor, row_stride,
-    chunks_per_row, own_chunk): that chunk of every row read from the tensor instead."""
+    `out` (sa_attn_fwd_map)."""
     for t, n in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
         _check(t, torch.bfloat16, f"attention.{n}")
         assert t.stride(-1) == 1
@@ -131,13 +129,6 @@ def attention(q, k, v, out, segs, nseg, max_q_len, heads, head_dim=128, scale=No
         assert o_rows.dtype == torch.int32 and o_rows.is_cuda and o_rows.is_contiguous()
     if scale is None:
         scale = head_dim ** -0.5
-    if v_chunks is not None:
-        call("sa_attn_fwd_vt_chunked", q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), segs.data_ptr(),
-             nseg, max_q_len, heads, head_dim, q.stride(0), k.stride(0), v.stride(0), out.stride(0), float(scale),
-             int(accumulate), kernel, _p(o_rows), int(v_chunks[0]), int(v_chunks[1]),
-             0 if v_own is None else v_own[0].data_ptr(), 0 if v_own is None else int(v_own[1]),
-             0 if v_own is None else int(v_own[2]), 0 if v_own is None else int(v_own[3]), _stream())
-        return out
     call("sa_attn_fwd_map", q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), segs.data_ptr(), nseg,
          max_q_len, heads, head_dim, q.stride(0), k.stride(0), v.stride(0), out.stride(0), float(scale),
          int(accumulate), kernel, _p(o_rows), _stream())
@@ -182,15 +173,14 @@ def qk_rmsnorm_rope(x, q_col, k_col, wq, wk, C, eps, rope=None, rows_per_batch=0
 
 
 def qkv_pack(x, wq, wk, C, eps, table, G, R, my_part, rope=None, rows_per_batch=0, tok_offset=0, grid=(1, 1, 1),
-             head_dim=128, n_frame_pairs=0, n_height_pairs=0, b_offset=0, with_v=True):
+             head_dim=128, n_frame_pairs=0, n_height_pairs=0, b_offset=0):
     """RMSNorm + RoPE of the q / k columns of the [M, 3C] QKV rows x, written with v into the sequence-parallel
-    send slabs / attention inputs that the int64 device `table` [G*R, 6] names (sa_qkv_pack); with_v=False: q and k
-    only, x = [M, >= 2C] (sa_qk_pack, the V^T exchange)."""
+    send slabs / attention inputs that the int64 device `table` [G*R, 6] names (sa_qkv_pack)."""
     _check(x, torch.bfloat16, "qkv_pack.x")
-    assert x.stride(1) == 1 and x.shape[1] >= (3 if with_v else 2) * C
+    assert x.stride(1) == 1 and x.shape[1] >= 3 * C
     assert table.dtype == torch.int64 and table.is_cuda and tuple(table.shape) == (G * R, 6)
     F, H, W = grid
-    call("sa_qkv_pack" if with_v else "sa_qk_pack", x.data_ptr(), x.stride(0), wq.data_ptr(), wk.data_ptr(), x.shape[0], C, head_dim, float(eps),
+    call("sa_qkv_pack", x.data_ptr(), x.stride(0), wq.data_ptr(), wk.data_ptr(), x.shape[0], C, head_dim, float(eps),
          _p(rope), rows_per_batch, tok_offset, F, H, W, n_frame_pairs, n_height_pairs, table.data_ptr(), G, R, my_part,
          b_offset, _stream())
 

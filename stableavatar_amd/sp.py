@@ -160,29 +160,18 @@ class UlyssesExchange:
 
     ``loopback=True`` sends this rank's own chunk through the transport as well (its Q/K/V through send slabs of
     its own, its head outputs through the first half of ``obuf``), a point-to-point transfer to itself: at degree 1
-    on RCCL that runs every send / receive of the exchange on the GPU the box has, with a bit-identical result.
-
-    ``vt=True`` moves V as V^T (the single-GPU attention's operand layout, SA_EPI_BF16_TP32): ``kv`` holds k only
-    [B*Lp, hg*D]; ``svt`` [B, G*hg*D, Lc] is this rank's V^T (every head, its tokens), written by a transposed-
-    epilogue GEMM per CFG row, and head group j's rows of it (one contiguous [hg*D, Lc] block) are the V send slab
-    of the ranks of group j; ``vt`` [B, N, hg*D, Lc] receives chunk (b, r) = the V^T of rank r's tokens for this
-    rank's head group -- the attention reads it in key chunks of Lc (sa_attn_fwd_vt_chunked), this rank's own chunk
-    straight from ``svt`` (unless loopback, where it arrives like the others)."""
+    on RCCL that runs every send / receive of the exchange on the GPU the box has, with a bit-identical result."""
 
     def __init__(self, plan: SPPlan, B: int, Lc: int, D: int, device, group=None, dtype=torch.bfloat16,
-                 loopback=False, vt=False):
+                 loopback=False):
         self.plan, self.group, self.B, self.Lc, self.D = plan, group, B, Lc, D
-        self.loopback, self.vt_mode = bool(loopback), bool(vt)
+        self.loopback = bool(loopback)
         p = plan
         N, G, g = p.world, p.G, p.group
         self.hgd = hgd = p.hg * D
         self.Lq, self.Lp = G * Lc, N * Lc
         self.q = torch.empty(B * self.Lq, hgd, device=device, dtype=dtype)
-        kvw = hgd if vt else 2 * hgd  # k | v rows, or k only (V^T travels on its own)
-        self.kv = torch.empty(B * self.Lp, kvw, device=device, dtype=dtype)
-        if vt:
-            self.svt = torch.empty(B, G * hgd, Lc, device=device, dtype=dtype)
-            self.vt = torch.empty(B, N, hgd, Lc, device=device, dtype=dtype)
+        self.kv = torch.empty(B * self.Lp, 2 * hgd, device=device, dtype=dtype)
         # + slack rows: the O-projection's last tile reads up to its tile height past the last panel
         # (sa_gemm_bf16_panels; the buffer range check does not cover the panel offset).  The slack comes from
         # the library (sa_gemm_panel_slack_rows = the tallest GEMM tile), so a taller tile cannot outgrow it.
@@ -193,9 +182,9 @@ class UlyssesExchange:
         self.pan = self.obuf[G * B * Lc:2 * G * B * Lc]
         self.remote = [d for d in range(N) if d != p.rank or self.loopback]
         self.sq = {d: torch.empty(B, Lc, hgd, device=device, dtype=dtype) for d in self.remote if d // G == p.part}
-        self.skv = {d: torch.empty(B, Lc, kvw, device=device, dtype=dtype) for d in self.remote}
+        self.skv = {d: torch.empty(B, Lc, 2 * hgd, device=device, dtype=dtype) for d in self.remote}
         qv = self.q.view(B, self.Lq, hgd)
-        kvv = self.kv.view(B, self.Lp, kvw)
+        kvv = self.kv.view(B, self.Lp, 2 * hgd)
         rows = []
         for d in range(N):
             if d == p.rank and not self.loopback:
@@ -220,31 +209,17 @@ class UlyssesExchange:
         p = self.plan
         G, Lc, Lq, Lp = p.G, self.Lc, self.Lq, self.Lp
         sends, recvs = [], []
-        hgd = self.hgd
         for b in rows:
             for d in self.remote:
                 if d in self.sq:
                     sends.append((self.sq[d][b], d))
                 sends.append((self.skv[d][b], d))
-                if self.vt_mode:
-                    j = d % G
-                    sends.append((self.svt[b, j * hgd:(j + 1) * hgd], d))
             for r in self.remote:
                 if r // G == p.part:
                     q0 = b * Lq + (r % G) * Lc
                     recvs.append((self.q[q0:q0 + Lc], r))
                 recvs.append((self.kv[b * Lp + r * Lc:b * Lp + (r + 1) * Lc], r))
-                if self.vt_mode:
-                    recvs.append((self.vt[b, r], r))
         return _p2p(sends, recvs, self.group)
-
-    def vt_args(self):
-        """(v, v_chunks, v_own) of ops.attention over the received V^T (chunk (b, r) at vt[b, r]; this rank's own
-        chunk from svt unless loopback)"""
-        p, hgd, Lc = self.plan, self.hgd, self.Lc
-        own = None if self.loopback else (self.svt[:, p.group * hgd:(p.group + 1) * hgd], self.svt.stride(0),
-                                          p.world, p.rank)
-        return self.vt.view(-1, Lc), (Lc, hgd * Lc), own
 
     def tokens(self, rows) -> Pending:
         """Head outputs of CFG rows ``rows`` back to the owners of their tokens (after the attention)."""

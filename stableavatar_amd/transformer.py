@@ -467,46 +467,13 @@ class WanTransformer3DFantasyModel(nn.Module):
     def _sp_exchange(self, plan, B, Lc, dev):
         """the sequence-parallel exchange buffers (attention inputs, send slabs, output / panel buffer, pack
         table, output row map) for this shape, kept across layers, steps and calls (one shape at a time)"""
-        # SA_SP_VT=1: V travels as V^T (read by the V^T attention kernels, sa_attn_fwd_vt_chunked) when the token
-        # chunk is whole 64-key blocks; bit-identical, but per rank 1-4 % slower at N = 2 / 8 than k | v rows (the
-        # separate V^T GEMM launch per CFG row costs more than the V^T attention saves at 1/N of the queries:
-        # profiles/r06/sp_rank_compute_vt_ab_r6k.jsonl), so off by default
-        vt = (torch.device(dev).type == "cuda" and Lc % 64 == 0 and os.environ.get("SA_SP_VT", "0") != "0")
-        key = (plan, B, Lc, self.d, str(dev), id(self.sp_group), self._sp_loopback, vt)
+        key = (plan, B, Lc, self.d, str(dev), id(self.sp_group), self._sp_loopback)
         ex = self._sp_ex
         if ex is None or ex[0] != key:
             self._sp_ex = None  # free the previous shape's buffers first
             ex = self._sp_ex = (key, sp.UlyssesExchange(plan, B, Lc, self.d, dev, self.sp_group,
-                                                        loopback=self._sp_loopback, vt=vt))
+                                                        loopback=self._sp_loopback))
         return ex[1]
-
-    def _sp_qkv(self, L, ws, ex, rows, pack_kw, rope_kw, b_offset=0):
-        """QKV projection + pack of the rows `rows` (a slice of ws.mod / ws.qkv, CFG rows b_offset..) into the
-        exchange: with V^T, q | k through the GEMM into the QKV rows and the pack, v per CFG row through the
-        transposed-epilogue GEMM straight into this rank's V^T (ex.svt), else q | k | v rows and the pack"""
-        dim = self.dim
-        if ex.vt_mode:
-            ops.linear(ws.mod[rows], L.w_qk, L.b_qk, ops.EPI_BF16, out=ws.qkv[rows, :2 * dim])
-            Lc = ex.Lc
-            n = (rows.stop - rows.start) // Lc
-            for i in range(n):
-                r0 = rows.start + i * Lc
-                ops.linear(ws.mod[r0:r0 + Lc], L.w_v, L.b_v, ops.EPI_BF16_TP32, out=ex.svt[b_offset + i])
-            ops.qkv_pack(ws.qkv[rows], L.nq, L.nk, dim, self.eps, b_offset=b_offset, with_v=False, **pack_kw,
-                         **rope_kw)
-        else:
-            ops.linear(ws.mod[rows], L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv[rows])
-            ops.qkv_pack(ws.qkv[rows], L.nq, L.nk, dim, self.eps, b_offset=b_offset, **pack_kw, **rope_kw)
-
-    def _sp_attention(self, ex, segs, nseg, Lq, hg, hgd):
-        """this rank's Ulysses attention (its query part x head group over every key), outputs by row map"""
-        if ex.vt_mode:
-            v, chunks, own = ex.vt_args()
-            ops.attention(ex.q, ex.kv, v, ex.obuf, segs, nseg, Lq, hg, kernel=ops.ATTN_VT_P32, o_rows=ex.omap,
-                          v_chunks=chunks, v_own=own)
-        else:
-            ops.attention(ex.q, ex.kv[:, :hgd], ex.kv[:, hgd:], ex.obuf, segs, nseg, Lq, hg,
-                          kernel=self.attn_kernel, o_rows=ex.omap)
 
     @staticmethod
     def _ctx_key(context, clip_fea):
@@ -653,13 +620,15 @@ class WanTransformer3DFantasyModel(nn.Module):
             with torch.cuda.stream(st):
                 ops.layernorm_mod(x[rs], ws.mod[rs], eps, shift=em[b:b + 1, 0], scale=em[b:b + 1, 1],
                                   rows_per_batch=Lc)
-                self._sp_qkv(L, ws, ex, rs, pack_kw, rope_kw, b_offset=b)
+                ops.linear(ws.mod[rs], L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv[rs])
+                ops.qkv_pack(ws.qkv[rs], L.nq, L.nk, dim, eps, b_offset=b, **pack_kw, **rope_kw)
                 pend.append(ex.heads([b]))
         for b, st in enumerate(rstreams):  # attention over the full key sequence, head outputs back to the owners
             with torch.cuda.stream(st):
                 pend[b].wait()
                 ev0 = self._record_event()
-                self._sp_attention(ex, segs_rows[b], 1, Lq, hg, hgd)
+                ops.attention(ex.q, ex.kv[:, :hgd], ex.kv[:, hgd:], ex.obuf, segs_rows[b], 1, Lq, hg,
+                              kernel=self.attn_kernel, o_rows=ex.omap)
                 self._record_span(ev0, rows=1, batch=B)
                 back.append(ex.tokens([b]))
         for b, st in enumerate(rstreams):  # O-projection + gated residual, cross-attention, FFN (1B:677-691)
@@ -921,13 +890,15 @@ class WanTransformer3DFantasyModel(nn.Module):
                     pend = []
                     for b in range(B):
                         rs = slice(b * Lc, (b + 1) * Lc)
-                        self._sp_qkv(L, ws, ex, rs, pack_kw, rope_kw, b_offset=b)
+                        ops.linear(ws.mod[rs], L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv[rs])
+                        ops.qkv_pack(ws.qkv[rs], L.nq, L.nk, dim, self.eps, b_offset=b, **pack_kw, **rope_kw)
                         pend.append(ex.heads([b]))
                     back = []
                     for b in range(B):
                         pend[b].wait()
                         ev0 = self._record_event()
-                        self._sp_attention(ex, segs_rows[b], 1, Lq, hg, hgd)
+                        ops.attention(ex.q, ex.kv[:, :hgd], ex.kv[:, hgd:], ex.obuf, segs_rows[b], 1, Lq, hg,
+                                      kernel=self.attn_kernel, o_rows=ex.omap)
                         self._record_span(ev0, rows=1, batch=B)
                         back.append(ex.tokens([b]))
                     for b in range(B):
@@ -943,17 +914,20 @@ class WanTransformer3DFantasyModel(nn.Module):
                         pend = []
                         for b in range(B):
                             rs = slice(b * Lc, (b + 1) * Lc)
-                            self._sp_qkv(L, ws, ex, rs, pack_kw, rope_kw, b_offset=b)
+                            ops.linear(ws.mod[rs], L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv[rs])
+                            ops.qkv_pack(ws.qkv[rs], L.nq, L.nk, dim, self.eps, b_offset=b, **pack_kw, **rope_kw)
                             pend.append(ex.heads([b]))
                         for p_ in pend:
                             p_.wait()
                     else:  # one exchange per direction for all rows
-                        self._sp_qkv(L, ws, ex, slice(0, B * Lc), pack_kw, rope_kw)
+                        ops.linear(ws.mod, L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv)
+                        ops.qkv_pack(ws.qkv, L.nq, L.nk, dim, self.eps, **pack_kw, **rope_kw)
                         ex.heads(range(B)).wait()
                     # Ulysses: full-sequence attention of this rank's (query part, head group), outputs written
                     # to the owners' send slabs / this rank's own O-projection panel, then heads -> tokens
                     ev0 = self._record_event()
-                    self._sp_attention(ex, segs_self, B, Lq, hg, hgd)
+                    ops.attention(ex.q, ex.kv[:, :hgd], ex.kv[:, hgd:], ex.obuf, segs_self, B, Lq, hg,
+                                  kernel=self.attn_kernel, o_rows=ex.omap)
                     self._record_span(ev0, rows=B, batch=B)
                     ex.tokens(range(B)).wait()
                     a0, pnl = ex.panels()

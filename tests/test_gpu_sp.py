@@ -109,65 +109,6 @@ def test_sp_matches_reference_golden(world, model):
             assert e_single < 1e-3, (rank, name, ov, e_single)
 
 
-def _vt_worker(rank, world, port, qret):
-    """the V^T exchange (k slabs + V^T blocks, the V^T attention with the own block in place) against the k | v
-    exchange (V-rows attention), same process, every schedule: bit-identical.  128x128 video (32x32 latent, 256
-    tokens per frame, 5 frames): Lc = 640 / 320 at N = 2 / 4, whole 64-key blocks"""
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    import torch.distributed as dist
-    sys.path.insert(0, HERE)
-    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
-    try:
-        from test_gpu_dit import make_model, run
-        from golden_cases import DIT_SMALL
-        from stableavatar_amd import synthetic
-        m = make_model(DIT_SMALL)
-        B, H, W = 3, 32, 32
-        lat = synthetic.seeded_normal((1, 16, 5, H, W), 201)
-        a = synthetic.seeded_normal((1, 39, 768), 206)
-        inp = dict(x=torch.cat([lat] * 3), y=synthetic.seeded_normal((B, 20, 5, H, W), 202),
-                   context=[synthetic.seeded_normal((20, 64), 203)] * 2 + [synthetic.seeded_normal((25, 64), 204)],
-                   clip_fea=synthetic.seeded_normal((1, 257, 1280), 205).expand(3, -1, -1).contiguous(),
-                   vocal=torch.cat([torch.zeros_like(a), a, a]), t=torch.full((3,), 937.5), seq_len=5 * 16 * 16,
-                   n_frames=17)
-        m.disable_multi_gpus_inference()
-        single = run(m, inp)
-        m.enable_multi_gpus_inference()
-        res = []
-        for ov in ("0", "4"):
-            os.environ["SA_SP_OVERLAP"] = ov
-            out = {}
-            for vt in ("1", "0"):
-                os.environ["SA_SP_VT"] = vt
-                out[vt] = run(m, inp)
-                assert m._sp_ex[1].vt_mode == (vt == "1")
-            res.append((ov, torch.equal(out["1"], out["0"]), ((out["1"] - single).norm() / single.norm()).item(),
-                        bool(torch.isfinite(out["1"]).all())))
-        qret.put((rank, res))
-    finally:
-        dist.destroy_process_group()
-
-
-@pytest.mark.timeout(400)
-@pytest.mark.parametrize("world", [2, 4])
-def test_sp_vt_exchange_bit_identical(world):
-    ctx = mp.get_context("spawn")
-    qret = ctx.Queue()
-    port = _rendezvous_file()
-    procs = [ctx.Process(target=_vt_worker, args=(r, world, port, qret)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = collect(procs, qret, world, timeout=360)
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
-    for rank, rows in res:
-        for ov, same, e_single, finite in rows:
-            print(f"world {world} rank {rank} overlap {ov}: V^T exchange bit-identical {same}, vs single-GPU "
-                  f"{e_single:.1e}")
-            assert finite and same and e_single < 1e-3, (rank, ov, same, e_single)
-
-
 def _rccl_worker(port, overlap, qret):
     """RCCL (backend "nccl") process group of ONE rank with the SP path forced on, in loopback mode
     (UlyssesExchange(loopback=True)): this rank's own token chunk goes through the point-to-point transport to

@@ -4,7 +4,7 @@ SURVEY.md §8 row a18; the seam is usp_attn_forward, wan/dist/wan_xfuser.py:72-1
 * sa_qkv_pack -- the Q/K/V RMSNorm + RoPE writing per-destination slabs -- against the in-place
   sa_qk_rmsnorm_rope followed by a torch scatter: bit-identical (same arithmetic, different stores);
 * sa_attn_fwd_map -- the attention storing by output row map -- against the plain attention scattered by
-  torch: bit-identical; sa_attn_fwd_vt_chunked (V^T in per-source chunks, the own chunk in place) against it;
+  torch: bit-identical;
 * sa_gemm_bf16_panels -- the O-projection reading column panels -- against the same GEMM on the
   contiguous matrix: bit-identical (same K order).
 Runs on the MI355X only."""
@@ -23,17 +23,15 @@ def _seed():
     torch.manual_seed(0)
 
 
-@pytest.mark.parametrize("vt", [False, True], ids=["qkv", "qk_vt_exchange"])
 @pytest.mark.parametrize("C,H,world,rank", [(1536, 12, 1, 0), (1536, 12, 2, 1), (1536, 12, 8, 5), (5120, 40, 8, 3),
                                             (1536, 12, 3, 2)])
-def test_qkv_pack_matches_inplace_norm_and_scatter(C, H, world, rank, vt):
-    """vt: sa_qk_pack (the V^T exchange) -- q and k only, the k slabs C/G wide"""
+def test_qkv_pack_matches_inplace_norm_and_scatter(C, H, world, rank):
     from stableavatar_amd.transformer import rope_table
     B, D = 3, 128
     F, Hh, W = 3, 4, 5                       # 60 tokens; the SP pad rows past them are normalised, not rotated
     Lc = sp.padded_len(F * Hh * W, world) // world
     plan = sp.make_plan(world, rank, H)
-    ex = sp.UlyssesExchange(plan, B, Lc, D, dev, vt=vt)
+    ex = sp.UlyssesExchange(plan, B, Lc, D, dev)
     qkv = torch.randn(B * Lc, 3 * C, device=dev).bfloat16()
     wq, wk = torch.randn(C, device=dev), torch.randn(C, device=dev)
     rope = rope_table(D).to(dev)
@@ -49,62 +47,22 @@ def test_qkv_pack_matches_inplace_norm_and_scatter(C, H, world, rank, vt):
         if per_row:
             for b in range(B):
                 ops.qkv_pack(qkv[b * Lc:(b + 1) * Lc], wq, wk, C, 1e-6, ex.table, plan.G, plan.R, plan.part,
-                             b_offset=b, with_v=not vt, **rope_kw)
+                             b_offset=b, **rope_kw)
         else:
-            ops.qkv_pack(qkv, wq, wk, C, 1e-6, ex.table, plan.G, plan.R, plan.part, with_v=not vt, **rope_kw)
+            ops.qkv_pack(qkv, wq, wk, C, 1e-6, ex.table, plan.G, plan.R, plan.part, **rope_kw)
         torch.cuda.synchronize()
         r3 = ref.view(B, Lc, 3, plan.G, hgd)
         for d, (qd, kd) in ex.slabs.items():
             g = d % plan.G
             if qd is not None:
                 assert torch.equal(qd, r3[:, :, 0, g]), d
-            if vt:
-                assert kd.shape[-1] == hgd and torch.equal(kd, r3[:, :, 1, g]), d
-            else:
-                assert torch.equal(kd[..., :hgd], r3[:, :, 1, g]) and torch.equal(kd[..., hgd:], r3[:, :, 2, g]), d
+            assert torch.equal(kd[..., :hgd], r3[:, :, 1, g]) and torch.equal(kd[..., hgd:], r3[:, :, 2, g]), d
         outs.append([t.clone() for t in (ex.q, ex.kv)])
     # rows of the attention inputs the pack does not own stay untouched (NaN), the own chunk is filled
     qv = outs[0][0].view(B, plan.G, Lc, hgd)
     assert not qv[:, plan.group].isnan().any()
     if plan.G > 1:
         assert qv[:, (plan.group + 1) % plan.G].isnan().all()
-
-
-@pytest.mark.parametrize("own", [False, True], ids=["all_chunks", "own_chunk_in_place"])
-@pytest.mark.parametrize("kernel", [3, 4], ids=["vt_auto", "vt_wg128"])
-def test_attention_vt_chunked(kernel, own):
-    """sa_attn_fwd_vt_chunked (the Ulysses V^T exchange's attention): V^T received as one [H*128, Lc] chunk per
-    (CFG row, source rank), the own rank's chunk read in place from the V^T GEMM output (every other chunk of that
-    slot NaN), a ragged last key block, output by row map -- bit-identical to the V-rows kernel on the flat layout"""
-    from stableavatar_amd.kbench import vt_layout
-    B, N, Lc, H, D = 2, 4, 192, 3, 128
-    Lp, Lq = N * Lc, 300
-    S = Lp - 40                                 # the keys past S (SP pads) are finite and masked
-    q = torch.randn(B * Lq, H * D, device=dev).bfloat16()
-    k = torch.randn(B * Lp, H * D, device=dev).bfloat16()
-    v = torch.randn(B * Lp, H * D, device=dev).bfloat16()
-    segs = torch.tensor([[b * Lq, Lq, b * Lp, S] for b in range(B)], dtype=torch.int32, device=dev)
-    rows = torch.randperm(2 * B * Lq, device=dev)[:B * Lq].to(torch.int32)
-    ref = torch.full((2 * B * Lq, H * D), float("nan"), device=dev, dtype=torch.bfloat16)
-    ops.attention(q, k, v, ref, segs, B, Lq, H, kernel=1, o_rows=rows)
-    vt = torch.empty(B, N, H * D, Lc, device=dev, dtype=torch.bfloat16)
-    for b in range(B):
-        for r in range(N):
-            vt[b, r] = vt_layout(v[b * Lp + r * Lc:b * Lp + (r + 1) * Lc], 3)[:, :Lc]
-    v_own = None
-    if own:
-        oi = 2                                  # this rank; its V^T: head group 1 of a 2-group GEMM output
-        svt = torch.full((B, 2 * H * D, Lc), float("nan"), device=dev, dtype=torch.bfloat16)
-        svt[:, H * D:] = vt[:, oi]
-        vt[:, oi] = float("nan")
-        v_own = (svt[:, H * D:], svt.stride(0), N, oi)
-    o = torch.full_like(ref, float("nan"))
-    ops.attention(q, k, vt.view(-1, Lc), o, segs, B, Lq, H, kernel=kernel, o_rows=rows, v_chunks=(Lc, H * D * Lc),
-                  v_own=v_own)
-    torch.cuda.synchronize()
-    assert torch.equal(o[rows.long()], ref[rows.long()])
-    with pytest.raises(RuntimeError):           # chunks that are not whole 64-key blocks
-        ops.attention(q, k, vt.view(-1, Lc), o, segs, B, Lq, H, kernel=kernel, v_chunks=(Lc - 32, H * D * Lc))
 
 
 @pytest.mark.parametrize("kernel", [1, 2], ids=["wg256", "wg128"])

@@ -30,9 +30,7 @@ def _sdpa(q, k, v):
 def _pack(ex, mine, plan):
     """test-side restatement of sa_qkv_pack's scatter (the norm / RoPE aside): head group g of this rank's
     q to destination my_part*G + g, of k | v to every r*G + g -- through the same slab views the device
-    table names.  V^T exchange (sa_qk_pack + the transposed-epilogue V GEMM): k only into the slabs, and this
-    rank's V^T of every head into ex.svt (the layout inside a chunk -- P's key order on the GPU -- is the
-    producer's and the consumer's business; the exchange moves whole [hg*D, Lc] blocks)"""
+    table names"""
     B, Lc = mine.shape[:2]
     hg = plan.hg
     for d, (qd, kd) in ex.slabs.items():
@@ -43,30 +41,10 @@ def _pack(ex, mine, plan):
             qd.copy_(grp[:, :, 0])
         else:
             assert d // plan.G != plan.part
-        kd.copy_(grp[:, :, 1] if ex.vt_mode else torch.cat([grp[:, :, 1], grp[:, :, 2]], -1))
-    if ex.vt_mode:
-        ex.svt.copy_(mine[:, :, 2].reshape(B, Lc, -1).transpose(1, 2))
+        kd.copy_(torch.cat([grp[:, :, 1], grp[:, :, 2]], -1))
 
 
-def _vt_values(ex, plan, B, Lp, hg, D):
-    """V [B, Lp, hg, D] of this rank's head group as the V^T attention reads it: chunk (b, r) from ex.vt, this
-    rank's own chunk from ex.svt unless loopback (ops.attention's v_chunks / v_own, sa_attn_fwd_vt_chunked)"""
-    v, (ck, cs), own = ex.vt_args()
-    N, Lc = plan.world, ex.Lc
-    out = torch.empty(B, Lp, hg * D)
-    chunks = v.reshape(-1)
-    for b in range(B):
-        for r in range(N):
-            c = b * N + r
-            if own is not None and r == own[3]:
-                blk = own[0][b]
-            else:
-                blk = chunks[c * cs:(c + 1) * cs].view(hg * D, ck)
-            out[b, r * Lc:(r + 1) * Lc] = blk.t()
-    return out.view(B, Lp, hg, D)
-
-
-def _worker(rank, world, port, B, Lp, H, D, q_ret, loopback=False, vt=False):
+def _worker(rank, world, port, B, Lp, H, D, q_ret, loopback=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
@@ -79,7 +57,7 @@ def _worker(rank, world, port, B, Lp, H, D, q_ret, loopback=False, vt=False):
         hg, G = plan.hg, plan.G
         res = []
         for rows in ([list(range(B))], [[b] for b in range(B)]):          # batched / per CFG row
-            ex = sp.UlyssesExchange(plan, B, Lc, D, "cpu", dtype=torch.float32, loopback=loopback, vt=vt)
+            ex = sp.UlyssesExchange(plan, B, Lc, D, "cpu", dtype=torch.float32, loopback=loopback)
             assert (rank in ex.remote) == loopback
             # the pack table is the slab views' addresses and strides (elements)
             for d, (qd, kd) in ex.slabs.items():
@@ -94,14 +72,9 @@ def _worker(rank, world, port, B, Lp, H, D, q_ret, loopback=False, vt=False):
             # the attention inputs: query part's tokens (head group g) and all keys
             qpart = qkv[:, plan.part * Lq:(plan.part + 1) * Lq, 0, plan.group * hg:(plan.group + 1) * hg]
             assert torch.equal(ex.q.view(B, Lq, hg, D), qpart)
-            if vt:
-                kh, vh = ex.kv.view(B, Lp, hg, D), _vt_values(ex, plan, B, Lp, hg, D)
-                assert torch.equal(vh, qkv[:, :, 2, plan.group * hg:(plan.group + 1) * hg])
-            else:
-                kvh = ex.kv.view(B, Lp, 2, hg, D)
-                kh, vh = kvh[:, :, 0], kvh[:, :, 1]
-            assert torch.equal(kh, qkv[:, :, 1, plan.group * hg:(plan.group + 1) * hg])
-            o = _sdpa(ex.q.view(B, Lq, hg, D), kh, vh).reshape(B * Lq, hg * D)
+            kvh = ex.kv.view(B, Lp, 2, hg, D)
+            assert torch.equal(kvh[:, :, 0], qkv[:, :, 1, plan.group * hg:(plan.group + 1) * hg])
+            o = _sdpa(ex.q.view(B, Lq, hg, D), kvh[:, :, 0], kvh[:, :, 1]).reshape(B * Lq, hg * D)
             ex.obuf[ex.omap.long()] = o                                   # the attention's row-mapped store
             for r in rows:
                 ex.tokens(r).wait()
@@ -118,22 +91,17 @@ def _worker(rank, world, port, B, Lp, H, D, q_ret, loopback=False, vt=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,H,loopback,vt", [(2, 12, False, False), (3, 12, False, False), (4, 12, False, False),
-                                                  (8, 12, False, False), (8, 40, False, False), (1, 12, True, False),
-                                                  (2, 12, True, False), (8, 12, True, False), (2, 12, False, True),
-                                                  (4, 12, False, True), (8, 12, False, True), (8, 40, False, True),
-                                                  (2, 12, True, True)])
-def test_ulysses_exchange_matches_full_attention(world, H, loopback, vt):
+@pytest.mark.parametrize("world,H,loopback", [(2, 12, False), (3, 12, False), (4, 12, False), (8, 12, False),
+                                               (8, 40, False), (1, 12, True), (2, 12, True), (8, 12, True)])
+def test_ulysses_exchange_matches_full_attention(world, H, loopback):
     """12 heads: the 1.3B model (N = 8 is U4 x 2 query parts); 40 heads: the 14B model (N = 8 is U8).  loopback:
-    each rank's own chunk also goes through the transport (to itself), the layout the degree-1 RCCL test runs.
-    vt: V moved as V^T blocks (the V^T attention's operand), this rank's own block read in place"""
+    each rank's own chunk also goes through the transport (to itself), the layout the degree-1 RCCL test runs"""
     B, D = 3, 16
     Lp = sp.padded_len(48, world)
     ctx = mp.get_context("spawn")
     qret = ctx.Queue()
     port = _rendezvous_file()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, B, Lp, H, D, qret, loopback, vt))
-             for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, B, Lp, H, D, qret, loopback)) for r in range(world)]
     for p in procs:
         p.start()
     res = [qret.get(timeout=120) for _ in range(world)]
