@@ -1168,9 +1168,8 @@ __device__ __forceinline__ void attn_cross3_body(const Cross3Args& a) {
   // staging by buffer descriptors rebased per block (SALU: base = the block's first row of this batch row's
   // source, range = its rows up to the source's last), so rows past the source read as zeros and are masked;
   // per-lane 32-bit offsets -- no 64-bit address VALU per block (the round-3 kernel formed clamped 64-bit row
-  // addresses for every piece of every block).  With the block offset in soffset instead, a descriptor whose
-  // records cover the whole source would still let the image stream's last block (257 = 4 x 64 + 1 keys) stage
-  // the 63 rows past its last key from memory; rebased, those rows read as zeros
+  // addresses for every piece of every block).  The rows past a source's last key (the image stream's last block:
+  // 257 = 4 x 64 + 1 keys) read as zeros through the records bound (the range check counts soffset too, round 6)
   int srow[PPW], kch[PPW], vch[PPW];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
