@@ -93,6 +93,16 @@ int sa_attn_fwd_map(const void* q, const void* k, const void* v, void* o, const 
                     int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride, int64_t v_stride,
                     int64_t o_stride, float scale, int accumulate, int kernel, const int32_t* o_rows, void* stream);
 
+/* sa_attn_fwd_map on the 8-wave kernel with the keys of the LAST split_tiles (segment, head, 256-query block) tiles
+ * split in two halves, each half a workgroup of its own writing fp32 partials (unnormalised O, running max, row sum)
+ * to work, and a second launch merging them (log-sum-exp) into o.  For launches whose last round over the CUs is at
+ * most half full (the Ulysses N = 8 per-rank shape: 378 tiles on 256 CUs -> the last 122 as 244 halves: 1.5 rounds
+ * instead of 2).  work: >= split_tiles * 2 * 256 * (head_dim + 2) floats, 16-B aligned. */
+int sa_attn_fwd_split(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
+                      int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride, int64_t v_stride,
+                      int64_t o_stride, float scale, int accumulate, const int32_t* o_rows, int split_tiles, void* work,
+                      int64_t work_bytes, void* stream);
+
 /* The three attentions of WanI2VTalkingCrossAttention.forward (1B:556-603) in one launch: per batch
  * row b, queries q[b*q_len + i] attend to text k/v rows [b*t_len, +t_len), image rows [b*i_len, +i_len)
  * and the vocal rows of their latent frame, [(b*n_frames + f)*nper, +nper) with

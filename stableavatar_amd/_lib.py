@@ -22,6 +22,7 @@ SIGNATURES = {
     "sa_attn_fwd": "pppppiiiillllfip",
     "sa_attn_fwd_ex": "pppppiiiillllfiip",
     "sa_attn_fwd_map": "pppppiiiillllfiipp",
+    "sa_attn_fwd_split": "pppppiiiillllfipiplp",
     "sa_layernorm_mod": "pliplipppplpiiifp",
     "sa_qk_rmsnorm_rope": "pliippiiifpiiiiiiip",
     "sa_qkv_pack": "plppiiifpiiiiiiipiiiip",

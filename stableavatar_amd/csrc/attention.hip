@@ -31,6 +31,11 @@ struct AttnArgs {
   float c;  // softmax scale * log2(e)
   int accumulate;
   const int* orows;  // output row of query row r = orows[r] (null: r); the Ulysses exchange's receive layout
+  // key-split launches (attn_fwd_v6_split_kernel): a 1-D grid whose first split_full workgroups are whole query tiles
+  // and whose last 2 x split_n are the two key halves of the last split_n tiles (tile = (segment, head, query block),
+  // nqb query blocks per segment, nheads heads); the halves write unnormalised fp32 partials to work
+  int nqb, nheads, split_full, split_n;
+  float* work;
 };
 
 constexpr int D = 128;
@@ -832,17 +837,57 @@ namespace {
 // query rows, one wave per SIMD, two workgroups per CU -- the same per-SIMD pairing at half the work
 // granularity, for launches whose 256-row workgroup count leaves the last round over the CUs mostly empty
 // (the per-rank shapes of Ulysses SP: 378 workgroups at N = 8)
-template <int NW>
+// SPLIT: the key-split launch (AttnArgs split_*): a half workgroup runs the flash loop over its half of the keys and
+// writes O (unnormalised), the running max and the row sum instead of the output; attn_split_merge_kernel combines the
+// two halves
+template <int NW, bool SPLIT = false>
 __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
   constexpr int QBW = NW * 32, PPW = 16 / NW;  // query rows per workgroup, K (and V) 1-KB pieces per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nx = gridDim.x, ny = gridDim.y;
-  const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
-  const int qb = flat % nx, h = (flat / nx) % ny, seg = flat / (nx * ny);
+  int qb, h, seg, half = -1, stile = 0;
+  if constexpr (SPLIT) {
+    int tile;
+    if ((int)blockIdx.x < a.split_full) {
+      tile = xcd_remap(blockIdx.x, a.split_full);
+    } else {
+      const int idx = blockIdx.x - a.split_full;
+      stile = idx >> 1;
+      half = idx & 1;
+      tile = a.split_full + stile;
+    }
+    qb = tile % a.nqb;
+    h = (tile / a.nqb) % a.nheads;
+    seg = tile / (a.nqb * a.nheads);
+  } else {
+    const int nx = gridDim.x, ny = gridDim.y;
+    const int flat = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
+    qb = flat % nx;
+    h = (flat / nx) % ny;
+    seg = flat / (nx * ny);
+  }
   const int* sg = a.segs + seg * 4;
-  const int q_row0 = sg[0], q_len = sg[1], kv_row0 = sg[2], kv_len = sg[3];
+  const int q_row0 = sg[0], q_len = sg[1];
+  int kv_row0 = sg[2], kv_len = sg[3];
+  if (SPLIT && half >= 0) {  // this half's keys: whole 64-key blocks in the first half
+    const int kper = ((kv_len + 1) / 2 + KVB - 1) / KVB * KVB;
+    if (half == 0) {
+      kv_len = min(kv_len, kper);
+    } else {
+      kv_row0 += kper;
+      kv_len -= kper;
+    }
+  }
   if (qb * QBW >= q_len) return;
   const int tid = threadIdx.x, lane = tid & 63;
+  float* const wblk = SPLIT && half >= 0 ? a.work + ((long)stile * 2 + half) * QBW * (D + 2) : nullptr;
+  if (SPLIT && half >= 0 && kv_len <= 0) {  // an empty half: m = -inf, l = 0, O = 0
+    for (int i = tid; i < QBW * D; i += NW * 64) wblk[i] = 0.f;
+    for (int i = tid; i < QBW; i += NW * 64) {
+      wblk[QBW * D + i] = -INFINITY;
+      wblk[QBW * D + QBW + i] = 0.f;
+    }
+    return;
+  }
   if (kv_len <= 0) {  // a segment with no keys: zeros, as SDPA (nothing to add when accumulating)
     if (!a.accumulate)
       for (int i = tid; i < QBW * (D / 8); i += NW * 64) {
@@ -955,6 +1000,19 @@ __device__ __forceinline__ void attn_fwd_v6_body(const AttnArgs& a) {
     attn_v6_block<0, TILE_BYTES, false>(st, qf, ka, va, kb + 1, kv_len, g);
   }
 
+  if (SPLIT && half >= 0) {  // partials: O^T[d][query] of this lane's d = 16 dt + 4 g + i, the query's max and sum
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int row = wave * 32 + qt * 16 + r16;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) *(f32x4*)(wblk + row * D + dt * 16 + 4 * g) = st.O[dt][qt];
+      if (g == 0) {
+        wblk[QBW * D + row] = -st.negm[qt];
+        wblk[QBW * D + QBW + row] = st.L[qt][0];
+      }
+    }
+    return;
+  }
   // lane rows g and g^1 (lanes l, l^16) hold adjacent 4-column groups of one query row: one
   // permlane16 swap per dword pairs d tiles (dt, dt+1) so each lane stores 16 contiguous bytes (T21)
 #pragma unroll
@@ -1326,6 +1384,39 @@ __global__ __launch_bounds__(512) void attn_cross3_kernel(Cross3Args a) { attn_c
 __global__ __launch_bounds__(256, 2) void attn_cross3_w4_kernel(Cross3Args a) { attn_cross3_body<4, 2>(a); }
 
 __global__ __launch_bounds__(512) void attn_fwd_v6_kernel(AttnArgs a) { attn_fwd_v6_body<8>(a); }
+__global__ __launch_bounds__(512) void attn_fwd_v6_split_kernel(AttnArgs a) { attn_fwd_v6_body<8, true>(a); }
+
+// the two key halves of each split tile -> the output: O = (w0 O0 + w1 O1) / (w0 l0 + w1 l1), w = 2^(m - max(m0, m1))
+__global__ __launch_bounds__(256) void attn_split_merge_kernel(AttnArgs a) {
+  const int stile = blockIdx.x, tile = a.split_full + stile;
+  const int qb = tile % a.nqb, h = (tile / a.nqb) % a.nheads, seg = tile / (a.nqb * a.nheads);
+  const int* sg = a.segs + seg * 4;
+  const int q_row0 = sg[0], q_len = sg[1];
+  if (qb * QB >= q_len) return;
+  const float* w0 = a.work + (long)stile * 2 * QB * (D + 2);
+  const float* w1 = w0 + QB * (D + 2);
+  for (int i = threadIdx.x; i < QB * (D / 4); i += 256) {
+    const int row = i / (D / 4), d = (i % (D / 4)) * 4, qi = qb * QB + row;
+    if (qi >= q_len) continue;
+    const float m0 = w0[QB * D + row], m1 = w1[QB * D + row];
+    const float M = fmaxf(m0, m1);
+    const float a0 = m0 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m0 - M);
+    const float a1 = m1 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m1 - M);
+    const float inv = 1.0f / (a0 * w0[QB * D + QB + row] + a1 * w1[QB * D + QB + row]);
+    const f32x4 x0 = *(const f32x4*)(w0 + row * D + d), x1 = *(const f32x4*)(w1 + row * D + d);
+    const int orow = a.orows ? a.orows[q_row0 + qi] : q_row0 + qi;
+    bf16* p = a.o + (long)orow * a.os + h * D + d;
+    bf16x4 o4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o4[j] = f2bf((a0 * x0[j] + a1 * x1[j]) * inv);
+    if (a.accumulate) {
+      const bf16x4 ov = *(const bf16x4*)p;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o4[j] = f2bf(bf2f(ov[j]) + bf2f(o4[j]));
+    }
+    *(bf16x4*)p = o4;
+  }
+}
 __global__ __launch_bounds__(256, 2) void attn_fwd_v6_w4_kernel(AttnArgs a) { attn_fwd_v6_body<4>(a); }
 __global__ __launch_bounds__(512) void attn_fwd_v6t_kernel(AttnArgs a) { attn_fwd_vt_body(a); }
 
@@ -1382,6 +1473,34 @@ extern "C" int sa_attn_fwd_map(const void* q, const void* k, const void* v, void
     dim3 grid((max_q_len + QB - 1) / QB, heads, nseg);
     hipLaunchKernelGGL(attn_fwd_v6_kernel, grid, dim3(512), LDS_BYTES, (hipStream_t)stream, a);
   }
+  SA_LAUNCH_CHECK();
+  return SA_OK;
+}
+
+extern "C" int sa_attn_fwd_split(const void* q, const void* k, const void* v, void* o, const int32_t* segs, int nseg,
+                                 int max_q_len, int heads, int head_dim, int64_t q_stride, int64_t k_stride,
+                                 int64_t v_stride, int64_t o_stride, float scale, int accumulate, const int32_t* o_rows,
+                                 int split_tiles, void* work, int64_t work_bytes, void* stream) {
+  if (!q || !k || !v || !o || !segs || nseg <= 0 || max_q_len <= 0 || heads <= 0 || head_dim != D) return SA_ERR_ARG;
+  if ((q_stride | k_stride | v_stride | o_stride) % 8) return SA_ERR_ARG;
+  if ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)o)) & 15) return SA_ERR_ARG;
+  const int nqb = (max_q_len + QB - 1) / QB;
+  const long ntiles = (long)nseg * heads * nqb;
+  if (split_tiles <= 0 || split_tiles > ntiles) return SA_ERR_ARG;
+  if (!work || (((uintptr_t)work) & 15) || work_bytes < (int64_t)split_tiles * 2 * QB * (D + 2) * 4) return SA_ERR_ARG;
+  static const bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)attn_fwd_v6_split_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
+    return true;
+  }();
+  (void)attr;
+  AttnArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, segs,
+             q_stride, k_stride, v_stride, o_stride, scale * 1.4426950408889634f, accumulate, o_rows,
+             nqb, heads, (int)(ntiles - split_tiles), split_tiles, (float*)work};
+  hipLaunchKernelGGL(attn_fwd_v6_split_kernel, dim3((unsigned)(ntiles + split_tiles)), dim3(512), LDS_BYTES,
+                     (hipStream_t)stream, a);
+  SA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(attn_split_merge_kernel, dim3(split_tiles), dim3(256), 0, (hipStream_t)stream, a);
   SA_LAUNCH_CHECK();
   return SA_OK;
 }

@@ -4,6 +4,8 @@ Tensors must already live on the GPU with the dtype/layout documented per functi
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ._lib import call
@@ -116,11 +118,25 @@ ATTN_AUTO = 0
 ATTN_VT_P32 = 3
 
 
+def attn_tail_split(n_tiles_before, n_tiles, device):
+    """How many of a launch's (segment, head, 256-query block) tiles to run as two key halves (sa_attn_fwd_split):
+    the tiles past the last full round over the CUs when that round is at most half full, counting n_tiles_before
+    tiles of launches running concurrently ahead of this one (the per-CFG-row streams of the sequence-parallel
+    schedule); 0 = no split.  SA_ATTN_SPLIT=0 disables it."""
+    if os.environ.get("SA_ATTN_SPLIT", "1") == "0":
+        return 0
+    ncu = _n_cu(device)
+    total = n_tiles_before + n_tiles
+    t = total % ncu
+    return t if total > ncu and 0 < t <= ncu // 2 and t <= n_tiles else 0
+
+
 def attention(q, k, v, out, segs, nseg, max_q_len, heads, head_dim=128, scale=None, accumulate=False,
-              kernel=ATTN_AUTO, o_rows=None):
+              kernel=ATTN_AUTO, o_rows=None, split_tiles=0):
     """Flash attention over row-segment table `segs` (int32 [nseg,4] on device); kernel = per-call
     schedule selection (sa_attn_fwd_ex; 0 = auto); o_rows = int32 device map query row -> output row of
-    `out` (sa_attn_fwd_map)."""
+    `out` (sa_attn_fwd_map); split_tiles > 0: the last split_tiles tiles as two key halves + a merge
+    (sa_attn_fwd_split, 8-wave kernel)."""
     for t, n in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
         _check(t, torch.bfloat16, f"attention.{n}")
         assert t.stride(-1) == 1
@@ -129,6 +145,12 @@ def attention(q, k, v, out, segs, nseg, max_q_len, heads, head_dim=128, scale=No
         assert o_rows.dtype == torch.int32 and o_rows.is_cuda and o_rows.is_contiguous()
     if scale is None:
         scale = head_dim ** -0.5
+    if split_tiles:
+        work = torch.empty(split_tiles * 2 * 256 * (head_dim + 2), device=q.device, dtype=torch.float32)
+        call("sa_attn_fwd_split", q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), segs.data_ptr(), nseg,
+             max_q_len, heads, head_dim, q.stride(0), k.stride(0), v.stride(0), out.stride(0), float(scale),
+             int(accumulate), _p(o_rows), int(split_tiles), work.data_ptr(), work.numel() * 4, _stream())
+        return out
     call("sa_attn_fwd_map", q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), segs.data_ptr(), nseg,
          max_q_len, heads, head_dim, q.stride(0), k.stride(0), v.stride(0), out.stride(0), float(scale),
          int(accumulate), kernel, _p(o_rows), _stream())

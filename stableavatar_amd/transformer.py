@@ -615,6 +615,11 @@ class WanTransformer3DFantasyModel(nn.Module):
         kvt, kvi = ctx.kv[li]
         nv = n_fr * nper
         pend, back = [], []
+        # the rows' attention launches run concurrently: the tiles past their last full round over the CUs (in the
+        # last row's launch) run as key halves (ops.attn_tail_split), all rows on the 8-wave kernel then
+        n_row = hg * -(-Lq // 256)
+        splits = [ops.attn_tail_split(b * n_row, n_row, x.device) if self.attn_kernel == 0 else 0 for b in range(B)]
+        akern = 1 if any(splits) else self.attn_kernel
         for b, st in enumerate(rstreams):  # self-attention inputs (1B:675-676) and the Q/K/V exchange
             rs = slice(b * Lc, (b + 1) * Lc)
             with torch.cuda.stream(st):
@@ -628,7 +633,7 @@ class WanTransformer3DFantasyModel(nn.Module):
                 pend[b].wait()
                 ev0 = self._record_event()
                 ops.attention(ex.q, ex.kv[:, :hgd], ex.kv[:, hgd:], ex.obuf, segs_rows[b], 1, Lq, hg,
-                              kernel=self.attn_kernel, o_rows=ex.omap)
+                              kernel=akern, o_rows=ex.omap, split_tiles=splits[b])
                 self._record_span(ev0, rows=1, batch=B)
                 back.append(ex.tokens([b]))
         for b, st in enumerate(rstreams):  # O-projection + gated residual, cross-attention, FFN (1B:677-691)
@@ -926,8 +931,9 @@ class WanTransformer3DFantasyModel(nn.Module):
                     # Ulysses: full-sequence attention of this rank's (query part, head group), outputs written
                     # to the owners' send slabs / this rank's own O-projection panel, then heads -> tokens
                     ev0 = self._record_event()
+                    split = ops.attn_tail_split(0, B * hg * -(-Lq // 256), dev) if self.attn_kernel == 0 else 0
                     ops.attention(ex.q, ex.kv[:, :hgd], ex.kv[:, hgd:], ex.obuf, segs_self, B, Lq, hg,
-                                  kernel=self.attn_kernel, o_rows=ex.omap)
+                                  kernel=self.attn_kernel, o_rows=ex.omap, split_tiles=split)
                     self._record_span(ev0, rows=B, batch=B)
                     ex.tokens(range(B)).wait()
                     a0, pnl = ex.panels()

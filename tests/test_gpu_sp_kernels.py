@@ -4,7 +4,7 @@ SURVEY.md §8 row a18; the seam is usp_attn_forward, wan/dist/wan_xfuser.py:72-1
 * sa_qkv_pack -- the Q/K/V RMSNorm + RoPE writing per-destination slabs -- against the in-place
   sa_qk_rmsnorm_rope followed by a torch scatter: bit-identical (same arithmetic, different stores);
 * sa_attn_fwd_map -- the attention storing by output row map -- against the plain attention scattered by
-  torch: bit-identical;
+  torch: bit-identical; sa_attn_fwd_split (the last tiles as two key halves + merge) against fp32 torch;
 * sa_gemm_bf16_panels -- the O-projection reading column panels -- against the same GEMM on the
   contiguous matrix: bit-identical (same K order).
 Runs on the MI355X only."""
@@ -63,6 +63,77 @@ def test_qkv_pack_matches_inplace_norm_and_scatter(C, H, world, rank):
     assert not qv[:, plan.group].isnan().any()
     if plan.G > 1:
         assert qv[:, (plan.group + 1) % plan.G].isnan().all()
+
+
+def _ref_attn(q, k, v, scale):
+    s = (q.float() @ k.float().t()) * scale
+    return torch.softmax(s, -1) @ v.float()
+
+
+@pytest.mark.parametrize("Lk", [777, 50, 128], ids=["ragged", "one_block_empty_half", "two_blocks"])
+@pytest.mark.parametrize("split", [1, 7, 36])
+def test_attention_key_split(Lk, split):
+    """sa_attn_fwd_split: the last `split` of 36 tiles (3 segments x 3 heads x 4 query blocks) as two key halves +
+    the log-sum-exp merge, output by row map and accumulated: vs fp32 torch, and the unsplit tiles bit-identical to
+    the plain launch"""
+    B, Lq, H, D = 3, 1000, 3, 128
+    q = torch.randn(B * Lq, H * D, device=dev).bfloat16()
+    k = torch.randn(B * Lk, H * D, device=dev).bfloat16()
+    v = torch.randn(B * Lk, H * D, device=dev).bfloat16()
+    segs = torch.tensor([[b * Lq, Lq, b * Lk, Lk] for b in range(B)], dtype=torch.int32, device=dev)
+    rows = torch.randperm(2 * B * Lq, device=dev)[:B * Lq].to(torch.int32)
+    plain = torch.full((2 * B * Lq, H * D), float("nan"), device=dev, dtype=torch.bfloat16)
+    ops.attention(q, k, v, plain, segs, B, Lq, H, kernel=1, o_rows=rows)
+    o = torch.full_like(plain, float("nan"))
+    ops.attention(q, k, v, o, segs, B, Lq, H, o_rows=rows, split_tiles=split)
+    torch.cuda.synchronize()
+    got, ref_p = o[rows.long()].view(B, Lq, H, D), plain[rows.long()].view(B, Lq, H, D)
+    for b in range(B):
+        for h in range(H):
+            ref = _ref_attn(q.view(B, Lq, H, D)[b, :, h], k.view(B, Lk, H, D)[b, :, h], v.view(B, Lk, H, D)[b, :, h],
+                            D ** -0.5)
+            assert ((got[b, :, h].float() - ref).norm() / ref.norm()).item() < 1e-2, (b, h)
+    # tiles in launch order (segment, head, query block); the first 36 - split are the plain kernel's
+    nqb = 4
+    for t in range(36 - split):
+        b, h, qb = t // (H * nqb), (t // nqb) % H, t % nqb
+        sl = slice(qb * 256, min((qb + 1) * 256, Lq))
+        assert torch.equal(got[b, sl, h], ref_p[b, sl, h]), t
+    assert (o.isnan().any(1) == ~torch.isin(torch.arange(2 * B * Lq, device=dev), rows.long())).all()
+    acc = o.clone()
+    ops.attention(q, k, v, acc, segs, B, Lq, H, o_rows=rows, split_tiles=split, accumulate=True)
+    assert ((acc[rows.long()].float() - 2 * o[rows.long()].float()).norm() / o[rows.long()].float().norm()) < 1e-2
+
+
+def test_attention_key_split_sp_shape():
+    """the Ulysses N = 8 per-rank launch (3 rows x 10 752 queries x 3 heads over 21 504 keys = 378 tiles): the split
+    policy picks the tiles past the first round over the CUs, and the split launch matches the plain one"""
+    B, Lq, Lk, H, D = 3, 10752, 21504, 3, 128
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    n_tiles = B * H * (Lq // 256)
+    split = ops.attn_tail_split(0, n_tiles, q_dev := torch.device(dev))
+    if n_cu == 256:
+        assert split == 122
+        # per-row launches on concurrent streams: only the last row's launch holds the tail
+        assert [ops.attn_tail_split(b * n_tiles // 3, n_tiles // 3, q_dev) for b in range(3)] == [0, 0, 122]
+    if not split:
+        pytest.skip(f"no tail split on {n_cu} CUs")
+    q = torch.randn(B * Lq, H * D, device=dev).bfloat16()
+    k = torch.randn(B * Lk, H * D, device=dev).bfloat16()
+    v = torch.randn(B * Lk, H * D, device=dev).bfloat16()
+    segs = torch.tensor([[b * Lq, Lq, b * Lk, Lk] for b in range(B)], dtype=torch.int32, device=dev)
+    plain = torch.empty(B * Lq, H * D, device=dev, dtype=torch.bfloat16)
+    ops.attention(q, k, v, plain, segs, B, Lq, H, kernel=1)
+    o = torch.empty_like(plain)
+    ops.attention(q, k, v, o, segs, B, Lq, H, split_tiles=split)
+    torch.cuda.synchronize()
+    rel = ((o.float() - plain.float()).norm() / plain.float().norm()).item()
+    assert rel < 5e-3, rel
+    tiles_plain = n_tiles - split  # whole tiles are the plain kernel's, bit for bit
+    ov, pv = o.view(B, Lq, H, D), plain.view(B, Lq, H, D)
+    for t in (0, tiles_plain - 1):
+        b, h, qb = t // (H * 42), (t // 42) % H, t % 42
+        assert torch.equal(ov[b, qb * 256:(qb + 1) * 256, h], pv[b, qb * 256:(qb + 1) * 256, h])
 
 
 @pytest.mark.parametrize("kernel", [1, 2], ids=["wg256", "wg128"])
