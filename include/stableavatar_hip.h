@@ -149,8 +149,9 @@ int sa_qk_rmsnorm_rope(void* x, int64_t ldx, int q_col, int k_col, const float* 
  * same RMSNorm + RoPE as sa_qk_rmsnorm_rope on the [M, 3C] QKV rows of this rank's token chunk (q at
  * column 0, k at C, v at 2C), written with v into per-destination slabs instead of in place.  Head group g
  * (C/G columns) of row (CFG row b = b_offset + row / rows_per_batch, token t = row % rows_per_batch) goes
- * as q to destination my_part*G + g and as k|v to destinations r*G + g, r < R; table = device int64
- * [G*R][6] {q_ptr, q_ld, q_bstride, kv_ptr, kv_ld, kv_bstride} in elements (v at k + C/G). */
+ * as q and as k|v to the slabs of destination my_part*G + g (the exchange sends the k|v slab on to the group's
+ * rank of every query part r < R); table = device int64 [G*R][6] {q_ptr, q_ld, q_bstride, kv_ptr, kv_ld,
+ * kv_bstride} in elements (v at k + C/G), rows r*G + g with r != my_part unread. */
 int sa_qkv_pack(const void* x, int64_t ldx, const float* wq, const float* wk, int M, int C, int head_dim, float eps,
                 const float* rope, int rows_per_batch, int tok_offset, int F, int H, int W, int n_frame_pairs,
                 int n_height_pairs, const int64_t* table, int G, int R, int my_part, int b_offset, void* stream);

@@ -311,13 +311,13 @@ struct PackStore {
       const long* e = table + (long)(my_part * G + g) * 6;
       store8<bf16>((bf16*)e[0] + b * e[2] + t * e[1] + w, y);
     } else {
+      // k | v once, into this query part's entry of head group g: the exchange sends that slab to the group's rank
+      // of every query part (the K/V of a group is the same for all of them)
       const u32x4 vv = *(const u32x4*)(vrow + c0);
-      for (int r = 0; r < R; ++r) {
-        const long* e = table + (long)(r * G + g) * 6;
-        bf16* kd = (bf16*)e[3] + b * e[5] + t * e[4] + w;
-        store8<bf16>(kd, y);
-        *(u32x4*)(kd + hgd) = vv;
-      }
+      const long* e = table + (long)(my_part * G + g) * 6;
+      bf16* kd = (bf16*)e[3] + b * e[5] + t * e[4] + w;
+      store8<bf16>(kd, y);
+      *(u32x4*)(kd + hgd) = vv;
     }
   }
 };

@@ -150,8 +150,9 @@ class UlyssesExchange:
       * ``q`` [B*Lq, hg*D] (rows b*Lq + j*Lc + t: token t of chunk j of this rank's query part) and ``kv``
         [B*Lp, 2*hg*D] (rows b*Lp + r*Lc + t, k | v) are the attention inputs; this rank's own chunk is
         written into them by ``ops.qkv_pack`` (through ``table``), the other chunks arrive into them;
-      * ``sq[d]`` [B, Lc, hg*D] and ``skv[d]`` [B, Lc, 2*hg*D] are the send slabs of remote destination d,
-        also written by ``ops.qkv_pack``;
+      * ``sq[d]`` [B, Lc, hg*D] and ``skv[d]`` [B, Lc, 2*hg*D] are the send slabs of remote destination d of this
+        rank's query part, also written by ``ops.qkv_pack``; the K/V of head group j goes to the group's rank of every
+        query part from the one slab of this part (``kv_source(j)``: written once, sent R times);
       * ``obuf`` [2*G*B*Lc, hg*D]: the attention writes query chunk j's head outputs to rows (j*B + b)*Lc + t
         of the first half (the send slab of chunk j's owner) -- except this rank's own chunk, which goes to
         the second half, ``pan``, whose panel j (rows j*B*Lc ..) receives head group j of this rank's tokens
@@ -181,21 +182,19 @@ class UlyssesExchange:
         self.obuf = torch.empty(2 * G * B * Lc + _panel_slack_rows(device), hgd, device=device, dtype=dtype)
         self.pan = self.obuf[G * B * Lc:2 * G * B * Lc]
         self.remote = [d for d in range(N) if d != p.rank or self.loopback]
-        self.sq = {d: torch.empty(B, Lc, hgd, device=device, dtype=dtype) for d in self.remote if d // G == p.part}
-        self.skv = {d: torch.empty(B, Lc, 2 * hgd, device=device, dtype=dtype) for d in self.remote}
+        mine = [d for d in self.remote if d // G == p.part]  # destinations of this query part
+        self.sq = {d: torch.empty(B, Lc, hgd, device=device, dtype=dtype) for d in mine}
+        self.skv = {d: torch.empty(B, Lc, 2 * hgd, device=device, dtype=dtype) for d in mine}
         qv = self.q.view(B, self.Lq, hgd)
         kvv = self.kv.view(B, self.Lp, 2 * hgd)
-        rows = []
-        for d in range(N):
-            if d == p.rank and not self.loopback:
-                qd, kd = qv[:, g * Lc:(g + 1) * Lc], kvv[:, p.rank * Lc:(p.rank + 1) * Lc]
-            else:
-                qd, kd = self.sq.get(d), self.skv[d]
-            rows.append([0, 0, 0] if qd is None else [qd.data_ptr(), qd.stride(1), qd.stride(0)])
-            rows[-1] += [kd.data_ptr(), kd.stride(1), kd.stride(0)]
-        self.slabs = {d: (self.sq.get(d), self.skv[d]) for d in self.remote}
+        self.slabs = {d: (self.sq[d], self.skv[d]) for d in mine}
         if not self.loopback:
             self.slabs[p.rank] = (qv[:, g * Lc:(g + 1) * Lc], kvv[:, p.rank * Lc:(p.rank + 1) * Lc])
+        rows = []
+        for d in range(N):
+            qd, kd = self.slabs.get(d, (None, None))  # other query parts' rows: not read by the pack
+            rows.append(([0, 0, 0] if qd is None else [qd.data_ptr(), qd.stride(1), qd.stride(0)]) +
+                        ([0, 0, 0] if kd is None else [kd.data_ptr(), kd.stride(1), kd.stride(0)]))
         self.table = torch.tensor(rows, dtype=torch.int64).to(device)
         j = torch.arange(G).view(1, G, 1)
         b = torch.arange(B).view(B, 1, 1)
@@ -203,6 +202,12 @@ class UlyssesExchange:
         own = (j == g).to(torch.int64) * (0 if self.loopback else 1)  # own chunk straight into its panel
         omap = own * (G * B * Lc) + (j * B + b) * Lc + t  # [B, G, Lc] = q row order
         self.omap = omap.reshape(-1).to(torch.int32).to(device)
+
+    def kv_source(self, j):
+        """the k | v slab [B, Lc, 2*hg*D] of head group j that the pack wrote (this query part's destination of the
+        group), sent to the group's rank in every query part"""
+        d = self.plan.part * self.plan.G + j
+        return self.slabs[d][1]
 
     def heads(self, rows) -> Pending:
         """Q/K/V of CFG rows ``rows`` to the ranks that attend over them (after ``ops.qkv_pack``)."""
@@ -213,7 +218,7 @@ class UlyssesExchange:
             for d in self.remote:
                 if d in self.sq:
                     sends.append((self.sq[d][b], d))
-                sends.append((self.skv[d][b], d))
+                sends.append((self.kv_source(d % G)[b], d))
             for r in self.remote:
                 if r // G == p.part:
                     q0 = b * Lq + (r % G) * Lc
