@@ -354,7 +354,11 @@ def make_inputs(dev, frames, size, seed, video_frames=None):
     g = torch.Generator().manual_seed(seed)
     latents = torch.randn(1, 16, T, h, h, generator=g).to(dev).bfloat16()  # CPU noise, injected (App. A.13)
     gd = torch.Generator(device=dev).manual_seed(seed + 1)
-    y = torch.randn(3, 20, fpb, h, h, device=dev, generator=gd).bfloat16()
+    # conditioning as the pipeline builds it (wan_inference_long_pipeline.py:693-700): the first-frame mask + the VAE
+    # latents of the reference frame and zeros (synthetic here), tripled for the CFG rows
+    from stableavatar_amd.pipeline import WanI2VTalkingInferenceLongPipeline
+    ref_lat = torch.randn(1, 16, fpb, h, h, device=dev, generator=gd)
+    y = WanI2VTalkingInferenceLongPipeline.mask_latents(ref_lat, frames).bfloat16()
     ctx = [torch.randn(n, 4096, device=dev, generator=gd) for n in (126, 126, 48)]
     ctx[1] = ctx[0]
     clip = torch.randn(1, 257, 1280, device=dev, generator=gd).expand(3, -1, -1).contiguous()

@@ -15,6 +15,7 @@ Fixes the reference's infinite loop when the clip is exactly one window (SURVEY.
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -206,6 +207,11 @@ class WanI2VTalkingInferenceLongPipeline:
         lat = latents.to(torch.bfloat16, copy=True).contiguous()
         pred = torch.empty_like(lat)
         yb = y.to(device=dev, dtype=torch.bfloat16).contiguous()
+        # the CFG rows' DiT inputs are equal when y's rows are (mask_latents triples one row, :693-700; the latents
+        # are tripled at :730 and t expanded at :733): the DiT then runs its first block's self-attention half once
+        # (forward_window shared_rows); checked once per call.  SA_CFG_SHARED=0 computes every row (A/B)
+        self._shared_rows = (cfg and os.environ.get("SA_CFG_SHARED", "1") != "0"
+                             and bool((yb[1:] == yb[:1]).all()))
         sig = [float(s) for s in sigmas]
         if self.window_group is not None:
             return self._denoise_window_parallel(lat, pred, yb, context, clip_context, window_features, timesteps,
@@ -218,7 +224,7 @@ class WanI2VTalkingInferenceLongPipeline:
                 Fw = e - s
                 noise = self.transformer.forward_window(lat, s, True, 3 if cfg else 1, tt, context, seq_len,
                                                         clip_context, yb[:, :, :Fw], window_features[(s, e)],
-                                                        clip_length)
+                                                        clip_length, shared_rows=self._shared_rows)
                 blend = s != 0 and i != 0
                 ops.flow_step(lat, pred, noise, s, sig[i + 1] - sig[i], audio_guide_scale or 0.0,
                               text_guide_scale or 0.0, overlap if blend else 0, pe, wts if blend else None, blend)
@@ -256,7 +262,7 @@ class WanI2VTalkingInferenceLongPipeline:
                     s, e, _ = wins[k]
                     self.transformer.forward_window(lat, s, True, R, tt, context, seq_len, clip_context,
                                                     yb[:, :, :e - s], window_features[(s, e)], clip_length,
-                                                    out=view(k))
+                                                    out=view(k), shared_rows=self._shared_rows)
                 pend.append(sp.all_gather_slots(slots[j * N:(j + 1) * N], r, grp))
             for p_ in pend:
                 p_.wait()

@@ -667,6 +667,32 @@ class WanTransformer3DFantasyModel(nn.Module):
 
     # ------------------------------------------------------------------ timing hooks (bench.py)
 
+    def _self_attention_rows(self, pk, L, x, ws, em, nb, Lc, Lp, use_vt, rope_kw, dev, batch, normed=False):
+        """The self-attention half of a block (1B:675-679) on the first nb CFG rows of the single-GPU layout: LN +
+        modulate (unless `normed`), q|k (+ v as V^T for kernel 3, or q|k|v rows), RMSNorm + RoPE, attention,
+        O-projection + gated residual into x"""
+        dim, H_ = self.dim, self.num_heads
+        r = slice(0, nb * Lc)
+        xr, mod, qkv, att = x[r], ws.mod[r], ws.qkv[r], ws.att[r]
+        if not normed:
+            ops.layernorm_mod(xr, mod, self.eps, shift=em[:nb, 0], scale=em[:nb, 1], rows_per_batch=Lc)
+        segs = self._segs.get(("self", nb, Lp), [[b * Lp, Lp, b * Lp, Lp] for b in range(nb)], dev)
+        if use_vt:
+            # q|k into the QKV rows, v straight into V^T (keys in P's order per 32) for attention kernel 3
+            ops.linear(mod, L.w_qk, L.b_qk, ops.EPI_BF16, out=qkv[:, :2 * dim])
+            ops.linear(mod, L.w_v, L.b_v, ops.EPI_BF16_TP32, out=ws.vt)
+            ops.qk_rmsnorm_rope(qkv, 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
+            ev0 = self._record_event()
+            ops.attention(qkv[:, :dim], qkv[:, dim:2 * dim], ws.vt, att, segs, nb, Lp, H_, kernel=ops.ATTN_VT_P32)
+        else:
+            ops.linear(mod, L.w_qkv, L.b_qkv, ops.EPI_BF16, out=qkv)
+            ops.qk_rmsnorm_rope(qkv, 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
+            ev0 = self._record_event()
+            ops.attention(qkv[:, :dim], qkv[:, dim:2 * dim], qkv[:, 2 * dim:], att, segs, nb, Lp, H_,
+                          kernel=self.attn_kernel)
+        self._record_span(ev0, rows=nb, batch=batch)
+        ops.linear(att, L.w_o, L.b_o, ops.EPI_RES_F32, out=xr, residual=xr, gate=em[:nb, 2], rows_per_batch=Lc)
+
     def _record_event(self):
         """HIP event on the current stream (the one the attention kernel is launched on), or None."""
         if self._events is None:
@@ -698,9 +724,14 @@ class WanTransformer3DFantasyModel(nn.Module):
                                    video_sample_n_frames, is_clip_level_modeling, cond_flag=cond_flag)
 
     def forward_window(self, lat, frame_offset, broadcast, B, t, context, seq_len, clip_fea, y, vocal_embeddings,
-                       video_sample_n_frames=81, is_clip_level_modeling=False, out=None, cond_flag=True):
+                       video_sample_n_frames=81, is_clip_level_modeling=False, out=None, cond_flag=True,
+                       shared_rows=False):
         """Forward on frames [frame_offset, frame_offset + Fw) of `lat` ([B|1, C, T, H, W]); with
-        broadcast=True one latent row feeds all B CFG rows (the pipeline's torch.cat([latents]*3))."""
+        broadcast=True one latent row feeds all B CFG rows (the pipeline's torch.cat([latents]*3)).
+        shared_rows=True (with broadcast): the caller guarantees the B rows of y are equal too, as the pipeline's
+        CFG batch has them (y tripled at wan_inference_long_pipeline.py:693-700, x at :730, t expanded at :733) --
+        then every row's input to the first block's self-attention half (patch embedding, time modulation) is the
+        same, and that half (1B:675-679) runs for one row and is copied to the others: bit-identical output."""
         if is_clip_level_modeling:
             raise NotImplementedError("clip-level audio modeling is a training mode (1B:1011-1015)")
         if self.model_type == "i2v":
@@ -853,6 +884,7 @@ class WanTransformer3DFantasyModel(nn.Module):
                           and os.environ.get("SA_CROSS3", "1") != "0")
             x = ws.x
             use_vt = not SP and self._vt_attention(Lp, dev)
+            dedup = shared_rows and broadcast and B > 1 and not SP
             if use_vt and ws.vt is None:
                 # zero-filled once: the pad columns past B * Lp are read (as P = 0 keys) by a partial last block, which
                 # stages a whole 64-key block: up to (B-1)*Lp + ceil64(Lp) <= ceil64(M) + 64 columns
@@ -883,11 +915,18 @@ class WanTransformer3DFantasyModel(nn.Module):
                                         segs_rows, row_segs, ctx, kvv, nper, G, n_fr, use_cross3, rstreams)
                     continue
                 em = emod[li]  # [B, 6, dim]
-                # self-attention (1B:675-679)
-                ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 0], scale=em[:, 1], rows_per_batch=Lc)
                 rope_kw = dict(rope=pk.rope, rows_per_batch=Lc, tok_offset=rank * Lc, grid=grid, head_dim=self.d,
                                n_frame_pairs=self.d // 2 - 2 * (self.d // 6), n_height_pairs=self.d // 6)
-                if SP and sp_rows:
+                first_shared = li == 0 and dedup
+                if not first_shared:  # self-attention (1B:675-679)
+                    ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 0], scale=em[:, 1], rows_per_batch=Lc)
+                if first_shared:
+                    # the CFG rows enter the first block identical (shared_rows): its self-attention half for
+                    # row 0 only, then the residual stream copied to the other rows
+                    self._self_attention_rows(pk, L, x, ws, em, 1, Lc, Lp, use_vt, rope_kw, dev, batch=B)
+                    for b in range(1, B):
+                        x[b * Lc:(b + 1) * Lc].copy_(x[:Lc])
+                elif SP and sp_rows:
                     # Ulysses pipelined over the CFG rows: row b's Q/K/V exchange is issued right after its
                     # QKV GEMM + pack (so it travels under rows b+1..'s GEMMs), row b's attention waits
                     # only on it, and row b's output exchange travels under the next rows' attention and
@@ -939,26 +978,9 @@ class WanTransformer3DFantasyModel(nn.Module):
                     a0, pnl = ex.panels()
                     ops.linear(a0, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2],
                                rows_per_batch=Lc, a_panels=pnl)
-                elif use_vt:
-                    # q|k into the QKV rows, v straight into V^T (keys in P's order per 32) for attention kernel 3
-                    ops.linear(ws.mod, L.w_qk, L.b_qk, ops.EPI_BF16, out=ws.qkv[:, :2 * dim])
-                    ops.linear(ws.mod, L.w_v, L.b_v, ops.EPI_BF16_TP32, out=ws.vt)
-                    ops.qk_rmsnorm_rope(ws.qkv, 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
-                    ev0 = self._record_event()
-                    ops.attention(ws.qkv[:, :dim], ws.qkv[:, dim:2 * dim], ws.vt, ws.att, segs_self, B, Lp, H_,
-                                  kernel=ops.ATTN_VT_P32)
-                    self._record_span(ev0, rows=B, batch=B)
-                    ops.linear(ws.att, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2],
-                               rows_per_batch=Lc)
                 else:
-                    ops.linear(ws.mod, L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv)
-                    ops.qk_rmsnorm_rope(ws.qkv, 0, dim, L.nq, L.nk, dim, self.eps, **rope_kw)
-                    ev0 = self._record_event()
-                    ops.attention(ws.qkv[:, :dim], ws.qkv[:, dim:2 * dim], ws.qkv[:, 2 * dim:], ws.att, segs_self, B,
-                                  Lp, H_, kernel=self.attn_kernel)
-                    self._record_span(ev0, rows=B, batch=B)
-                    ops.linear(ws.att, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2],
-                               rows_per_batch=Lc)
+                    self._self_attention_rows(pk, L, x, ws, em, B, Lc, Lp, use_vt, rope_kw, dev, batch=B,
+                                              normed=True)
                 # cross-attention: text + image + per-frame vocal (1B:534-605, 684)
                 ops.layernorm_mod(x, ws.mod, self.eps, weight=L.n3w, bias=L.n3b)
                 qc = ws.qkv[:, :dim]
@@ -1009,11 +1031,13 @@ class WanTransformer3DFantasy14BModel(WanTransformer3DFantasyModel):
     VOCAL = "14B"
 
     def forward_window(self, lat, frame_offset, broadcast, B, t, context, seq_len, clip_fea, y, vocal_embeddings,
-                       video_sample_n_frames=81, is_clip_level_modeling=False, out=None, cond_flag=True):
+                       video_sample_n_frames=81, is_clip_level_modeling=False, out=None, cond_flag=True,
+                       shared_rows=False):
         if video_sample_n_frames != 81:
             raise ValueError("the 14B vocal path is built for 81-frame windows (21 latent frames, 14B:1008-1010)")
         return super().forward_window(lat, frame_offset, broadcast, B, t, context, seq_len, clip_fea, y,
-                                      vocal_embeddings, 81, is_clip_level_modeling, out=out, cond_flag=cond_flag)
+                                      vocal_embeddings, 81, is_clip_level_modeling, out=out, cond_flag=cond_flag,
+                                      shared_rows=shared_rows)
 
 
 def call_gemm_batched(cols, w, bias, xout, B, real, Lp, dim, kpad):

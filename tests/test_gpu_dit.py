@@ -121,3 +121,31 @@ def test_dit_riflex_vs_reference_golden():
     assert rel(out, ref) < 2e-2 and cos(out, ref) > 0.9995, (rel(out, ref), cos(out, ref))
     m.disable_riflex()
     assert torch.equal(run(m, inp), base)
+
+
+@pytest.mark.parametrize("wh", [(8, 8), (32, 32)], ids=["v_rows_80tok", "vt_1280tok"])
+def test_dit_shared_cfg_rows_first_block_once(wh):
+    """forward_window(shared_rows=True): the CFG rows' inputs are equal (the pipeline's tripled latents, y and t,
+    wan_inference_long_pipeline.py:693-700,730,733), so the first block's self-attention half runs for one row and
+    is copied -- the output equals the full computation bit for bit (V rows at 80 tokens, the V^T kernel at 1 280)"""
+    from stableavatar_amd import synthetic
+    from stableavatar_amd.pipeline import WanI2VTalkingInferenceLongPipeline
+    m = make_model(DIT_SMALL)
+    H, W = wh
+    dev = "cuda"
+    lat = synthetic.seeded_normal((1, 16, 5, H, W), 301).to(dev).bfloat16()
+    y = WanI2VTalkingInferenceLongPipeline.mask_latents(synthetic.seeded_normal((1, 16, 5, H, W), 302).to(dev),
+                                                        17).bfloat16()
+    ctx = [synthetic.seeded_normal((20, 64), 303).to(dev)] * 2 + [synthetic.seeded_normal((25, 64), 304).to(dev)]
+    clip = synthetic.seeded_normal((1, 257, 1280), 305).expand(3, -1, -1).contiguous().to(dev)
+    a = synthetic.seeded_normal((1, 39, 768), 306).to(dev)
+    voc = torch.cat([torch.zeros_like(a), a, a])
+    t = torch.tensor([937.5], device=dev)
+    S = 5 * (H // 2) * (W // 2)
+    outs = []
+    with torch.no_grad():
+        for shared in (False, True):
+            outs.append(m.forward_window(lat, 0, True, 3, t, ctx, S, clip, y, voc, 17, shared_rows=shared).clone())
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1])
