@@ -24,7 +24,7 @@ m.load_state_dict(synthetic.fill_state_dict(param_shapes(cfg), 0, backend="torch
 m = m.to(dev)
 g = torch.Generator(device=dev).manual_seed(0)
 lat = torch.randn(1, 16, 21, 64, 64, device=dev, generator=g).bfloat16()
-y = torch.randn(3, 20, 21, 64, 64, device=dev, generator=g).bfloat16()
+y = torch.randn(1, 20, 21, 64, 64, device=dev, generator=g).bfloat16().expand(3, -1, -1, -1, -1).contiguous()
 ctx = [torch.randn(n, 4096, device=dev, generator=g) for n in (120, 120, 60)]
 clip = torch.randn(3, 257, 1280, device=dev, generator=g)
 voc = torch.randn(3, 167, 768, device=dev, generator=g)
@@ -41,8 +41,11 @@ def fake_gather(local, B, Lc, world, group=None):
 sp.gather_tokens = fake_gather
 
 
+shared = os.environ.get("SA_SPRC_SHARED", "1") != "0"  # the pipeline's CFG rows: equal inputs (shared_rows)
+
+
 def fwd():
-    return m.forward_window(lat, 0, True, 3, t, ctx, 21504, clip, y, voc, 81)
+    return m.forward_window(lat, 0, True, 3, t, ctx, 21504, clip, y, voc, 81, shared_rows=shared)
 
 
 res = []

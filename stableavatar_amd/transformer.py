@@ -599,14 +599,15 @@ class WanTransformer3DFantasyModel(nn.Module):
         return out
 
     def _sp_layer_rows(self, pk, L, li, x, ws, em, ex, pack_kw, rank, Lc, Lq, hg, hgd, grid, segs_rows, row_segs,
-                       ctx, kvv, nper, Gf, n_fr, use_cross3, rstreams):
+                       ctx, kvv, nper, Gf, n_fr, use_cross3, rstreams, sa=True):
         """One DiT block (1B:650-695) with Ulysses sequence parallelism, each CFG row on its own stream
         (SA_SP_OVERLAP=4): row b's Q/K/V exchange (wan_xfuser.py:102-107) travels while the other rows compute
         (their QKV GEMMs, attention, O-projection, cross-attention and FFN), and its head-output exchange travels
         under the other rows' attention and FFN.  The host issues the phases of the three rows interleaved
         (QKV+pack+send for every row, then attention+send back for every row, then the rest of the block), so the
         transport sees the same order of transfers on every rank.  Per-row kernels are the batched ones applied to
-        row slices: the output is bit-identical to the batched schedule."""
+        row slices: the output is bit-identical to the batched schedule.  sa=False: the self-attention half already
+        ran (_sp_self_attention_row0), the block starts at its cross-attention."""
         dim, H_, eps = self.dim, self.num_heads, self.eps
         B = len(rstreams)
         rope_kw = dict(rope=pk.rope, rows_per_batch=Lc, tok_offset=rank * Lc, grid=grid, head_dim=self.d,
@@ -620,7 +621,7 @@ class WanTransformer3DFantasyModel(nn.Module):
         n_row = hg * -(-Lq // 256)
         splits = [ops.attn_tail_split(b * n_row, n_row, x.device) if self.attn_kernel == 0 else 0 for b in range(B)]
         akern = 1 if any(splits) else self.attn_kernel
-        for b, st in enumerate(rstreams):  # self-attention inputs (1B:675-676) and the Q/K/V exchange
+        for b, st in enumerate(rstreams if sa else []):  # self-attention inputs (1B:675-676) and the Q/K/V exchange
             rs = slice(b * Lc, (b + 1) * Lc)
             with torch.cuda.stream(st):
                 ops.layernorm_mod(x[rs], ws.mod[rs], eps, shift=em[b:b + 1, 0], scale=em[b:b + 1, 1],
@@ -628,7 +629,7 @@ class WanTransformer3DFantasyModel(nn.Module):
                 ops.linear(ws.mod[rs], L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv[rs])
                 ops.qkv_pack(ws.qkv[rs], L.nq, L.nk, dim, eps, b_offset=b, **pack_kw, **rope_kw)
                 pend.append(ex.heads([b]))
-        for b, st in enumerate(rstreams):  # attention over the full key sequence, head outputs back to the owners
+        for b, st in enumerate(rstreams if sa else []):  # attention over every key, head outputs back to the owners
             with torch.cuda.stream(st):
                 pend[b].wait()
                 ev0 = self._record_event()
@@ -640,10 +641,11 @@ class WanTransformer3DFantasyModel(nn.Module):
             rs = slice(b * Lc, (b + 1) * Lc)
             xr, mod, att = x[rs], ws.mod[rs], ws.att[rs]
             with torch.cuda.stream(st):
-                back[b].wait()
-                a0, pnl = ex.panels(range(b, b + 1))
-                ops.linear(a0, L.w_o, L.b_o, ops.EPI_RES_F32, out=xr, residual=xr, gate=em[b:b + 1, 2],
-                           rows_per_batch=Lc, a_panels=pnl)
+                if sa:
+                    back[b].wait()
+                    a0, pnl = ex.panels(range(b, b + 1))
+                    ops.linear(a0, L.w_o, L.b_o, ops.EPI_RES_F32, out=xr, residual=xr, gate=em[b:b + 1, 2],
+                               rows_per_batch=Lc, a_panels=pnl)
                 ops.layernorm_mod(xr, mod, eps, weight=L.n3w, bias=L.n3b)
                 qc = ws.qkv[rs, :dim]
                 ops.linear(mod, L.w_cq, L.b_cq, ops.EPI_BF16, out=qc)
@@ -666,6 +668,27 @@ class WanTransformer3DFantasyModel(nn.Module):
                            rows_per_batch=Lc)
 
     # ------------------------------------------------------------------ timing hooks (bench.py)
+
+    def _sp_self_attention_row0(self, L, x, ws, em, ex, pack_kw, rope_kw, Lc, Lq, hg, hgd, seg0, B):
+        """The first block's self-attention half (1B:675-679) for CFG row 0 through the Ulysses exchange (its Q/K/V
+        and head outputs only), on the current stream, the residual stream then copied to rows 1..B-1: the CFG rows
+        enter the block identical (forward_window shared_rows), and every rank takes this path together"""
+        dim, eps = self.dim, self.eps
+        rs = slice(0, Lc)
+        ops.layernorm_mod(x[rs], ws.mod[rs], eps, shift=em[0:1, 0], scale=em[0:1, 1], rows_per_batch=Lc)
+        ops.linear(ws.mod[rs], L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv[rs])
+        ops.qkv_pack(ws.qkv[rs], L.nq, L.nk, dim, eps, b_offset=0, **pack_kw, **rope_kw)
+        ex.heads([0]).wait()
+        ev0 = self._record_event()
+        ops.attention(ex.q, ex.kv[:, :hgd], ex.kv[:, hgd:], ex.obuf, seg0, 1, Lq, hg, kernel=self.attn_kernel,
+                      o_rows=ex.omap)
+        self._record_span(ev0, rows=1, batch=B)
+        ex.tokens([0]).wait()
+        a0, pnl = ex.panels(range(0, 1))
+        ops.linear(a0, L.w_o, L.b_o, ops.EPI_RES_F32, out=x[rs], residual=x[rs], gate=em[0:1, 2], rows_per_batch=Lc,
+                   a_panels=pnl)
+        for b in range(1, B):
+            x[b * Lc:(b + 1) * Lc].copy_(x[rs])
 
     def _self_attention_rows(self, pk, L, x, ws, em, nb, Lc, Lp, use_vt, rope_kw, dev, batch, normed=False):
         """The self-attention half of a block (1B:675-679) on the first nb CFG rows of the single-GPU layout: LN +
@@ -884,7 +907,9 @@ class WanTransformer3DFantasyModel(nn.Module):
                           and os.environ.get("SA_CROSS3", "1") != "0")
             x = ws.x
             use_vt = not SP and self._vt_attention(Lp, dev)
-            dedup = shared_rows and broadcast and B > 1 and not SP
+            # shared_rows: the first block's self-attention half once (single-GPU layout, or the one-stream and
+            # per-row-stream Ulysses schedules)
+            dedup = shared_rows and broadcast and B > 1 and (not SP or sp_streams or not (sp_rows or sp_rows_x))
             if use_vt and ws.vt is None:
                 # zero-filled once: the pad columns past B * Lp are read (as P = 0 keys) by a partial last block, which
                 # stages a whole 64-key block: up to (B-1)*Lp + ceil64(Lp) <= ceil64(M) + 64 columns
@@ -910,77 +935,85 @@ class WanTransformer3DFantasyModel(nn.Module):
                 row_segs = self._row_cross_segs(B, Lc, ctx, voc_list, dev)
             for li, L in enumerate(pk.layers):
                 kvv = kvv_all[:, 2 * dim * li:2 * dim * (li + 1)]
-                if sp_streams:
-                    self._sp_layer_rows(pk, L, li, x, ws, emod[li], ex, pack_kw, rank, Lc, Lq, hg, hgd, grid,
-                                        segs_rows, row_segs, ctx, kvv, nper, G, n_fr, use_cross3, rstreams)
-                    continue
                 em = emod[li]  # [B, 6, dim]
                 rope_kw = dict(rope=pk.rope, rows_per_batch=Lc, tok_offset=rank * Lc, grid=grid, head_dim=self.d,
                                n_frame_pairs=self.d // 2 - 2 * (self.d // 6), n_height_pairs=self.d // 6)
                 first_shared = li == 0 and dedup
-                if not first_shared:  # self-attention (1B:675-679)
-                    ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 0], scale=em[:, 1], rows_per_batch=Lc)
                 if first_shared:
                     # the CFG rows enter the first block identical (shared_rows): its self-attention half for
                     # row 0 only, then the residual stream copied to the other rows
-                    self._self_attention_rows(pk, L, x, ws, em, 1, Lc, Lp, use_vt, rope_kw, dev, batch=B)
-                    for b in range(1, B):
-                        x[b * Lc:(b + 1) * Lc].copy_(x[:Lc])
-                elif SP and sp_rows:
-                    # Ulysses pipelined over the CFG rows: row b's Q/K/V exchange is issued right after its
-                    # QKV GEMM + pack (so it travels under rows b+1..'s GEMMs), row b's attention waits
-                    # only on it, and row b's output exchange travels under the next rows' attention and
-                    # the earlier rows' O-projections
-                    pend = []
-                    for b in range(B):
-                        rs = slice(b * Lc, (b + 1) * Lc)
-                        ops.linear(ws.mod[rs], L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv[rs])
-                        ops.qkv_pack(ws.qkv[rs], L.nq, L.nk, dim, self.eps, b_offset=b, **pack_kw, **rope_kw)
-                        pend.append(ex.heads([b]))
-                    back = []
-                    for b in range(B):
-                        pend[b].wait()
-                        ev0 = self._record_event()
-                        ops.attention(ex.q, ex.kv[:, :hgd], ex.kv[:, hgd:], ex.obuf, segs_rows[b], 1, Lq, hg,
-                                      kernel=self.attn_kernel, o_rows=ex.omap)
-                        self._record_span(ev0, rows=1, batch=B)
-                        back.append(ex.tokens([b]))
-                    for b in range(B):
-                        rs = slice(b * Lc, (b + 1) * Lc)
-                        back[b].wait()
-                        a0, pnl = ex.panels(range(b, b + 1))
-                        ops.linear(a0, L.w_o, L.b_o, ops.EPI_RES_F32, out=x[rs], residual=x[rs],
-                                   gate=em[b:b + 1, 2], rows_per_batch=Lc, a_panels=pnl)
-                elif SP:
-                    if sp_rows_x:
-                        # per-row Q/K/V exchanges issued as each row's QKV GEMM + pack lands (they travel
-                        # under the later rows' GEMMs), one batched attention once all have arrived
+                    if SP:
+                        seg0 = self._segs.get(("self_sp_row", 0, Lp, Lq, S), [[0, Lq, 0, S]], dev)
+                        self._sp_self_attention_row0(L, x, ws, em, ex, pack_kw, rope_kw, Lc, Lq, hg, hgd, seg0, B)
+                        if sp_streams:
+                            for rs_ in rstreams:
+                                rs_.wait_stream(main)
+                    else:
+                        self._self_attention_rows(pk, L, x, ws, em, 1, Lc, Lp, use_vt, rope_kw, dev, batch=B)
+                        for b in range(1, B):
+                            x[b * Lc:(b + 1) * Lc].copy_(x[:Lc])
+                if sp_streams:
+                    self._sp_layer_rows(pk, L, li, x, ws, em, ex, pack_kw, rank, Lc, Lq, hg, hgd, grid,
+                                        segs_rows, row_segs, ctx, kvv, nper, G, n_fr, use_cross3, rstreams,
+                                        sa=not first_shared)
+                    continue
+                if not first_shared:  # self-attention (1B:675-679)
+                    ops.layernorm_mod(x, ws.mod, self.eps, shift=em[:, 0], scale=em[:, 1], rows_per_batch=Lc)
+                    if SP and sp_rows:
+                        # Ulysses pipelined over the CFG rows: row b's Q/K/V exchange is issued right after its
+                        # QKV GEMM + pack (so it travels under rows b+1..'s GEMMs), row b's attention waits
+                        # only on it, and row b's output exchange travels under the next rows' attention and
+                        # the earlier rows' O-projections
                         pend = []
                         for b in range(B):
                             rs = slice(b * Lc, (b + 1) * Lc)
                             ops.linear(ws.mod[rs], L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv[rs])
                             ops.qkv_pack(ws.qkv[rs], L.nq, L.nk, dim, self.eps, b_offset=b, **pack_kw, **rope_kw)
                             pend.append(ex.heads([b]))
-                        for p_ in pend:
-                            p_.wait()
-                    else:  # one exchange per direction for all rows
-                        ops.linear(ws.mod, L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv)
-                        ops.qkv_pack(ws.qkv, L.nq, L.nk, dim, self.eps, **pack_kw, **rope_kw)
-                        ex.heads(range(B)).wait()
-                    # Ulysses: full-sequence attention of this rank's (query part, head group), outputs written
-                    # to the owners' send slabs / this rank's own O-projection panel, then heads -> tokens
-                    ev0 = self._record_event()
-                    split = ops.attn_tail_split(0, B * hg * -(-Lq // 256), dev) if self.attn_kernel == 0 else 0
-                    ops.attention(ex.q, ex.kv[:, :hgd], ex.kv[:, hgd:], ex.obuf, segs_self, B, Lq, hg,
-                                  kernel=self.attn_kernel, o_rows=ex.omap, split_tiles=split)
-                    self._record_span(ev0, rows=B, batch=B)
-                    ex.tokens(range(B)).wait()
-                    a0, pnl = ex.panels()
-                    ops.linear(a0, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2],
-                               rows_per_batch=Lc, a_panels=pnl)
-                else:
-                    self._self_attention_rows(pk, L, x, ws, em, B, Lc, Lp, use_vt, rope_kw, dev, batch=B,
-                                              normed=True)
+                        back = []
+                        for b in range(B):
+                            pend[b].wait()
+                            ev0 = self._record_event()
+                            ops.attention(ex.q, ex.kv[:, :hgd], ex.kv[:, hgd:], ex.obuf, segs_rows[b], 1, Lq, hg,
+                                          kernel=self.attn_kernel, o_rows=ex.omap)
+                            self._record_span(ev0, rows=1, batch=B)
+                            back.append(ex.tokens([b]))
+                        for b in range(B):
+                            rs = slice(b * Lc, (b + 1) * Lc)
+                            back[b].wait()
+                            a0, pnl = ex.panels(range(b, b + 1))
+                            ops.linear(a0, L.w_o, L.b_o, ops.EPI_RES_F32, out=x[rs], residual=x[rs],
+                                       gate=em[b:b + 1, 2], rows_per_batch=Lc, a_panels=pnl)
+                    elif SP:
+                        if sp_rows_x:
+                            # per-row Q/K/V exchanges issued as each row's QKV GEMM + pack lands (they travel
+                            # under the later rows' GEMMs), one batched attention once all have arrived
+                            pend = []
+                            for b in range(B):
+                                rs = slice(b * Lc, (b + 1) * Lc)
+                                ops.linear(ws.mod[rs], L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv[rs])
+                                ops.qkv_pack(ws.qkv[rs], L.nq, L.nk, dim, self.eps, b_offset=b, **pack_kw, **rope_kw)
+                                pend.append(ex.heads([b]))
+                            for p_ in pend:
+                                p_.wait()
+                        else:  # one exchange per direction for all rows
+                            ops.linear(ws.mod, L.w_qkv, L.b_qkv, ops.EPI_BF16, out=ws.qkv)
+                            ops.qkv_pack(ws.qkv, L.nq, L.nk, dim, self.eps, **pack_kw, **rope_kw)
+                            ex.heads(range(B)).wait()
+                        # Ulysses: full-sequence attention of this rank's (query part, head group), outputs written
+                        # to the owners' send slabs / this rank's own O-projection panel, then heads -> tokens
+                        ev0 = self._record_event()
+                        split = ops.attn_tail_split(0, B * hg * -(-Lq // 256), dev) if self.attn_kernel == 0 else 0
+                        ops.attention(ex.q, ex.kv[:, :hgd], ex.kv[:, hgd:], ex.obuf, segs_self, B, Lq, hg,
+                                      kernel=self.attn_kernel, o_rows=ex.omap, split_tiles=split)
+                        self._record_span(ev0, rows=B, batch=B)
+                        ex.tokens(range(B)).wait()
+                        a0, pnl = ex.panels()
+                        ops.linear(a0, L.w_o, L.b_o, ops.EPI_RES_F32, out=x, residual=x, gate=em[:, 2],
+                                   rows_per_batch=Lc, a_panels=pnl)
+                    else:
+                        self._self_attention_rows(pk, L, x, ws, em, B, Lc, Lp, use_vt, rope_kw, dev, batch=B,
+                                                  normed=True)
                 # cross-attention: text + image + per-frame vocal (1B:534-605, 684)
                 ops.layernorm_mod(x, ws.mod, self.eps, weight=L.n3w, bias=L.n3b)
                 qc = ws.qkv[:, :dim]

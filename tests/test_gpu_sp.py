@@ -109,6 +109,62 @@ def test_sp_matches_reference_golden(world, model):
             assert e_single < 1e-3, (rank, name, ov, e_single)
 
 
+def _shared_rows_worker(rank, world, port, qret):
+    """forward_window(shared_rows=True) on the Ulysses path: the first block's self-attention half for CFG row 0
+    through the exchange, copied to the other rows -- equal to computing every row, in every schedule"""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    import torch.distributed as dist
+    sys.path.insert(0, HERE)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
+    try:
+        from test_gpu_dit import make_model
+        from golden_cases import DIT_SMALL
+        from stableavatar_amd import synthetic
+        from stableavatar_amd.pipeline import WanI2VTalkingInferenceLongPipeline
+        m = make_model(DIT_SMALL)
+        dev = "cuda"
+        lat = synthetic.seeded_normal((1, 16, 5, 8, 8), 401).to(dev).bfloat16()
+        y = WanI2VTalkingInferenceLongPipeline.mask_latents(synthetic.seeded_normal((1, 16, 5, 8, 8), 402).to(dev),
+                                                            17).bfloat16()
+        ctx = [synthetic.seeded_normal((20, 64), 403).to(dev)] * 2 + [synthetic.seeded_normal((25, 64), 404).to(dev)]
+        clip = synthetic.seeded_normal((1, 257, 1280), 405).expand(3, -1, -1).contiguous().to(dev)
+        a = synthetic.seeded_normal((1, 39, 768), 406).to(dev)
+        voc = torch.cat([torch.zeros_like(a), a, a])
+        t = torch.tensor([937.5], device=dev)
+        m.enable_multi_gpus_inference()
+        res = []
+        for ov in ("0", "2", "3", "4"):
+            os.environ["SA_SP_OVERLAP"] = ov
+            outs = []
+            with torch.no_grad():
+                for shared in (False, True):
+                    outs.append(m.forward_window(lat, 0, True, 3, t, ctx, 80, clip, y, voc, 17,
+                                                 shared_rows=shared).float().cpu())
+            res.append((ov, torch.equal(outs[0], outs[1]), bool(torch.isfinite(outs[0]).all())))
+        qret.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("world", [2, 4])
+def test_sp_shared_cfg_rows_first_block_once(world):
+    ctx = mp.get_context("spawn")
+    qret = ctx.Queue()
+    port = _rendezvous_file()
+    procs = [ctx.Process(target=_shared_rows_worker, args=(r, world, port, qret)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = collect(procs, qret, world, timeout=360)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, rows in res:
+        for ov, same, finite in rows:
+            print(f"world {world} rank {rank} overlap {ov}: shared first block bit-identical {same}")
+            assert finite and same, (rank, ov)
+
+
 def _rccl_worker(port, overlap, qret):
     """RCCL (backend "nccl") process group of ONE rank with the SP path forced on, in loopback mode
     (UlyssesExchange(loopback=True)): this rank's own token chunk goes through the point-to-point transport to
