@@ -330,3 +330,66 @@ def test_rccl_window_dp_and_vae_loopback_degree1():
     print(res)
     assert res["window_dp"][0], res
     assert res["vae_loopback"][0] and res["vae_loopback"][2] == 3, res
+
+
+def _split_rank_worker(qret):
+    """one Ulysses rank of N = 8 at the config-2 shape (3 rows x 2 688 tokens, 2 full-width blocks) with the transfers
+    stubbed out (the exchange buffers hold the same seeded values in both runs): the self-attention launches with
+    their tail split into key halves (the default: ops.attn_tail_split, schedule 4 splits the last row's launch and runs
+    every row on the 8-wave kernel; schedule 0 splits the batched launch) against SA_ATTN_SPLIT=0"""
+    import torch
+    from golden_cases import DIT_FULL
+    from stableavatar_amd import ops, sp, synthetic
+    from stableavatar_amd.transformer import WanTransformer3DFantasyModel, param_shapes
+    dev = "cuda"
+    cfg = dict(DIT_FULL, num_layers=2)
+    m = WanTransformer3DFantasyModel(**cfg)
+    m.load_state_dict(synthetic.fill_state_dict(param_shapes(cfg), 61))
+    m = m.to(dev)
+    sp._p2p = lambda sends, recvs, group: sp.Pending(None)
+    sp.gather_tokens = lambda local, B, Lc, world, group=None: torch.zeros(B * world * Lc, local.shape[1],
+                                                                             device=local.device, dtype=local.dtype)
+    m.sp_group, m.sp_world_size, m.sp_world_rank, m._sp_enabled = None, 8, 5, True
+    g = torch.Generator(device=dev).manual_seed(0)
+    lat = torch.randn(1, 16, 21, 64, 64, device=dev, generator=g).bfloat16()
+    y = torch.randn(3, 20, 21, 64, 64, device=dev, generator=g).bfloat16()
+    ctx = [torch.randn(n, 4096, device=dev, generator=g) for n in (120, 120, 60)]
+    clip = torch.randn(3, 257, 1280, device=dev, generator=g)
+    voc = torch.randn(3, 167, 768, device=dev, generator=g)
+    t = torch.tensor([990.0], device=dev)
+    res = []
+    with torch.no_grad():
+        for ov in ("4", "0"):
+            os.environ["SA_SP_OVERLAP"] = ov
+            outs = []
+            for split in ("0", "1"):
+                os.environ["SA_ATTN_SPLIT"] = split
+                m.forward_window(lat, 0, True, 3, t, ctx, 21504, clip, y, voc, 81)  # builds the exchange
+                ex = m._sp_ex[1]
+                gb = torch.Generator(device=dev).manual_seed(1)
+                for buf in (ex.q, ex.kv, ex.obuf):
+                    buf.normal_(generator=gb)
+                m.forward_window(lat, 0, True, 3, t, ctx, 21504, clip, y, voc, 81)
+                # this rank's residual stream after the blocks (the stubbed all-gather returns zeros for the output)
+                outs.append(next(iter(m._ws.values())).x.clone())
+            torch.cuda.synchronize()
+            n_split = ops.attn_tail_split(0, 3 * 3 * 42, torch.device(dev))
+            a, b = outs[0].double(), outs[1].double()  # stubbed transfers: large values, norms in fp64
+            rel = ((b - a).norm() / a.norm()).item()
+            res.append((ov, rel, bool(torch.isfinite(outs[1]).all()), n_split, bool(torch.isfinite(outs[0]).all())))
+    qret.put(res)
+
+
+@pytest.mark.timeout(400)
+def test_sp_rank_attention_key_split_n8_shape():
+    ctx = mp.get_context("spawn")
+    qret = ctx.Queue()
+    p = ctx.Process(target=_split_rank_worker, args=(qret,))
+    p.start()
+    res = collect([p], qret, 1, timeout=360)[0]
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    for ov, rel, finite, n_split, finite0 in res:
+        print(f"N = 8 rank shape, schedule {ov}: key-split tail ({n_split} tiles) vs unsplit rel {rel:.2e} "
+              f"(finite: split {finite}, unsplit {finite0})")
+        assert finite and finite0 and rel < 5e-3, (ov, rel)
