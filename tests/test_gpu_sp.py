@@ -215,6 +215,60 @@ def test_sp_rccl_path_degree1(overlap):
         assert same, (case, loop, err)
 
 
+def _rccl_shared_rows_worker(port, qret):
+    """the CFG rows' shared first block on RCCL (degree 1, loopback): row 0's Q/K/V and head outputs through real
+    P2P ops, in the one-stream and per-row-stream schedules, vs the single-GPU forward computing every row"""
+    import torch.distributed as dist
+    sys.path.insert(0, HERE)
+    from test_gpu_dit import make_model
+    from golden_cases import DIT_SMALL
+    from stableavatar_amd import synthetic
+    from stableavatar_amd.pipeline import WanI2VTalkingInferenceLongPipeline
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method="file://" + port, rank=0, world_size=1,
+                            device_id=torch.device("cuda:0"))
+    try:
+        m = make_model(DIT_SMALL)
+        dev = "cuda"
+        lat = synthetic.seeded_normal((1, 16, 5, 8, 8), 501).to(dev).bfloat16()
+        y = WanI2VTalkingInferenceLongPipeline.mask_latents(synthetic.seeded_normal((1, 16, 5, 8, 8), 502).to(dev),
+                                                            17).bfloat16()
+        ctx = [synthetic.seeded_normal((20, 64), 503).to(dev)] * 2 + [synthetic.seeded_normal((25, 64), 504).to(dev)]
+        clip = synthetic.seeded_normal((1, 257, 1280), 505).expand(3, -1, -1).contiguous().to(dev)
+        a = synthetic.seeded_normal((1, 39, 768), 506).to(dev)
+        voc = torch.cat([torch.zeros_like(a), a, a])
+        t = torch.tensor([937.5], device=dev)
+
+        def fwd(shared):
+            with torch.no_grad():
+                o = m.forward_window(lat, 0, True, 3, t, ctx, 80, clip, y, voc, 17, shared_rows=shared).float()
+            torch.cuda.synchronize()
+            return o.cpu()
+        m.disable_multi_gpus_inference()
+        single = fwd(False)
+        m.enable_multi_gpus_inference(loopback=True)
+        res = []
+        for ov in ("0", "4"):
+            os.environ["SA_SP_OVERLAP"] = ov
+            res.append((ov, torch.equal(fwd(True), single)))
+        qret.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sp_rccl_shared_rows_degree1():
+    ctx = mp.get_context("spawn")
+    qret = ctx.Queue()
+    p = ctx.Process(target=_rccl_shared_rows_worker, args=(_rendezvous_file(), qret))
+    p.start()
+    res = collect([p], qret, 1)[0]
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    for ov, same in res:
+        print(f"RCCL degree 1 loopback, shared first block, overlap {ov}: bit-identical {same}")
+        assert same, ov
+
+
 def _rccl_fullsize_worker(port, overlap, qret):
     """config-2 size on the RCCL transport: a 1-layer full-width 1.3B DiT (dim 1536, 12 heads, ffn 8960) at the
     512^2 x 81f shape (L = 21 504 tokens, B = 3 CFG rows), Ulysses at degree 1 with loopback transfers (every Q/K/V
