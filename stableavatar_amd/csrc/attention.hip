@@ -50,7 +50,10 @@ constexpr int LDS_BYTES = 2 * STAGE_BYTES;   // 64 KB
 // transposed (ds_read_b64_tr_b16) reads (cdna_hip_programming.md T10 form (b))
 __device__ __forceinline__ int gsw(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 
-constexpr float RESCALE_THR = 8.0f;  // log2 units: P <= 2^8 between rescales
+constexpr float RESCALE_THR = 8.0f;  // log2 units: P <= 2^8 between rescales (fused cross-attention)
+// self-attention blocks (v6_softmax_p): the running max sits RESCALE_BIAS above the rows' maxima after each move, and
+// the next move comes when a score passes its row's maximum by RESCALE_BIAS + 1 = RESCALE_THR
+constexpr float RESCALE_BIAS = RESCALE_THR - 1.0f;
 
 // non-canonicalising f32 max (MFMA outputs are never signalling NaNs): fmaxf makes hipcc insert a
 // v_max_f32 x, x canonicalisation per operand (MI355X_MICROARCH.md, App. B attention pitfalls).  The
@@ -474,23 +477,72 @@ __device__ __forceinline__ float rowmax64(const f32x4 (&S)[4][2], int qt) {
   return vmax2(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 
-// max over this lane's 32 scores (both query tiles), as a 3-ary tree (depth 4 instead of a 16-long chain)
-__device__ __forceinline__ float lanemax32(const f32x4 (&S)[4][2]) {
-  float v[32];
+// P = bf16(exp2(S)) of a block in PV operand order (pb[c][qt]: key tiles 2c, 2c+1 of query tile qt); S is kept
+__device__ __forceinline__ void v6_pack_exp(const f32x4 (&S)[4][2], bf16x8 (&pb)[2][2]) {
 #pragma unroll
-  for (int kt = 0; kt < 4; ++kt)
+  for (int c = 0; c < 2; ++c)
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[kt * 8 + qt * 4 + i] = S[kt][qt][i];
-  float r[12];
+      for (int j = 0; j < 4; ++j) {
+        pb[c][qt][j] = f2bf(__builtin_amdgcn_exp2f(S[2 * c][qt][j]));
+        pb[c][qt][4 + j] = f2bf(__builtin_amdgcn_exp2f(S[2 * c + 1][qt][j]));
+      }
+}
+
+// The online-softmax step of one 64-key block (attn_v6_block, attn_v6t_block): P into pb, the running max moved
+// first where needed.  The running max is kept RESCALE_BIAS log2 units above the rows' maxima (P <= 2^-7 right after
+// a move), and the test runs on the bf16 P: some P >= 2 -- a score 8 above its row's maximum -- iff bit 14 of some
+// packed P is set (P >= 0: biased exponent >= 128), so the OR of the 16 P dwords (8 v_or3) decides, where a max tree
+// over the 32 scores took 16 ops (6.08-6.18 vs 6.19-6.22 ms per config-2 launch).  The first block, or a failed test,
+// moves the running max of every row whose block maximum passes it, rescales O and L and forms P again from S.
+template <bool FIRST_CT>
+__device__ __forceinline__ void v6_softmax_p(V6State& st, f32x4 (&S)[4][2], bf16x8 (&pb)[2][2], bool first_rt) {
+  const bool FIRST = FIRST_CT || first_rt;
+  bool move = FIRST;
+  if (!FIRST) {
+    v6_pack_exp(S, pb);
+    u32x4 w[4];
 #pragma unroll
-  for (int j = 0; j < 10; ++j) r[j] = vmax3(v[3 * j], v[3 * j + 1], v[3 * j + 2]);
-  r[10] = v[30];
-  r[11] = v[31];
-  const float a = vmax3(r[0], r[1], r[2]), b = vmax3(r[3], r[4], r[5]), c = vmax3(r[6], r[7], r[8]),
-              d = vmax3(r[9], r[10], r[11]);
-  return vmax2(vmax3(a, b, c), d);
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) w[2 * c + qt] = __builtin_bit_cast(u32x4, pb[c][qt]);
+    uint32_t acc = w[0][0] | w[0][1] | w[0][2];
+    acc = acc | w[0][3] | w[1][0];
+    acc = acc | w[1][1] | w[1][2];
+    acc = acc | w[1][3] | w[2][0];
+    acc = acc | w[2][1] | w[2][2];
+    acc = acc | w[2][3] | w[3][0];
+    acc = acc | w[3][1] | w[3][2];
+    acc = acc | w[3][3];
+    move = !__all((acc & 0x40004000u) == 0u);  // wave-uniform
+  }
+  if (move) {
+    float mx[2], alpha[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) mx[qt] = rowmax64(S, qt);  // max of c S - m over the block's 64 keys
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const float delta = FIRST ? mx[qt] + RESCALE_BIAS : fmaxf(mx[qt] + RESCALE_BIAS, 0.f);
+      alpha[qt] = __builtin_amdgcn_exp2f(-delta);
+      st.negm[qt] -= delta;
+      st.negm4[qt] = (f32x4){st.negm[qt], st.negm[qt], st.negm[qt], st.negm[qt]};
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) S[kt][qt][i] -= delta;
+    }
+    if (!FIRST)  // O and L are still zero on the first block (no 0 x inf for a very negative max)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        st.L[qt] *= alpha[qt];
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) st.O[dt][qt][i] *= alpha[qt];
+      }
+    v6_pack_exp(S, pb);
+  }
 }
 
 // one 64-key block whose K / V stages sit at KOFF / VOFF from the read bases (self-attention: K and V of a
@@ -501,7 +553,6 @@ template <int KOFF, int VOFF, bool FIRST_CT>
 __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2][4], const uint32_t* ka,
                                               const uint32_t* va, int kb, int kv_len, int g,
                                               bool first_rt = false) {
-  const bool FIRST = FIRST_CT || first_rt;
   f32x4 S[4][2];
 #pragma unroll
   for (int kt = 0; kt < 4; ++kt)
@@ -534,70 +585,30 @@ __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2]
       for (int i = 0; i < 4; ++i)
         if (kb * KVB + kt * 16 + 4 * g + i >= kv_len) { S[kt][0][i] = -INFINITY; S[kt][1][i] = -INFINITY; }
   }
-  // the rescale test needs no row reduction: some row's max exceeds the threshold iff some lane's max
-  // over its 32 scores does (16 v_max3 and one compare per block instead of two row-max trees with their
-  // lane swaps: 6.59 vs 6.77 ms per config-2 launch, bit-identical); the rows' maxima are formed only on
-  // the (rare) rescale path
-  // the first block (peeled: FIRST) always sets the running max
-  if (FIRST || !__all(lanemax32(S) <= RESCALE_THR)) {  // wave-uniform
-    float mx[2];
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) mx[qt] = rowmax64(S, qt);  // max of c S - m over the block's 64 keys
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const float delta = FIRST ? mx[qt] : fmaxf(mx[qt], 0.f);
-      if (!FIRST) {  // O and L are still zero on the first block (no 0 x inf for a very negative max)
-        const float alpha = __builtin_amdgcn_exp2f(-delta);
-        st.L[qt] *= alpha;
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) st.O[dt][qt][i] *= alpha;
-      }
-      st.negm[qt] -= delta;
-      st.negm4[qt] = (f32x4){st.negm[qt], st.negm[qt], st.negm[qt], st.negm[qt]};
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) S[kt][qt][i] -= delta;
-    }
-  }
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) S[kt][qt][i] = __builtin_amdgcn_exp2f(S[kt][qt][i]);
+  bf16x8 pb[2][2];
+  v6_softmax_p<FIRST_CT>(st, S, pb, first_rt);
   // O^T += V^T P^T, key chunk c = tiles (2c, 2c+1)
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
-    bf16x8 pb[2];
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        pb[qt][j] = f2bf(S[2 * c][qt][j]);
-        pb[qt][4 + j] = f2bf(S[2 * c + 1][qt][j]);
-      }
     {
       bf16x8 ones;
 #pragma unroll
       for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
-      st.L[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[0], st.L[0], 0, 0, 0);
-      st.L[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[1], st.L[1], 0, 0, 0);
+      st.L[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[c][0], st.L[0], 0, 0, 0);
+      st.L[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[c][1], st.L[1], 0, 0, 0);
     }
     if (c == 0) {
       wait_v<8>(v0);
-      v6_mma_v(st.O, 0, v0, pb);
+      v6_mma_v(st.O, 0, v0, pb[c]);
       v6_read_v<VOFF, 1, 0>(v0, va);
       wait_v<8>(v1);
-      v6_mma_v(st.O, 4, v1, pb);
+      v6_mma_v(st.O, 4, v1, pb[c]);
       v6_read_v<VOFF, 1, 4>(v1, va);
     } else {
       wait_v<8>(v0);
-      v6_mma_v(st.O, 0, v0, pb);
+      v6_mma_v(st.O, 0, v0, pb[c]);
       wait_v<0>(v1);
-      v6_mma_v(st.O, 4, v1, pb);
+      v6_mma_v(st.O, 4, v1, pb[c]);
     }
   }
 }
@@ -622,37 +633,6 @@ __device__ __forceinline__ void v6t_mma_v(f32x4 (&O)[8][2], int dt0, const u32x4
     O[dt0 + t][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb[0], O[dt0 + t][0], 0, 0, 0);
     O[dt0 + t][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb[1], O[dt0 + t][1], 0, 0, 0);
   }
-}
-
-// the rescale of attn_v6_block (shared by the V^T forms): some row's max above the threshold (or the first block)
-// -> move the running max; ORESCALE(alpha[2]) rescales the output accumulators
-template <bool FIRST, class ORescale>
-__device__ __forceinline__ void v6_softmax_rescale(f32x4 (&S)[4][2], f32x4 (&L)[2], float (&negm)[2], f32x4 (&negm4)[2],
-                                                   ORescale orescale) {
-  if (FIRST || !__all(lanemax32(S) <= RESCALE_THR)) {  // wave-uniform
-    float mx[2], alpha[2];
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) mx[qt] = rowmax64(S, qt);
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const float delta = FIRST ? mx[qt] : fmaxf(mx[qt], 0.f);
-      alpha[qt] = __builtin_amdgcn_exp2f(-delta);
-      if (!FIRST) L[qt] *= alpha[qt];
-      negm[qt] -= delta;
-      negm4[qt] = (f32x4){negm[qt], negm[qt], negm[qt], negm[qt]};
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) S[kt][qt][i] -= delta;
-    }
-    if (!FIRST) orescale(alpha);
-  }
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) S[kt][qt][i] = __builtin_amdgcn_exp2f(S[kt][qt][i]);
 }
 
 template <int KOFF>
@@ -696,43 +676,29 @@ __device__ __forceinline__ void attn_v6t_block(V6State& st, const bf16x8 (&qf)[2
   v6t_read_v<VOFF, 0, 0>(v0, vb);
   v6t_read_v<VOFF, 0, 4>(v1, vb);
   v6_tail_mask(S, kb, kv_len, g);
-  v6_softmax_rescale<FIRST>(S, st.L, st.negm, st.negm4, [&](const float (&al)[2]) {
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) st.O[dt][qt][i] *= al[qt];
-  });
+  bf16x8 pb[2][2];
+  v6_softmax_p<FIRST>(st, S, pb, false);
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
-    bf16x8 pb[2];
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        pb[qt][j] = f2bf(S[2 * c][qt][j]);
-        pb[qt][4 + j] = f2bf(S[2 * c + 1][qt][j]);
-      }
     {
       bf16x8 ones;
 #pragma unroll
       for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
-      st.L[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[0], st.L[0], 0, 0, 0);
-      st.L[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[1], st.L[1], 0, 0, 0);
+      st.L[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[c][0], st.L[0], 0, 0, 0);
+      st.L[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[c][1], st.L[1], 0, 0, 0);
     }
     if (c == 0) {
       wait_k4<4>(v0);
-      v6t_mma_v(st.O, 0, v0, pb);
+      v6t_mma_v(st.O, 0, v0, pb[c]);
       v6t_read_v<VOFF, 1, 0>(v0, vb);
       wait_k4<4>(v1);
-      v6t_mma_v(st.O, 4, v1, pb);
+      v6t_mma_v(st.O, 4, v1, pb[c]);
       v6t_read_v<VOFF, 1, 4>(v1, vb);
     } else {
       wait_k4<4>(v0);
-      v6t_mma_v(st.O, 0, v0, pb);
+      v6t_mma_v(st.O, 0, v0, pb[c]);
       wait_k4<0>(v1);
-      v6t_mma_v(st.O, 4, v1, pb);
+      v6t_mma_v(st.O, 4, v1, pb[c]);
     }
   }
 }
