@@ -477,6 +477,61 @@ __device__ __forceinline__ float rowmax64(const f32x4 (&S)[4][2], int qt) {
   return vmax2(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 
+// max over this lane's 32 scores (both query tiles), as a 3-ary tree (depth 4 instead of a 16-long chain)
+__device__ __forceinline__ float lanemax32(const f32x4 (&S)[4][2]) {
+  float v[32];
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[kt * 8 + qt * 4 + i] = S[kt][qt][i];
+  float r[12];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) r[j] = vmax3(v[3 * j], v[3 * j + 1], v[3 * j + 2]);
+  r[10] = v[30];
+  r[11] = v[31];
+  const float a = vmax3(r[0], r[1], r[2]), b = vmax3(r[3], r[4], r[5]), c = vmax3(r[6], r[7], r[8]),
+              d = vmax3(r[9], r[10], r[11]);
+  return vmax2(vmax3(a, b, c), d);
+}
+
+// the fused cross-attention's softmax step (attn_v6_block<.., false>): the rescale test on the scores (a lane max
+// over its 32 scores against RESCALE_THR, no row reduction unless it fails), the exponentials in place in S.  It
+// keeps the cross-attention kernels inside 256 VGPRs with the fewest spills (the P-side test of v6_softmax_p holds
+// the scores and the packed P of the whole block at once)
+__device__ __forceinline__ void v6_softmax_s(V6State& st, f32x4 (&S)[4][2], const bool FIRST) {
+  if (FIRST || !__all(lanemax32(S) <= RESCALE_THR)) {  // wave-uniform
+    float mx[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) mx[qt] = rowmax64(S, qt);  // max of c S - m over the block's 64 keys
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const float delta = FIRST ? mx[qt] : fmaxf(mx[qt], 0.f);
+      if (!FIRST) {  // O and L are still zero on the first block (no 0 x inf for a very negative max)
+        const float alpha = __builtin_amdgcn_exp2f(-delta);
+        st.L[qt] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) st.O[dt][qt][i] *= alpha;
+      }
+      st.negm[qt] -= delta;
+      st.negm4[qt] = (f32x4){st.negm[qt], st.negm[qt], st.negm[qt], st.negm[qt]};
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) S[kt][qt][i] -= delta;
+    }
+  }
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) S[kt][qt][i] = __builtin_amdgcn_exp2f(S[kt][qt][i]);
+}
+
 // P = bf16(exp2(S)) of a block in PV operand order (pb[c][qt]: key tiles 2c, 2c+1 of query tile qt); S is kept
 __device__ __forceinline__ void v6_pack_exp(const f32x4 (&S)[4][2], bf16x8 (&pb)[2][2]) {
 #pragma unroll
@@ -549,7 +604,7 @@ __device__ __forceinline__ void v6_softmax_p(V6State& st, f32x4 (&S)[4][2], bf16
 // stage adjacent in a 2-stage ring; the fused cross-attention: separate 3-stage K and V regions).  The first
 // block of a softmax sets the running max: FIRST_CT at compile time (self-attention), first_rt per source
 // (cross-attention)
-template <int KOFF, int VOFF, bool FIRST_CT>
+template <int KOFF, int VOFF, bool FIRST_CT, bool PTEST = true>
 __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2][4], const uint32_t* ka,
                                               const uint32_t* va, int kb, int kv_len, int g,
                                               bool first_rt = false) {
@@ -585,11 +640,22 @@ __device__ __forceinline__ void attn_v6_block(V6State& st, const bf16x8 (&qf)[2]
       for (int i = 0; i < 4; ++i)
         if (kb * KVB + kt * 16 + 4 * g + i >= kv_len) { S[kt][0][i] = -INFINITY; S[kt][1][i] = -INFINITY; }
   }
+  // PTEST: the self-attention kernels' step (P-side rescale test, P for the whole block); else the fused
+  // cross-attention's (v6_softmax_s: P formed per key chunk below)
   bf16x8 pb[2][2];
-  v6_softmax_p<FIRST_CT>(st, S, pb, first_rt);
+  if constexpr (PTEST) v6_softmax_p<FIRST_CT>(st, S, pb, first_rt);
+  else v6_softmax_s(st, S, FIRST_CT || first_rt);
   // O^T += V^T P^T, key chunk c = tiles (2c, 2c+1)
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
+    if constexpr (!PTEST)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pb[c][qt][j] = f2bf(S[2 * c][qt][j]);
+          pb[c][qt][4 + j] = f2bf(S[2 * c + 1][qt][j]);
+        }
     {
       bf16x8 ones;
 #pragma unroll
@@ -1302,7 +1368,7 @@ __device__ __forceinline__ void attn_cross3_body(const Cross3Args& a) {
     const int kb = src == 0 ? jj : (src == 1 ? jj - nT : jj - nT - nI);
     const int len = src == 0 ? a.t_len : (src == 1 ? a.i_len : a.nper);
     at_slot(jj % NST);
-    attn_v6_block<0, 0, false>(st, qf, kas, vas, kb, len, g, kb == 0);
+    attn_v6_block<0, 0, false, false>(st, qf, kas, vas, kb, len, g, kb == 0);
     if (jj == nT - 1 || jj == nT + nI - 1 || jj == ntot - 1) finish(src);
   };
   // the vocal stream's single block when a frame has at most 32 audio tokens (StableAvatar: 32), and the image
